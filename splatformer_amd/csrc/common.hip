@@ -1,0 +1,157 @@
+// Error plumbing + generic device primitives (scan) shared by every stage.
+#include "common.h"
+
+#include <cstring>
+
+namespace sfx {
+
+static thread_local char g_err[1024] = {0};
+
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+void clear_error() { g_err[0] = 0; }
+
+}  // namespace sfx
+
+// ---------------------------------------------------------------------------
+// Inclusive / exclusive int32 scan, three launches: per-block scan (1024 items
+// per 256-thread block), a single-workgroup scan of the block totals, then an
+// offset add.  Used for cum_tiles_hit (gsplat's torch.cumsum(num_tiles_hit,
+// dtype=int32)) and every histogram/run-length offset in the library.
+// ---------------------------------------------------------------------------
+namespace {
+
+constexpr int SCAN_THREADS = 256;
+constexpr int SCAN_ITEMS = 4;
+constexpr int SCAN_TILE = SCAN_THREADS * SCAN_ITEMS;
+
+template <typename T>
+__device__ T block_exclusive_scan(T v, T* smem, T* total) {
+  // smem: SCAN_THREADS/64 entries of wave totals
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  T x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    T y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) smem[wid] = x;
+  __syncthreads();
+  T wave_off = 0, tot = 0;
+  for (int w = 0; w < SCAN_THREADS / 64; ++w) {
+    T s = smem[w];
+    if (w < wid) wave_off += s;
+    tot += s;
+  }
+  __syncthreads();
+  *total = tot;
+  return wave_off + x - v;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(SCAN_THREADS) scan_tiles(const T* __restrict__ in, T* __restrict__ out,
+                                                           T* __restrict__ tile_sums, long long n, int inclusive) {
+  __shared__ T smem[SCAN_THREADS / 64];
+  const long long base = (long long)blockIdx.x * SCAN_TILE + (long long)threadIdx.x * SCAN_ITEMS;
+  T v[SCAN_ITEMS];
+  T s = 0;
+#pragma unroll
+  for (int i = 0; i < SCAN_ITEMS; ++i) {
+    v[i] = (base + i < n) ? in[base + i] : (T)0;
+    s += v[i];
+  }
+  T total;
+  T excl = block_exclusive_scan<T>(s, smem, &total);
+  T run = excl;
+#pragma unroll
+  for (int i = 0; i < SCAN_ITEMS; ++i) {
+    T nv = run + v[i];
+    if (base + i < n) out[base + i] = inclusive ? nv : run;
+    run = nv;
+  }
+  if (threadIdx.x == 0 && tile_sums) tile_sums[blockIdx.x] = total;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(SCAN_THREADS) scan_single(T* __restrict__ data, long long n, T* __restrict__ grand) {
+  // exclusive scan of `data` in place, one workgroup, chunked.
+  __shared__ T smem[SCAN_THREADS / 64];
+  T carry = 0;
+  for (long long start = 0; start < n; start += SCAN_TILE) {
+    const long long base = start + (long long)threadIdx.x * SCAN_ITEMS;
+    T v[SCAN_ITEMS];
+    T s = 0;
+#pragma unroll
+    for (int i = 0; i < SCAN_ITEMS; ++i) {
+      v[i] = (base + i < n) ? data[base + i] : (T)0;
+      s += v[i];
+    }
+    T total;
+    T excl = block_exclusive_scan<T>(s, smem, &total);
+    T run = carry + excl;
+#pragma unroll
+    for (int i = 0; i < SCAN_ITEMS; ++i) {
+      if (base + i < n) data[base + i] = run;
+      run += v[i];
+    }
+    carry += total;
+  }
+  if (threadIdx.x == 0 && grand) *grand = carry;
+}
+
+template <typename T>
+__global__ void add_tile_offsets(T* __restrict__ out, const T* __restrict__ tile_offs, long long n) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] += tile_offs[i / SCAN_TILE];
+}
+
+template <typename T>
+int scan_impl(long long n, const T* in, T* out, int inclusive, void* ws, size_t ws_bytes, T* total, hipStream_t st) {
+  if (n == 0) {
+    if (total) hipMemsetAsync(total, 0, sizeof(T), st);
+    return sfx::check_launch("scan");
+  }
+  const long long tiles = (n + SCAN_TILE - 1) / SCAN_TILE;
+  if (ws_bytes < (size_t)tiles * sizeof(T)) {
+    sfx::set_error("scan: workspace too small (%zu < %zu)", ws_bytes, (size_t)tiles * sizeof(T));
+    return SFX_ERR_WORKSPACE;
+  }
+  T* sums = reinterpret_cast<T*>(ws);
+  scan_tiles<T><<<(unsigned)tiles, SCAN_THREADS, 0, st>>>(in, out, sums, n, inclusive);
+  scan_single<T><<<1, SCAN_THREADS, 0, st>>>(sums, tiles, total);
+  if (tiles > 1) add_tile_offsets<T><<<sfx::ceil_div(n, 256), 256, 0, st>>>(out, sums, n);
+  return sfx::check_launch("scan");
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* sfx_last_error(void) { return sfx::g_err; }
+
+int sfx_abi_version(void) { return 1; }
+
+size_t sfx_scan_workspace_bytes(long long n) {
+  const long long tiles = (n + SCAN_TILE - 1) / SCAN_TILE;
+  return (size_t)(tiles > 0 ? tiles : 1) * sizeof(long long);
+}
+
+int sfx_scan_i32(long long n, const int32_t* in, int32_t* out, int inclusive, void* ws, size_t ws_bytes,
+                 int32_t* total, void* stream) {
+  SFX_REQUIRE(n >= 0, "sfx_scan_i32: n < 0");
+  SFX_REQUIRE(n == 0 || (in && out), "sfx_scan_i32: null buffer");
+  return scan_impl<int32_t>(n, in, out, inclusive, ws, ws_bytes, total, sfx::as_stream(stream));
+}
+
+int sfx_scan_i64(long long n, const int64_t* in, int64_t* out, int inclusive, void* ws, size_t ws_bytes,
+                 int64_t* total, void* stream) {
+  SFX_REQUIRE(n >= 0, "sfx_scan_i64: n < 0");
+  SFX_REQUIRE(n == 0 || (in && out), "sfx_scan_i64: null buffer");
+  return scan_impl<int64_t>(n, in, out, inclusive, ws, ws_bytes, total, sfx::as_stream(stream));
+}
+
+}  // extern "C"

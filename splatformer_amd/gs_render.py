@@ -1,0 +1,143 @@
+"""Render glue: mirror of reference utils/gs_utils.py:12-114.
+
+`rasterize_gaussians_to_singleimg` / `rasterize_gaussians_to_multiimgs` keep the
+reference signatures (gs_utils.py:20, :29).  Two device paths, both HIP:
+
+* eval (no autograd needed): one fused kernel `sfx_render_prep_project`
+  (viewmat, exp/normalise/sigmoid, SH, EWA projection) followed by the
+  device scan / radix sort / tile rasterizer -- no torch elementwise ops and
+  no `.item()` on the camera (intrinsics are taken as host scalars).
+* training (params require grad): the reference's torch glue around the
+  autograd Functions of `gsplat_compat` so gradients flow to the refined
+  Gaussians (reference train.py:273-289).
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Tuple
+
+import torch
+from torch import Tensor
+
+from . import _lib
+from ._lib import call, ptr, stream
+from .gsplat_compat import (_RasterizeGaussians, bin_and_sort_gaussians, compute_cumulative_intersects,
+                            project_gaussians, rasterize_gaussians, spherical_harmonics)
+
+BLOCK_WIDTH = 16
+C0 = 0.28209479177387814
+
+
+def SH2RGB(sh):
+    return sh * C0 + 0.5
+
+
+def RGB2SH(rgb):
+    return (rgb - 0.5) / C0
+
+
+def _scalar(x) -> float:
+    return float(x.item()) if isinstance(x, Tensor) else float(x)
+
+
+def rasterize_gaussians_to_multiimgs(gs_params: Dict[str, Tensor], cameras: Dict) -> Tuple[List[Tensor], List[Tensor]]:
+    """gs_utils.py:20-27: render every camera_to_world of `cameras` sequentially."""
+    rgbs, alphas = [], []
+    for camera_to_world in cameras["camera_to_worlds"]:
+        rgb, alpha = rasterize_gaussians_to_singleimg(gs_params, camera_to_world, **cameras)
+        rgbs.append(rgb)
+        alphas.append(alpha)
+    return rgbs, alphas
+
+
+def _needs_grad(gs_params) -> bool:
+    return torch.is_grad_enabled() and any(isinstance(v, Tensor) and v.requires_grad for v in gs_params.values())
+
+
+def rasterize_gaussians_to_singleimg(gs_params, camera_to_world, cx, cy, fx, fy, width, height, background_color,
+                                     **kwargs):
+    """gs_utils.py:29-114 -> (rgb [H,W,3] clamped <= 1, alpha [H,W,1])."""
+    gs_params = {k: v.float() if v.dtype == torch.half else v for k, v in gs_params.items()}
+    if "opacities" not in gs_params and "opacities_sigmoid" not in gs_params:
+        raise ValueError("No opacities found in gs_params")
+    H, W = int(_scalar(height)), int(_scalar(width))
+    fx, fy, cx, cy = _scalar(fx), _scalar(fy), _scalar(cx), _scalar(cy)
+    if _needs_grad(gs_params) or "opacities_sigmoid" in gs_params:
+        return _render_autograd(gs_params, camera_to_world, cx, cy, fx, fy, W, H, background_color)
+    return _render_fused(gs_params, camera_to_world, cx, cy, fx, fy, W, H, background_color)
+
+
+def _render_fused(gs, c2w, cx, cy, fx, fy, W, H, background):
+    means = gs["means"].contiguous()
+    _lib.require_gpu(means)
+    dev = means.device
+    n = means.shape[0]
+    dc = gs["features_dc"].contiguous()
+    rest = gs.get("features_rest")
+    nb = 1 + (rest.shape[1] if rest is not None else 0)
+    if rest is not None:
+        rest = rest.contiguous()
+    c2w = c2w.detach().float().contiguous()
+    f = lambda *s, dt=torch.float32: torch.empty(*s, device=dev, dtype=dt)
+    viewmat, rgbs, opac = f(3, 4), f(n, 3), f(n, 1)
+    xys, depths, radii, conics, tiles = f(n, 2), f(n), f(n, dt=torch.int32), f(n, 3), f(n, dt=torch.int32)
+    call("sfx_render_prep_project", n, nb, ptr(means), ptr(gs["scales"].contiguous()), ptr(gs["quats"].contiguous()),
+         ptr(gs["opacities"].contiguous()), ptr(dc), ptr(rest), ptr(c2w), fx, fy, cx, cy, H, W, BLOCK_WIDTH,
+         ptr(viewmat), ptr(rgbs), ptr(opac), ptr(xys), ptr(depths), ptr(radii), ptr(conics), ptr(tiles), stream())
+    bg = background.to(device=dev, dtype=torch.float32).contiguous()
+    rgb, alpha = _RasterizeGaussians.apply(xys, depths, radii, conics, tiles, rgbs, opac, H, W, BLOCK_WIDTH, bg, True)
+    rgb = torch.clamp(rgb, max=1.0)
+    return rgb, alpha.unsqueeze(-1)
+
+
+def _render_autograd(gs_params, camera_to_world, cx, cy, fx, fy, W, H, background_color):
+    """Line-for-line the reference glue (gs_utils.py:32-112) over the HIP autograd ops."""
+    R = camera_to_world[:3, :3]
+    T = camera_to_world[:3, 3:4]
+    R_edit = torch.diag(torch.tensor([1, -1, -1], device=R.device, dtype=R.dtype))
+    R = R @ R_edit
+    R_inv = R.T
+    T_inv = -R_inv @ T
+    viewmat = torch.eye(4, device=R.device, dtype=R.dtype)
+    viewmat[:3, :3] = R_inv
+    viewmat[:3, 3:4] = T_inv
+    means = gs_params["means"]
+    scales = torch.exp(gs_params["scales"])
+    quats = gs_params["quats"] / torch.norm(gs_params["quats"], dim=-1, keepdim=True)
+    mask = (quats.norm(dim=-1) - 1) < 1e-6
+    inv_mask = ~mask
+    if inv_mask.any():
+        quats = quats.clone()
+        quats[inv_mask] = torch.tensor([0, 0, 0, 1.0], device=quats.device)
+    if "opacities" in gs_params:
+        opacities = torch.sigmoid(gs_params["opacities"])
+    else:
+        opacities = gs_params["opacities_sigmoid"]
+    if "features_rest" in gs_params:
+        colors = torch.cat([gs_params["features_dc"].unsqueeze(1), gs_params["features_rest"]], dim=1)
+    else:
+        colors = gs_params["features_dc"].unsqueeze(1)
+    n = int(math.sqrt(colors.shape[1]) - 1)
+    if n == 0:
+        rgbs = torch.sigmoid(colors[:, 0, :])
+    else:
+        viewdirs_ = means.detach() - camera_to_world.detach()[:3, 3]
+        viewdirs_norm = viewdirs_.norm(dim=-1, keepdim=True)
+        viewdirs = viewdirs_ / viewdirs_norm
+        bad = (viewdirs_norm == 0).squeeze(-1)
+        if bool(bad.any()):
+            viewdirs = viewdirs.clone()
+            viewdirs[bad] = torch.tensor([0.0, 0.0, 1.0], device=viewdirs.device)
+        rgbs = spherical_harmonics(n, viewdirs, colors)
+        rgbs = torch.clamp(rgbs + 0.5, min=0.0)
+    xys, depths, radii, conics, comp, num_tiles_hit, cov3d = project_gaussians(
+        means, scales, 1, quats, viewmat.squeeze()[:3, :].float(), fx, fy, cx, cy, H, W, BLOCK_WIDTH)
+    rgb, alpha = rasterize_gaussians(xys, depths, radii, conics, num_tiles_hit, rgbs, opacities, H, W, BLOCK_WIDTH,
+                                     background=background_color, return_alpha=True)
+    rgb = torch.clamp(rgb, max=1.0)
+    alpha = alpha.unsqueeze(-1)
+    return rgb, alpha
+
+
+__all__ = ["rasterize_gaussians_to_multiimgs", "rasterize_gaussians_to_singleimg", "BLOCK_WIDTH", "SH2RGB", "RGB2SH",
+           "bin_and_sort_gaussians", "compute_cumulative_intersects"]

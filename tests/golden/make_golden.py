@@ -1,0 +1,198 @@
+"""Capture golden vectors from the reference's own glue code (run in the build
+container only; /root/reference does not exist on the GPU box).
+
+The reference's Python glue imports with stub modules for its absent
+dependencies (gin, cv2, plyfile, torch_scatter, gsplat, pointcept), see
+SURVEY.md §8(c).  We then run:
+
+1. `utils/gs_utils.py:rasterize_gaussians_to_singleimg` with a *recording*
+   gsplat stub: the arguments the glue hands to gsplat (viewmat, exp'd
+   scales, normalised/NaN-patched quats, sigmoid opacities, SH coeff layout,
+   viewdirs, clamp(+0.5) colours, H/W/fx/fy/cx/cy/block width, background)
+   are saved -- they pin the render glue (oracle/render_ref.py and the fused
+   HIP prep kernel).
+2. `models/feature_predictor.py:FeaturePredictor` (ptv3_base.gin head config,
+   zeroinit off so heads are non-trivial) with a recording stub backbone:
+   the backbone input dict (coord, grid_coord, offset, feat) and the refined
+   outputs for a fixed backbone feature pin batchify / grid_coord / heads /
+   residual / tanh semantics.
+
+Outputs: tests/golden/render_glue.npz, tests/golden/feature_predictor.npz
+(inputs and outputs only -- data, no reference source).
+"""
+from __future__ import annotations
+
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+
+REF = "/root/reference"
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+
+def install_stubs(recorder):
+    gin = types.ModuleType("gin")
+
+    def configurable(*a, **k):
+        if a and callable(a[0]):
+            return a[0]
+        return lambda f: f
+
+    gin.configurable = configurable
+    gin.external_configurable = lambda *a, **k: a[0]
+    sys.modules["gin"] = gin
+    for m in ["cv2", "torch_scatter"]:
+        sys.modules[m] = types.ModuleType(m)
+    ply = types.ModuleType("plyfile")
+    ply.PlyData = object
+    ply.PlyElement = object
+    sys.modules["plyfile"] = ply
+
+    gs = types.ModuleType("gsplat")
+
+    def spherical_harmonics(deg, viewdirs, coeffs):
+        recorder["sh"] = dict(deg=deg, viewdirs=viewdirs.clone(), coeffs=coeffs.clone())
+        from oracle import gsplat_ref
+        return gsplat_ref.spherical_harmonics(deg, viewdirs, coeffs)
+
+    def project_gaussians(*args):
+        names = ["means3d", "scales", "glob_scale", "quats", "viewmat", "fx", "fy", "cx", "cy", "img_height",
+                 "img_width", "block_width"]
+        recorder["project"] = {k: (v.clone() if isinstance(v, torch.Tensor) else v) for k, v in zip(names, args)}
+        from oracle import gsplat_ref
+        return gsplat_ref.project_gaussians(*args)
+
+    def rasterize_gaussians(xys, depths, radii, conics, num_tiles_hit, colors, opacity, H, W, bw, background=None,
+                            return_alpha=False):
+        recorder["raster"] = dict(colors=colors.clone(), opacity=opacity.clone(), H=H, W=W, bw=bw,
+                                  background=background.clone(), return_alpha=return_alpha)
+        from oracle import gsplat_ref
+        return gsplat_ref.rasterize_gaussians(xys, depths, radii, conics, num_tiles_hit, colors, opacity, H, W, bw,
+                                              background=background, return_alpha=return_alpha)
+
+    gs.spherical_harmonics = spherical_harmonics
+    gs.project_gaussians = project_gaussians
+    gs.rasterize_gaussians = rasterize_gaussians
+    sys.modules["gsplat"] = gs
+
+    # reference models/pointtransformer_v3.py needs pointcept/spconv: stub the module with a recording backbone
+    ptv3 = types.ModuleType("models.pointtransformer_v3")
+
+    class PointTransformerV3Model(torch.nn.Module):
+        output_dim = 96
+
+        def __init__(self, in_channels, additional_info=None, **kw):
+            super().__init__()
+            g = torch.Generator().manual_seed(1234)
+            self.proj = torch.nn.Parameter(torch.randn(in_channels + 3, 96, generator=g) * 0.3)
+
+        def forward(self, data_dict):
+            recorder["backbone_in"] = {k: (v.clone() if isinstance(v, torch.Tensor) else v)
+                                       for k, v in data_dict.items()}
+            x = torch.cat([data_dict["feat"], data_dict["grid_coord"].float() / 384.0], 1)
+            feat = torch.tanh(x @ self.proj)
+            recorder["backbone_out"] = feat.clone()
+            return {"feat": feat}
+
+    ptv3.PointTransformerV3Model = PointTransformerV3Model
+    sys.modules["models.pointtransformer_v3"] = ptv3
+    spc = types.ModuleType("models.spconv")
+    spc.SparseConvModel = object
+    sys.modules["models.spconv"] = spc
+
+
+def main():
+    rec = {}
+    sys.path.insert(0, os.path.dirname(os.path.dirname(OUT)))  # repo root (for oracle)
+    install_stubs(rec)
+    sys.path.insert(0, REF)
+    orig_tensor = torch.tensor
+
+    def tensor_cpu(*a, **k):  # gs_utils.py:35 hard-codes device='cuda'
+        if k.get("device") == "cuda":
+            k["device"] = "cpu"
+        return orig_tensor(*a, **k)
+
+    torch.tensor = tensor_cpu
+    import importlib
+    gs_utils = importlib.import_module("utils.gs_utils")
+    import models  # noqa: F401  (namespace package of the reference)
+    fp_mod = importlib.import_module("models.feature_predictor")
+    from splatformer_amd.scenes import make_cameras, make_scene
+
+    # ---- 1. render glue, SH degree 1 and 0 -----------------------------------
+    out = {}
+    for deg in (1, 0, 3):
+        s = make_scene(96, sh_degree=deg, seed=11 + deg)
+        s["quats"][5] = float("nan")   # exercise the NaN-quaternion patch (gs_utils.py:47-51)
+        cams = make_cameras(64, 48, n_views=2)
+        cams["background_color"] = orig_tensor([0.1, 0.2, 0.3])
+        c2w = cams["camera_to_worlds"][1]
+        rec.clear()
+        gs_utils.rasterize_gaussians_to_singleimg(
+            s, c2w, orig_tensor(cams["cx"]), orig_tensor(cams["cy"]), orig_tensor(cams["fx"]),
+            orig_tensor(cams["fy"]), orig_tensor(cams["width"]), orig_tensor(cams["height"]),
+            cams["background_color"])
+        p = f"deg{deg}_"
+        for k, v in s.items():
+            out[p + "in_" + k] = v.numpy()
+        out[p + "c2w"] = c2w.numpy()
+        out[p + "intr"] = np.array([cams["fx"], cams["fy"], cams["cx"], cams["cy"], cams["width"], cams["height"]],
+                                   dtype=np.float64)
+        out[p + "background"] = cams["background_color"].numpy()
+        pr = rec["project"]
+        out[p + "viewmat"] = pr["viewmat"].numpy()
+        out[p + "scales"] = pr["scales"].numpy()
+        out[p + "quats"] = pr["quats"].numpy()
+        out[p + "proj_scalars"] = np.array([pr["glob_scale"], pr["fx"], pr["fy"], pr["cx"], pr["cy"],
+                                            pr["img_height"], pr["img_width"], pr["block_width"]], dtype=np.float64)
+        out[p + "opacity"] = rec["raster"]["opacity"].numpy()
+        out[p + "colors"] = rec["raster"]["colors"].numpy()
+        if "sh" in rec:
+            out[p + "sh_deg"] = np.array(rec["sh"]["deg"])
+            out[p + "sh_viewdirs"] = rec["sh"]["viewdirs"].numpy()
+            out[p + "sh_coeffs"] = rec["sh"]["coeffs"].numpy()
+    np.savez_compressed(os.path.join(OUT, "render_glue.npz"), **out)
+
+    # ---- 2. FeaturePredictor (ptv3_base.gin head configuration) --------------
+    torch.manual_seed(0)
+    model = fp_mod.FeaturePredictor(
+        backbone_type="PT", sh_degree=1,
+        input_features=["means", "scales", "opacities", "quats", "features_dc", "features_rest"],
+        input_feat_to_mlp=True,
+        output_features=["means", "scales", "opacities", "quats", "features_dc", "features_rest"],
+        output_head_nlayer=4, output_head_type="mlp-relu", output_head_width=128, output_features_type="res",
+        res_feature_activation={"means": torch.nn.Tanh(), "features_dc": torch.nn.Identity(),
+                                "features_rest": torch.nn.Identity(), "scales": torch.nn.Identity(),
+                                "opacities": torch.nn.Identity(), "quats": torch.nn.Identity()},
+        max_scale_normalized=1e-2, grid_resolution=384, resume_ckpt=None, input_embed_to_mlp=False,
+        zeroinit=False, additional_info={"tome": "base", "r": 0.0})
+    model.eval()
+    s = make_scene(200, sh_degree=1, seed=5)
+    rec.clear()
+    with torch.no_grad():
+        outs = model([s], [0])
+    fo = {}
+    for k, v in s.items():
+        fo["in_" + k] = v.numpy()
+    bi = rec["backbone_in"]
+    fo["bb_coord"] = bi["coord"].numpy()
+    fo["bb_grid_coord"] = bi["grid_coord"].numpy()
+    fo["bb_offset"] = bi["offset"].numpy()
+    fo["bb_feat"] = bi["feat"].numpy()
+    fo["bb_grid_size"] = bi["grid_size"].numpy()
+    fo["bb_out"] = rec["backbone_out"].numpy()
+    for k, v in model.features_outputhead.state_dict().items():
+        fo["head." + k] = v.numpy()
+    for k, v in outs[0].items():
+        fo["out_" + k] = v.numpy()
+    np.savez_compressed(os.path.join(OUT, "feature_predictor.npz"), **fo)
+    torch.tensor = orig_tensor
+    print("wrote", sorted(out)[:4], "...", len(out), "render arrays;", len(fo), "feature-predictor arrays")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,203 @@
+"""HIP render path (libsfx) vs the gsplat v0.1.11 CPU oracle on identical inputs.
+
+Tolerances: fp32 kernels vs fp32 oracle -- 1e-5 relative on per-Gaussian
+projections, 1e-4 absolute on images, |dPSNR| <= 1e-4 dB on uint8-quantised
+renders (BASELINE.json north_star); integer/index outputs (radii, tile
+counts, sorted intersection ids, tile bins) bit-exact.
+"""
+import math
+
+import pytest
+import torch
+
+from oracle import gsplat_ref, render_ref
+from splatformer_amd import gs_render, gsplat_compat
+from splatformer_amd.scenes import make_cameras, make_scene, to_device
+
+pytestmark = pytest.mark.gpu
+
+
+def _scene(n, deg, seed):
+    return make_scene(n, sh_degree=deg, seed=seed)
+
+
+@pytest.mark.parametrize("deg", [0, 1, 2, 3, 4])
+def test_sh_fwd_bwd(device, deg):
+    n = 3000
+    g = torch.Generator().manual_seed(deg)
+    nb = (deg + 1) ** 2
+    coeffs = torch.randn(n, nb + 1 if deg < 4 else nb, 3, generator=g)  # extra basis -> stride test
+    dirs = torch.randn(n, 3, generator=g)
+    ref = gsplat_ref.spherical_harmonics(deg, dirs, coeffs)
+    c = coeffs.to(device).requires_grad_(True)
+    out = gsplat_compat.spherical_harmonics(deg, dirs.to(device), c)
+    torch.testing.assert_close(out.cpu(), ref, rtol=1e-5, atol=1e-6)
+    v = torch.randn(n, 3, generator=g)
+    out.backward(v.to(device))
+    refg = gsplat_ref.spherical_harmonics_bwd(deg, dirs, v, coeffs.shape[1])
+    torch.testing.assert_close(c.grad.cpu(), refg, rtol=1e-5, atol=1e-6)
+
+
+def _proj_inputs(n, seed, W=160, H=120):
+    s = make_scene(n, 1, seed)
+    cams = make_cameras(W, H, n_views=9)
+    c2w = cams["camera_to_worlds"][seed % 9]
+    a = render_ref.glue_args(s, c2w)
+    return a, cams, W, H
+
+
+@pytest.mark.parametrize("seed", [0, 4, 8])
+def test_project_fwd(device, seed):
+    a, cams, W, H = _proj_inputs(5000, seed)
+    args = (a["means"], a["scales"], 1.0, a["quats"], a["viewmat"], cams["fx"], cams["fy"], cams["cx"], cams["cy"], H,
+            W, 16)
+    ref = gsplat_ref.project_gaussians(*args)
+    dev = [x.to(device) if isinstance(x, torch.Tensor) else x for x in args]
+    out = gsplat_compat.project_gaussians(*dev)
+    names = ["xys", "depths", "radii", "conics", "comp", "num_tiles_hit", "cov3d"]
+    for nm, r, o in zip(names, ref, out):
+        o = o.cpu()
+        if r.dtype == torch.int32:
+            mism = (r != o).sum().item()
+            assert mism <= max(2, r.numel() // 2000), f"{nm}: {mism} integer mismatches"
+        else:
+            torch.testing.assert_close(o, r, rtol=2e-5, atol=1e-5, msg=nm)
+
+
+def test_scan_and_sort_exact(device):
+    g = torch.Generator().manual_seed(3)
+    for n in [1, 5, 2047, 2048, 2049, 100_000, 1_234_567]:
+        keys = torch.randint(0, 1 << 44, (n,), generator=g, dtype=torch.int64)
+        keys[::7] = keys[0]  # many ties -> stability matters
+        vals = torch.randperm(n, generator=g).to(torch.int32)
+        kd, vd = keys.to(device), vals.to(device)
+        ko, vo = torch.empty_like(kd), torch.empty_like(vd)
+        from splatformer_amd import _lib
+        ws = _lib.workspace(_lib.fn("sfx_sort_workspace_bytes")(n), device)
+        _lib.call("sfx_sort_pairs_u64", n, kd.data_ptr(), vd.data_ptr(), ko.data_ptr(), vo.data_ptr(), 0, 44,
+                  ws.data_ptr(), ws.numel(), _lib.stream())
+        ref = torch.sort(keys, stable=True)
+        assert torch.equal(ko.cpu(), ref.values)
+        assert torch.equal(vo.cpu(), vals[ref.indices])
+        # argsort mode (vals NULL)
+        _lib.call("sfx_sort_pairs_u64", n, kd.data_ptr(), None, ko.data_ptr(), vo.data_ptr(), 0, 44,
+                  ws.data_ptr(), ws.numel(), _lib.stream())
+        assert torch.equal(vo.cpu().long(), ref.indices)
+        cnt = torch.randint(0, 9, (n,), generator=g, dtype=torch.int32)
+        total, cum = gsplat_compat.compute_cumulative_intersects(cnt.to(device))
+        assert total == int(cnt.sum())
+        assert torch.equal(cum.cpu(), torch.cumsum(cnt, 0, dtype=torch.int32))
+
+
+def test_bin_and_sort_exact(device):
+    a, cams, W, H = _proj_inputs(4000, 2)
+    ref = gsplat_ref.project_gaussians(a["means"], a["scales"], 1.0, a["quats"], a["viewmat"], cams["fx"],
+                                       cams["fy"], cams["cx"], cams["cy"], H, W, 16)
+    xys, depths, radii, _, _, tiles, _ = ref
+    tx, ty = (W + 15) // 16, (H + 15) // 16
+    k_ref, g_ref, b_ref = gsplat_ref.bin_and_sort_gaussians(xys, depths, radii, tiles, tx, ty, 16)
+    num, cum = gsplat_compat.compute_cumulative_intersects(tiles.to(device))
+    assert num == k_ref.numel()
+    _, _, ks, gs, bins = gsplat_compat.bin_and_sort_gaussians(xys.shape[0], num, xys.to(device), depths.to(device),
+                                                              radii.to(device), cum, (tx, ty, 1), 16)
+    assert torch.equal(ks.cpu(), k_ref)
+    assert torch.equal(gs.cpu(), g_ref)
+    assert torch.equal(bins.cpu(), b_ref)
+
+
+def _psnr_u8(x, gt):
+    return float(gsplat_ref.psnr_u8(x[None], gt[None]))
+
+
+@pytest.mark.parametrize("deg,n,res", [(1, 4000, (128, 96)), (0, 2000, (64, 64)), (3, 3000, (100, 70))])
+def test_render_fused_matches_oracle(device, deg, n, res):
+    W, H = res
+    s = _scene(n, deg, seed=deg + 20)
+    cams = make_cameras(W, H, n_views=3)
+    cams["background_color"] = torch.tensor([0.05, 0.1, 0.2])
+    gt = torch.rand(H, W, 3, generator=torch.Generator().manual_seed(9))
+    sd, cd = to_device(s, device), to_device(cams, device)
+    for v in range(3):
+        c2w = cams["camera_to_worlds"][v]
+        rr, ar = render_ref.rasterize_gaussians_to_singleimg(s, c2w, **cams)
+        with torch.no_grad():
+            rh, ah = gs_render.rasterize_gaussians_to_singleimg(sd, cd["camera_to_worlds"][v], **cd)
+        rh, ah = rh.cpu(), ah.cpu()
+        assert rh.shape == (H, W, 3) and ah.shape == (H, W, 1)
+        torch.testing.assert_close(rh, rr, rtol=0, atol=2e-4)
+        torch.testing.assert_close(ah, ar, rtol=0, atol=2e-4)
+        assert abs(_psnr_u8(rh, gt) - _psnr_u8(rr, gt)) <= 1e-4
+        # mean abs error, and the PSNR between the two renders, far above quantisation
+        assert (rh - rr).abs().mean() < 1e-6
+
+
+def test_render_empty_and_culled(device):
+    cams = make_cameras(32, 32, n_views=1)
+    s = make_scene(50, 1, seed=1)
+    s["means"] = s["means"] + 10.0  # far outside the frustum / behind: all culled
+    sd, cd = to_device(s, device), to_device(cams, device)
+    with torch.no_grad():
+        rh, ah = gs_render.rasterize_gaussians_to_singleimg(sd, cd["camera_to_worlds"][0], **cd)
+    rr, ar = render_ref.rasterize_gaussians_to_singleimg(s, cams["camera_to_worlds"][0], **cams)
+    torch.testing.assert_close(rh.cpu(), rr)
+    torch.testing.assert_close(ah.cpu(), ar)  # gsplat empty-branch: alpha == 1
+
+
+def test_render_backward_matches_oracle(device):
+    W, H = 96, 80
+    s = _scene(1500, 1, seed=31)
+    cams = make_cameras(W, H, n_views=2)
+    c2w = cams["camera_to_worlds"][1]
+    a = render_ref.glue_args(s, c2w)
+    xys, depths, radii, conics, comp, tiles, cov3d = gsplat_ref.project_gaussians(
+        a["means"], a["scales"], 1.0, a["quats"], a["viewmat"], cams["fx"], cams["fy"], cams["cx"], cams["cy"], H, W,
+        16)
+    bg = torch.tensor([0.3, 0.2, 0.1])
+    g = torch.Generator().manual_seed(5)
+    v_out = torch.randn(H, W, 3, generator=g)
+    v_alpha = torch.randn(H, W, generator=g)
+    # HIP forward+backward through the autograd Function
+    t = lambda x: x.to(device).clone().requires_grad_(x.dtype == torch.float32)
+    xd, cd_, rd, od = t(xys), t(conics), t(a["rgbs"]), t(a["opacities"])
+    img, alpha = gsplat_compat.rasterize_gaussians(xd, depths.to(device), radii.to(device), cd_, tiles.to(device), rd,
+                                                   od, H, W, 16, background=bg.to(device), return_alpha=True)
+    (img * v_out.to(device)).sum().add_((alpha * v_alpha.to(device)).sum()).backward()
+    # oracle backward on the oracle forward state
+    tx, ty = (W + 15) // 16, (H + 15) // 16
+    _, gids, bins = gsplat_ref.bin_and_sort_gaussians(xys, depths, radii, tiles, tx, ty, 16)
+    _, fT, fidx = gsplat_ref.rasterize_forward(tx, ty, 16, H, W, gids, bins, xys, conics, a["rgbs"], a["opacities"],
+                                               bg)
+    # alpha = 1 - T -> dL/dalpha enters with the reference's sign convention
+    rv = gsplat_ref.rasterize_backward(tx, ty, 16, H, W, gids, bins, xys, conics, a["rgbs"], a["opacities"], bg, fT,
+                                       fidx, v_out, v_alpha)
+    for nm, got, exp in zip(["v_xy", "v_conic", "v_rgb", "v_opacity"], [xd.grad, cd_.grad, rd.grad, od.grad], rv):
+        got = got.cpu()
+        scale = exp.abs().max().clamp_min(1e-6)
+        err = (got - exp).abs().max() / scale
+        assert err < 2e-4, f"{nm}: rel err {err}"
+
+
+def test_project_backward_matches_oracle(device):
+    a, cams, W, H = _proj_inputs(3000, 5)
+    args = (a["means"], a["scales"], 1.0, a["quats"], a["viewmat"], cams["fx"], cams["fy"], cams["cx"], cams["cy"], H,
+            W, 16)
+    xys, depths, radii, conics, comp, tiles, cov3d = gsplat_ref.project_gaussians(*args)
+    g = torch.Generator().manual_seed(1)
+    n = xys.shape[0]
+    vx, vc = torch.randn(n, 2, generator=g), torch.randn(n, 3, generator=g) * 1e-3
+    vd, vco = torch.zeros(n), torch.zeros(n)
+    ref = gsplat_ref.project_gaussians_backward(a["means"], a["scales"], 1.0, a["quats"], a["viewmat"], cams["fx"],
+                                                cams["fy"], cov3d, radii, conics, comp, vx, vd, vc, vco)
+    m = a["means"].to(device).requires_grad_(True)
+    sc = a["scales"].to(device).requires_grad_(True)
+    q = a["quats"].to(device).requires_grad_(True)
+    out = gsplat_compat.project_gaussians(m, sc, 1.0, q, a["viewmat"].to(device), cams["fx"], cams["fy"], cams["cx"],
+                                          cams["cy"], H, W, 16)
+    (out[0] * vx.to(device)).sum().add_((out[3] * vc.to(device)).sum()).backward()
+    for nm, got, exp in zip(["v_mean", "v_scale", "v_quat"], [m.grad, sc.grad, q.grad], ref):
+        got = got.cpu()
+        live = radii > 0
+        scale = exp[live].abs().max().clamp_min(1e-6)
+        err = ((got - exp)[live].abs().max() / scale).item()
+        assert err < 1e-4, f"{nm}: rel err {err}"
+        assert float(got[~live].abs().max() if (~live).any() else 0) == 0.0
