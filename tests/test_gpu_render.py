@@ -31,7 +31,7 @@ def test_sh_fwd_bwd(device, deg):
     ref = gsplat_ref.spherical_harmonics(deg, dirs, coeffs)
     c = coeffs.to(device).requires_grad_(True)
     out = gsplat_compat.spherical_harmonics(deg, dirs.to(device), c)
-    torch.testing.assert_close(out.cpu(), ref, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(out.cpu(), ref, rtol=1e-5, atol=5e-6)
     v = torch.randn(n, 3, generator=g)
     out.backward(v.to(device))
     refg = gsplat_ref.spherical_harmonics_bwd(deg, dirs, v, coeffs.shape[1])
