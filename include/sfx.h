@@ -71,10 +71,13 @@ int sfx_project_bwd(int n, const float* means, const float* scales, float glob_s
 
 /* Fused eval-path glue + SH + projection: utils/gs_utils.py:32-95 in one pass
  * (camera_to_world [3x4|4x4 row-major, OpenGL] -> viewmat_out[3x4]; exp(scales),
- * normalised quats, sigmoid(opacities), SH colours, project_gaussians). */
-int sfx_render_prep_project(int n, int num_bases, const float* means, const float* log_scales,
-                            const float* quats_raw, const float* opac_logit, const float* features_dc,
-                            const float* features_rest, const float* camera_to_world, float fx, float fy, float cx,
+ * normalised quats, sigmoid(opacities), SH colours, project_gaussians).  Each attribute is read with its
+ * own row stride (elements), so the packed [N,23] refined-Gaussian record of the heads can be rendered
+ * in place; features_rest rows hold (num_bases-1)*3 coefficients. */
+int sfx_render_prep_project(int n, int num_bases, const float* means, long long ld_means, const float* log_scales,
+                            long long ld_scales, const float* quats_raw, long long ld_quats, const float* opac_logit,
+                            long long ld_opac, const float* features_dc, long long ld_dc, const float* features_rest,
+                            long long ld_rest, const float* camera_to_world, float fx, float fy, float cx,
                             float cy, int img_h, int img_w, int block_width, float* viewmat_out, float* rgbs,
                             float* opacities, float* xys, float* depths, int* radii, float* conics,
                             int* num_tiles_hit, void* stream);
@@ -99,6 +102,68 @@ int sfx_rasterize_bwd(int tiles_x, int tiles_y, int block_width, int img_h, int 
                       const float* opacity, const float* background, const float* final_Ts, const int* final_idx,
                       const float* v_out, const float* v_out_alpha, float* v_xy, float* v_xy_abs, float* v_conic,
                       float* v_rgb, float* v_opacity, void* stream);
+
+/* ---- refiner: Pointcept PTv3 m1 + FeaturePredictor (models/pointtransformer_v3.py, feature_predictor.py) -- */
+/* fp32 MFMA GEMM, Y = act((A' W^T + bias) * scale + shift) + R[ridx]; A' = A or, with gather_idx [M][S],
+ * the concatenation of S gathered rows (SubMConv3d implicit GEMM).  act: 0 none, 1 GELU(erf), 2 ReLU,
+ * 3 tanh, applied to columns < act_ncols (-1 = all).  Ypre (optional) receives the pre-residual value.
+ * groups > 1 runs a grouped GEMM (block-diagonal heads) with the given per-group element strides.
+ * Replaces nn.Linear / BatchNorm1d(eval) / GELU / residual adds of Block, Embedding, SerializedPooling,
+ * SerializedUnpooling and the FeaturePredictor heads (feature_predictor.py:74-94, :201-235), and
+ * spconv.SubMConv3d (Block.cpe) through gather_idx. */
+int sfx_linear(int M, int N, int K, const float* A, long long lda, const int* gather_idx, int num_segments,
+               const float* W, long long ldw, const float* bias, const float* scale, const float* shift, int act,
+               int act_ncols, const float* R, long long ldr, const int* residual_idx, float* Y, long long ldy,
+               float* Ypre, long long ldypre, int groups, long long group_stride_A, long long group_stride_W,
+               long long group_stride_bias, long long group_stride_Y, void* stream);
+
+/* nn.LayerNorm rows (C <= 512): Block.norm1 / norm2 */
+int sfx_layernorm(int M, int C, const float* X, long long ldx, const float* gamma, const float* beta, float eps,
+                  float* Y, long long ldy, void* stream);
+/* Block tail of cpe + shortcut + norm1: X_out = X + LN_cpe(T); H = LN1(X_out)  (X_out may alias X) */
+int sfx_cpe_residual_ln(int M, int C, const float* T, const float* X, const float* gamma_cpe, const float* beta_cpe,
+                        const float* gamma1, const float* beta1, float eps, float* X_out, float* H, void* stream);
+
+/* SerializedAttention (non-flash): windows win[w] = (key_start, query_start) over serialized positions,
+ * qkv [N,3C] in point order, order [N] serialized->point; out[order[p]] for every query position p. */
+int sfx_window_attention(int num_windows, int window, int heads, int head_dim, int channels, const float* qkv,
+                         const int* order, const int* win, float scale, float* out, void* stream);
+
+/* Point.serialization: codes[R][n] = batch << 3*depth | enc_t(grid) for order types t0..t3 (0 z, 1 z-trans,
+ * 2 hilbert, 3 hilbert-trans) and combined sort keys r << code_bits | code; finalize turns the argsort of
+ * the keys into order[R][n] / inverse[R][n]. */
+int sfx_serialize_keys(int n, const int* grid_coord, const int* batch, int depth, int num_orders, int t0, int t1,
+                       int t2, int t3, int code_bits, int64_t* codes, uint64_t* keys, void* stream);
+int sfx_serialize_finalize(int n, int num_orders, const int* sorted_pos, int* order, int* inverse, void* stream);
+
+/* SerializedPooling: run heads of the code[0] >> shift sort, cluster ids / idx_ptr / head indices,
+ * pooled codes+grid+batch, segment max (+BN affine +GELU) of the projected features, mean of coords. */
+int sfx_pool_flags(int n, const uint64_t* sorted_keys, int shift, int* flags, void* stream);
+int sfx_pool_assign(int n, const int* sorted_idx, const int* cid_inclusive, const int* flags, int* cluster,
+                    int* idx_ptr, int* head, void* stream);
+int sfx_pool_gather(int m, int n, int num_orders, const int* head, const int64_t* codes, int pooling_depth,
+                    const int* grid_coord, const int* batch, int code_bits, int64_t* new_codes, uint64_t* keys,
+                    int* new_grid, int* new_batch, void* stream);
+int sfx_segment_max_affine_act(int m, int C, const int* idx_ptr, const int* sorted_idx, const float* X,
+                               const float* scale, const float* shift, int act, float* Y, void* stream);
+int sfx_segment_mean(int m, int D, const int* idx_ptr, const int* sorted_idx, const float* X, float* Y,
+                     void* stream);
+
+/* spconv SubMConv3d indice pairs (indice_key=stage{s}): nbr[n][27], k = (dx+1)*9+(dy+1)*3+(dz+1), -1 absent,
+ * duplicate voxels resolve to the lowest point index.  table_*: 2^log2cap scratch slots. */
+int sfx_subm_table_log2(int n);
+int sfx_subm_neighbors(int n, const int* grid_coord, const int* batch, int log2cap, unsigned long long* table_keys,
+                       int* table_vals, int* nbr, void* stream);
+
+/* FeaturePredictor batchify (feature_predictor.py:134-156): strided attribute rows -> feat rows
+ * [means,scales,opacities,quats,dc,rest], grid_coord = floor(means*res), optional atomic grid max. */
+int sfx_gs_pack(int n, const float* means, long long ld_means, const float* scales, long long ld_scales,
+                const float* opacities, long long ld_opacities, const float* quats, long long ld_quats,
+                const float* features_dc, long long ld_dc, const float* features_rest, long long ld_rest,
+                int rest_dim, float grid_resolution, float* feat, long long ld_feat, int* grid_coord, int* grid_max,
+                void* stream);
+/* Pointcept offset2batch */
+int sfx_offsets_to_batch(int n, int B, const long long* offsets, int* batch, void* stream);
 
 #ifdef __cplusplus
 }

@@ -35,7 +35,8 @@ SIGNATURES: dict[str, list] = {
     "sfx_sh_bwd": [I, I, I, P, P, P, P],
     "sfx_project_fwd": [I, P, P, F, P, P, F, F, F, F, I, I, I, F, P, P, P, P, P, P, P, P],
     "sfx_project_bwd": [I, P, P, F, P, P, F, F, P, P, P, P, P, P, P, P, P, P, P, P, P, P],
-    "sfx_render_prep_project": [I, I, P, P, P, P, P, P, P, F, F, F, F, I, I, I, P, P, P, P, P, P, P, P, P],
+    "sfx_render_prep_project": [I, I, P, L, P, L, P, L, P, L, P, L, P, L, P, F, F, F, F, I, I, I, P, P, P, P, P, P, P,
+                                P, P],
     "sfx_isect_emit": [I, P, P, P, P, I, I, I, P, P, P],
     "sfx_tile_bins": [I, P, I, P, P],
     "sfx_rasterize_fwd": [I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P],

@@ -1,0 +1,168 @@
+// Serialized windowed multi-head attention (PTv3 SerializedAttention,
+// non-flash path: reference models/pointtransformer_v3.py:121-126 patch 128,
+// math restated in-tree at visualize.py:140-179).
+//
+// For each window of K <= 128 consecutive serialized positions and each head:
+//   S = (q * scale) k^T ; P = softmax_keys(S) ; O = P v
+// q/k/v rows are gathered straight from the qkv projection [N, 3C] through
+// the serialized order (`qkv[order]`, row layout [3][H][d]) and the output row
+// is scattered back through the same order (`feat[inverse]`), so neither the
+// padded/permuted qkv nor the [N', H, K, K] score tensor is materialised.
+//
+// Window table: win[w] = (key_start, query_start) in serialized positions.
+// Pointcept pads a ragged last window by duplicating the K - n%K points that
+// precede it (get_padding_and_inverse); that window therefore attends over
+// the last K real points and only its new queries are written -- the table
+// encodes exactly that (key_start = n - K, query_start = floor(n/K)*K).
+//
+// gfx950: one 256-thread workgroup per (window, head), 4 waves x 32 queries.
+// S^T = K Q^T on v_mfma_f32_32x32x2_f32 puts each query on a lane column and
+// its 128 keys in registers (64 per half-wave), so the softmax is a register
+// reduction + one cross-half exchange, and P^T feeds the P.V MFMA directly as
+// the B operand (no LDS round trip for P).
+#include "common.h"
+
+namespace {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+constexpr int KMAX = 128;
+
+template <int D>
+__global__ void __launch_bounds__(256, 2)
+window_attn_kernel(const float* __restrict__ qkv, const int* __restrict__ order, const int* __restrict__ win,
+                   int Kwin, int C, float scale, float* __restrict__ out) {
+  constexpr int DP = D + 4;
+  constexpr int HALF = D / 2;  // k-values per lane half in S = K Q^T
+  __shared__ __attribute__((aligned(16))) float Qs[KMAX * DP];
+  __shared__ __attribute__((aligned(16))) float Ks[KMAX * DP];
+  __shared__ __attribute__((aligned(16))) float Vs[KMAX * DP];
+  __shared__ int rows[KMAX];
+
+  const int w = blockIdx.x, head = blockIdx.y;
+  const int key_start = win[2 * w], query_start = win[2 * w + 1];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, h = lane >> 5, l32 = lane & 31;
+  const long long ld = 3ll * C;
+
+  if (tid < KMAX) rows[tid] = tid < Kwin ? order[key_start + tid] : -1;
+  __syncthreads();
+  // gather q/k/v rows of this head: KMAX rows x 3 mats x D/4 float4
+  constexpr int CH = D / 4;
+  for (int e = tid; e < KMAX * 3 * CH; e += 256) {
+    const int row = e / (3 * CH);
+    const int rem = e - row * 3 * CH;
+    const int mat = rem / CH, ch = rem - mat * CH;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    const int src = rows[row];
+    if (src >= 0) v = *reinterpret_cast<const float4*>(qkv + (long long)src * ld + mat * C + head * D + 4 * ch);
+    if (mat == 0) {
+      v.x *= scale; v.y *= scale; v.z *= scale; v.w *= scale;
+      *reinterpret_cast<float4*>(&Qs[row * DP + 4 * ch]) = v;
+    } else if (mat == 1) {
+      *reinterpret_cast<float4*>(&Ks[row * DP + 4 * ch]) = v;
+    } else {
+      *reinterpret_cast<float4*>(&Vs[row * DP + 4 * ch]) = v;
+    }
+  }
+  __syncthreads();
+
+  // S^T[key][query] for this wave's 32 queries, 4 key blocks of 32
+  floatx16 s[4];
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s[kb][r] = 0.f;
+  const float* qrow = &Qs[(32 * wid + l32) * DP + h * HALF];
+#pragma unroll
+  for (int c = 0; c < HALF / 4; ++c) {
+    const float4 qv = *reinterpret_cast<const float4*>(qrow + 4 * c);
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+      const float4 kv = *reinterpret_cast<const float4*>(&Ks[(kb * 32 + l32) * DP + h * HALF + 4 * c]);
+      s[kb] = __builtin_amdgcn_mfma_f32_32x32x2f32(kv.x, qv.x, s[kb], 0, 0, 0);
+      s[kb] = __builtin_amdgcn_mfma_f32_32x32x2f32(kv.y, qv.y, s[kb], 0, 0, 0);
+      s[kb] = __builtin_amdgcn_mfma_f32_32x32x2f32(kv.z, qv.z, s[kb], 0, 0, 0);
+      s[kb] = __builtin_amdgcn_mfma_f32_32x32x2f32(kv.w, qv.w, s[kb], 0, 0, 0);
+    }
+  }
+  // softmax over keys (register axis + the other half-wave)
+  float mx = -INFINITY;
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int key = kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (key >= Kwin) s[kb][r] = -INFINITY;
+      mx = fmaxf(mx, s[kb][r]);
+    }
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  float sum = 0.f;
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float e = expf(s[kb][r] - mx);
+      s[kb][r] = e;
+      sum += e;
+    }
+  sum += __shfl_xor(sum, 32, 64);
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s[kb][r] = s[kb][r] / sum;
+
+  // O^T[dd][query] = sum_key V[key][dd] P^T[key][query]
+  floatx16 o;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) o[r] = 0.f;
+  const bool dd_ok = l32 < D;
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+    for (int st = 0; st < 16; ++st) {
+      const int key = kb * 32 + (st & 3) + 8 * (st >> 2) + 4 * h;
+      const float a = dd_ok ? Vs[key * DP + l32] : 0.f;
+      o = __builtin_amdgcn_mfma_f32_32x32x2f32(a, s[kb][st], o, 0, 0, 0);
+    }
+
+  // scatter: query 32*wid + l32 (lane column), dd rows (r&3) + 8(r>>2) + 4h
+  const int qi = 32 * wid + l32;
+  const int qpos = key_start + qi;
+  if (qi < Kwin && qpos >= query_start) {
+    float* dst = out + (long long)rows[qi] * C + head * D;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int dd = 8 * g + 4 * h;
+      if (dd + 3 < D) {
+        *reinterpret_cast<float4*>(dst + dd) = make_float4(o[4 * g + 0], o[4 * g + 1], o[4 * g + 2], o[4 * g + 3]);
+      }
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+// qkv [N, 3C] (point order), order [N] serialized->point, win [num_windows][2], out [N, C]
+int sfx_window_attention(int num_windows, int window, int heads, int head_dim, int channels, const float* qkv,
+                         const int* order, const int* win, float scale, float* out, void* stream) {
+  SFX_REQUIRE(num_windows >= 0, "sfx_window_attention: num_windows < 0");
+  SFX_REQUIRE(window >= 1 && window <= KMAX, "sfx_window_attention: window must be in [1, 128]");
+  SFX_REQUIRE(heads * head_dim == channels, "sfx_window_attention: heads * head_dim != channels");
+  SFX_REQUIRE(head_dim == 16 || head_dim == 24 || head_dim == 32,
+              "sfx_window_attention: head_dim %d unsupported (16, 24, 32)", head_dim);
+  if (num_windows == 0) return SFX_OK;
+  SFX_REQUIRE(qkv && order && win && out, "sfx_window_attention: null buffer");
+  dim3 grid(num_windows, heads);
+  hipStream_t st = sfx::as_stream(stream);
+  if (head_dim == 16)
+    window_attn_kernel<16><<<grid, 256, 0, st>>>(qkv, order, win, window, channels, scale, out);
+  else if (head_dim == 24)
+    window_attn_kernel<24><<<grid, 256, 0, st>>>(qkv, order, win, window, channels, scale, out);
+  else
+    window_attn_kernel<32><<<grid, 256, 0, st>>>(qkv, order, win, window, channels, scale, out);
+  return sfx::check_launch("sfx_window_attention");
+}
+
+}  // extern "C"

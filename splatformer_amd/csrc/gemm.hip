@@ -253,7 +253,7 @@ int sfx_linear(int M, int N, int K, const float* A, long long lda, const int* ga
   a.Ypre = Ypre; a.ldypre = ldypre; a.gA = group_stride_A; a.gW = group_stride_W; a.gB = group_stride_bias;
   a.gY = group_stride_Y;
   const bool vec = (K % 4 == 0) && (lda % 4 == 0) && (ldw % 4 == 0) && aligned16(A) && aligned16(W) &&
-                   (group_stride_A % 4 == 0) && (group_stride_W % 4 == 0) && (!gather_idx || Kseg % 32 == 0 || true);
+                   (group_stride_A % 4 == 0) && (group_stride_W % 4 == 0);
   hipStream_t st = sfx::as_stream(stream);
   const long long tiles128 = (long long)sfx::ceil_div(M, 128) * sfx::ceil_div(N, 128) * groups;
   if (N <= 64)

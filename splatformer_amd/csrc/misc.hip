@@ -1,0 +1,82 @@
+// Small data-movement kernels around the refiner:
+//  * sfx_gs_pack: FeaturePredictor batchify (reference
+//    models/feature_predictor.py:134-156): concatenate the Gaussian attributes
+//    in `input_features` order [means, scales, opacities, quats, features_dc,
+//    features_rest.view(N,-1)] into a strided feature buffer, and emit
+//    grid_coord = floor(coord * grid_resolution) (int32) -- one pass.
+//  * sfx_offsets_to_batch: Pointcept offset2batch.
+#include "common.h"
+
+namespace {
+
+__global__ void gs_pack_kernel(int n, const float* __restrict__ means, long long ld_m, const float* __restrict__ scales,
+                               long long ld_s, const float* __restrict__ opac, long long ld_o,
+                               const float* __restrict__ quats, long long ld_q, const float* __restrict__ dc,
+                               long long ld_dc, const float* __restrict__ rest, long long ld_r, int rest_dim,
+                               float grid_resolution, float* __restrict__ feat, long long ld_f,
+                               int* __restrict__ grid_coord, int* __restrict__ grid_max) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  int mx = 0;
+  if (i < n) {
+    float* f = feat + (long long)i * ld_f;
+    int c = 0;
+    for (int k = 0; k < 3; ++k) f[c++] = means[(long long)i * ld_m + k];
+    for (int k = 0; k < 3; ++k) f[c++] = scales[(long long)i * ld_s + k];
+    f[c++] = opac[(long long)i * ld_o];
+    for (int k = 0; k < 4; ++k) f[c++] = quats[(long long)i * ld_q + k];
+    for (int k = 0; k < 3; ++k) f[c++] = dc[(long long)i * ld_dc + k];
+    for (int k = 0; k < rest_dim; ++k) f[c++] = rest[(long long)i * ld_r + k];
+    if (grid_coord) {
+      for (int k = 0; k < 3; ++k) {
+        const int g = (int)floorf(means[(long long)i * ld_m + k] * grid_resolution);
+        grid_coord[3 * i + k] = g;
+        mx = max(mx, g);
+      }
+    }
+  }
+  if (grid_coord && grid_max) {  // all lanes active: wave-reduce, one atomic per wave
+    mx = sfx::wave_max_i(mx);
+    if ((threadIdx.x & 63) == 0) atomicMax(grid_max, mx);
+  }
+}
+
+__global__ void offsets_to_batch_kernel(int n, int B, const long long* __restrict__ offsets, int* __restrict__ batch) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  int lo = 0, hi = B - 1;  // first b with offsets[b] > i
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (offsets[mid] > i) hi = mid; else lo = mid + 1;
+  }
+  batch[i] = lo;
+}
+
+}  // namespace
+
+extern "C" {
+
+int sfx_gs_pack(int n, const float* means, long long ld_means, const float* scales, long long ld_scales,
+                const float* opacities, long long ld_opacities, const float* quats, long long ld_quats,
+                const float* features_dc, long long ld_dc, const float* features_rest, long long ld_rest,
+                int rest_dim, float grid_resolution, float* feat, long long ld_feat, int* grid_coord, int* grid_max,
+                void* stream) {
+  SFX_REQUIRE(n >= 0 && rest_dim >= 0, "sfx_gs_pack: bad sizes");
+  if (n == 0) return SFX_OK;
+  SFX_REQUIRE(means && scales && opacities && quats && features_dc && feat && (rest_dim == 0 || features_rest),
+              "sfx_gs_pack: null buffer");
+  SFX_REQUIRE(ld_feat >= 14 + rest_dim, "sfx_gs_pack: ld_feat too small");
+  gs_pack_kernel<<<sfx::ceil_div(n, 256), 256, 0, sfx::as_stream(stream)>>>(
+      n, means, ld_means, scales, ld_scales, opacities, ld_opacities, quats, ld_quats, features_dc, ld_dc,
+      features_rest, ld_rest, rest_dim, grid_resolution, feat, ld_feat, grid_coord, grid_max);
+  return sfx::check_launch("sfx_gs_pack");
+}
+
+int sfx_offsets_to_batch(int n, int B, const long long* offsets, int* batch, void* stream) {
+  SFX_REQUIRE(n >= 0 && B >= 1, "sfx_offsets_to_batch: bad sizes");
+  if (n == 0) return SFX_OK;
+  SFX_REQUIRE(offsets && batch, "sfx_offsets_to_batch: null buffer");
+  offsets_to_batch_kernel<<<sfx::ceil_div(n, 256), 256, 0, sfx::as_stream(stream)>>>(n, B, offsets, batch);
+  return sfx::check_launch("sfx_offsets_to_batch");
+}
+
+}  // extern "C"

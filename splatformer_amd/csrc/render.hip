@@ -285,10 +285,14 @@ __global__ void project_fwd_kernel(int n, const float* __restrict__ means, const
 // opacity = sigmoid, SH colours (+0.5, clamp >= 0; sigmoid(dc) at degree 0),
 // then project_gaussians with glob_scale 1.  Block 0 lane 0 also stores the
 // 3x4 viewmat for the caller.
+struct PrepStrides {
+  long long means, scales, quats, opac, dc, rest;
+};
+
 __global__ void render_prep_project_kernel(int n, int num_bases, const float* __restrict__ means,
                                            const float* __restrict__ log_scales, const float* __restrict__ quats_raw,
                                            const float* __restrict__ opac_logit, const float* __restrict__ dc,
-                                           const float* __restrict__ rest, const float* __restrict__ c2w,
+                                           const float* __restrict__ rest, PrepStrides ld, const float* __restrict__ c2w,
                                            float fx, float fy, float cx, float cy, int img_h, int img_w, int bw,
                                            float* __restrict__ viewmat_out, float* __restrict__ rgbs,
                                            float* __restrict__ opac, float* __restrict__ xys,
@@ -315,20 +319,24 @@ __global__ void render_prep_project_kernel(int n, int num_bases, const float* __
 #pragma unroll
     for (int k = 0; k < 12; ++k) viewmat_out[k] = vm[k];
   if (i >= n) return;
-  const float px = means[3 * i], py = means[3 * i + 1], pz = means[3 * i + 2];
-  const float sc0 = expf(log_scales[3 * i]), sc1 = expf(log_scales[3 * i + 1]), sc2 = expf(log_scales[3 * i + 2]);
-  float q0 = quats_raw[4 * i], q1 = quats_raw[4 * i + 1], q2 = quats_raw[4 * i + 2], q3 = quats_raw[4 * i + 3];
+  const float* mp = means + i * ld.means;
+  const float* sp = log_scales + i * ld.scales;
+  const float* qp = quats_raw + i * ld.quats;
+  const float* dcp = dc + i * ld.dc;
+  const float px = mp[0], py = mp[1], pz = mp[2];
+  const float sc0 = expf(sp[0]), sc1 = expf(sp[1]), sc2 = expf(sp[2]);
+  float q0 = qp[0], q1 = qp[1], q2 = qp[2], q3 = qp[3];
   const float qn = sqrtf(q0 * q0 + q1 * q1 + q2 * q2 + q3 * q3);
   q0 /= qn; q1 /= qn; q2 /= qn; q3 /= qn;
   if (isnan(q0) || isnan(q1) || isnan(q2) || isnan(q3)) {
     q0 = 0.f; q1 = 0.f; q2 = 0.f; q3 = 1.f;
   }
-  opac[i] = 1.f / (1.f + expf(-opac_logit[i]));
+  opac[i] = 1.f / (1.f + expf(-opac_logit[i * ld.opac]));
   // colours
   const int degree = num_bases >= 25 ? 4 : num_bases >= 16 ? 3 : num_bases >= 9 ? 2 : num_bases >= 4 ? 1 : 0;
   if (degree == 0) {
 #pragma unroll
-    for (int ch = 0; ch < 3; ++ch) rgbs[3 * i + ch] = 1.f / (1.f + expf(-dc[3 * i + ch]));
+    for (int ch = 0; ch < 3; ++ch) rgbs[3 * i + ch] = 1.f / (1.f + expf(-dcp[ch]));
   } else {
     float vx = px - t[0], vy = py - t[1], vz = pz - t[2];
     const float vn = sqrtf(vx * vx + vy * vy + vz * vz);
@@ -340,10 +348,10 @@ __global__ void render_prep_project_kernel(int n, int num_bases, const float* __
     const float nrm = sqrtf(vx * vx + vy * vy + vz * vz);
     const float x = vx / nrm, y = vy / nrm, z = vz / nrm;
     const float xx = x * x, xy = x * y, xz = x * z, yy = y * y, yz = y * z, zz = z * z;
-    const float* c = rest + (size_t)i * (num_bases - 1) * 3 - 3;  // c[3*k + ch] for k >= 1
+    const float* c = rest + i * ld.rest - 3;  // c[3*k + ch] for k >= 1
 #pragma unroll
     for (int ch = 0; ch < 3; ++ch) {
-      float acc = SH_C0 * dc[3 * i + ch];
+      float acc = SH_C0 * dcp[ch];
       acc += SH_C1 * (-y * c[3 + ch] + z * c[6 + ch] - x * c[9 + ch]);
       if (degree >= 2) {
         acc += (SH_C2[0] * xy * c[12 + ch] + SH_C2[1] * yz * c[15 + ch] + SH_C2[2] * (2.f * zz - xx - yy) * c[18 + ch] +
@@ -827,9 +835,10 @@ int sfx_project_fwd(int n, const float* means, const float* scales, float glob_s
   return sfx::check_launch("sfx_project_fwd");
 }
 
-int sfx_render_prep_project(int n, int num_bases, const float* means, const float* log_scales,
-                            const float* quats_raw, const float* opac_logit, const float* features_dc,
-                            const float* features_rest, const float* camera_to_world, float fx, float fy, float cx,
+int sfx_render_prep_project(int n, int num_bases, const float* means, long long ld_means, const float* log_scales,
+                            long long ld_scales, const float* quats_raw, long long ld_quats, const float* opac_logit,
+                            long long ld_opac, const float* features_dc, long long ld_dc, const float* features_rest,
+                            long long ld_rest, const float* camera_to_world, float fx, float fy, float cx,
                             float cy, int img_h, int img_w, int block_width, float* viewmat_out, float* rgbs,
                             float* opacities, float* xys, float* depths, int* radii, float* conics,
                             int* num_tiles_hit, void* stream) {
@@ -844,7 +853,8 @@ int sfx_render_prep_project(int n, int num_bases, const float* means, const floa
                     rgbs && opacities && xys && depths && radii && conics && num_tiles_hit,
                 "sfx_render_prep_project: null buffer");
   render_prep_project_kernel<<<sfx::ceil_div(n > 0 ? n : 1, 256), 256, 0, sfx::as_stream(stream)>>>(
-      n, num_bases, means, log_scales, quats_raw, opac_logit, features_dc, features_rest, camera_to_world, fx, fy, cx,
+      n, num_bases, means, log_scales, quats_raw, opac_logit, features_dc, features_rest,
+      PrepStrides{ld_means, ld_scales, ld_quats, ld_opac, ld_dc, ld_rest}, camera_to_world, fx, fy, cx,
       cy, img_h, img_w, block_width, viewmat_out, rgbs, opacities, xys, depths, radii, conics, num_tiles_hit);
   return sfx::check_launch("sfx_render_prep_project");
 }

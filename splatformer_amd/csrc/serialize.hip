@@ -1,0 +1,242 @@
+// Point serialization and serialized pooling (Pointcept PTv3 m1 semantics,
+// reference models/pointtransformer_v3.py:130 orders ("z","z-trans",
+// "hilbert","hilbert-trans"), :380 Point.serialization, :290-299
+// SerializedPooling).
+//
+// Codes are computed per point in registers (bit interleave for z-order, the
+// Skilling transform as integer bit ops for Hilbert), all orders are sorted
+// in ONE stable radix sort by prefixing the order index above the code bits,
+// and a finalize pass writes order/inverse.  Pooling sorts code[0] by its
+// bits above 3*pooling_depth (== torch.unique + sort(cluster)), marks run
+// heads, scans them into cluster ids and reduces features per run.
+#include "common.h"
+
+namespace {
+
+// ---- z-order (OCNN KeyLUT xyz2key): bit i of x -> 3i+2, y -> 3i+1, z -> 3i
+__device__ __forceinline__ uint64_t z_encode(uint32_t x, uint32_t y, uint32_t z, int depth) {
+  uint64_t key = 0;
+  for (int i = 0; i < depth; ++i) {
+    key |= (uint64_t)((x >> i) & 1u) << (3 * i + 2);
+    key |= (uint64_t)((y >> i) & 1u) << (3 * i + 1);
+    key |= (uint64_t)((z >> i) & 1u) << (3 * i + 0);
+  }
+  return key;
+}
+
+// ---- Hilbert (Pointcept hilbert.encode, Skilling 2004), locs = (x,y,z) -> dims 0,1,2
+__device__ __forceinline__ uint64_t hilbert_encode(uint32_t x, uint32_t y, uint32_t z, int nb) {
+  uint32_t g[3] = {x & ((1u << nb) - 1u), y & ((1u << nb) - 1u), z & ((1u << nb) - 1u)};
+  for (int bit = 0; bit < nb; ++bit) {
+    const int pos = nb - 1 - bit;          // bit index (MSB-first position `bit`)
+    const uint32_t low = (1u << pos) - 1u;  // positions bit+1 .. nb-1 (lower bits)
+    for (int d = 0; d < 3; ++d) {
+      const uint32_t m = (g[d] >> pos) & 1u;
+      if (m) {
+        g[0] ^= low;
+      } else {
+        const uint32_t t = (g[0] ^ g[d]) & low;
+        g[d] ^= t;
+        g[0] ^= t;
+      }
+    }
+  }
+  // interleave MSB-first as [bit][dim] (dim 0 most significant in a triplet)
+  uint64_t gray = 0;
+  for (int k = 0; k < nb; ++k) {
+    const int pos = nb - 1 - k;
+    for (int d = 0; d < 3; ++d) gray = (gray << 1) | ((g[d] >> pos) & 1u);
+  }
+  // gray -> binary: prefix xor from the MSB
+  uint64_t b = gray;
+  b ^= b >> 1;
+  b ^= b >> 2;
+  b ^= b >> 4;
+  b ^= b >> 8;
+  b ^= b >> 16;
+  b ^= b >> 32;
+  return b;
+}
+
+__device__ __forceinline__ uint64_t encode_order(int type, int x, int y, int z, int depth) {
+  switch (type) {
+    case 0: return z_encode(x, y, z, depth);
+    case 1: return z_encode(y, x, z, depth);
+    case 2: return hilbert_encode(x, y, z, depth);
+    default: return hilbert_encode(y, x, z, depth);
+  }
+}
+
+__global__ void serialize_keys_kernel(int n, const int* __restrict__ grid, const int* __restrict__ batch, int depth,
+                                      int num_orders, int4 types, int code_bits, int64_t* __restrict__ codes,
+                                      uint64_t* __restrict__ keys) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int x = grid[3 * i], y = grid[3 * i + 1], z = grid[3 * i + 2];
+  const uint64_t b = batch ? (uint64_t)batch[i] : 0ull;
+  const int t[4] = {types.x, types.y, types.z, types.w};
+  for (int r = 0; r < num_orders; ++r) {
+    const uint64_t code = (b << (3 * depth)) | encode_order(t[r], x, y, z, depth);
+    codes[(long long)r * n + i] = (int64_t)code;
+    keys[(long long)r * n + i] = ((uint64_t)r << code_bits) | code;
+  }
+}
+
+// sorted positions of the R*n combined keys -> order[r][p], inverse[r][i]
+__global__ void serialize_finalize_kernel(int n, int R, const int* __restrict__ sorted_pos, int* __restrict__ order,
+                                          int* __restrict__ inverse) {
+  const long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= (long long)R * n) return;
+  const int r = (int)(q / n), p = (int)(q - (long long)r * n);
+  const int i = sorted_pos[q] - r * n;
+  order[q] = i;
+  inverse[(long long)r * n + i] = p;
+}
+
+// ---- pooling -------------------------------------------------------------
+__global__ void pool_flags_kernel(int n, const uint64_t* __restrict__ sorted_keys, int shift, int* __restrict__ flags) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  flags[p] = (p == 0 || (sorted_keys[p] >> shift) != (sorted_keys[p - 1] >> shift)) ? 1 : 0;
+}
+
+__global__ void pool_assign_kernel(int n, const int* __restrict__ sorted_idx, const int* __restrict__ cid_incl,
+                                   const int* __restrict__ flags, int* __restrict__ cluster, int* __restrict__ idx_ptr,
+                                   int* __restrict__ head) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  const int c = cid_incl[p] - 1;
+  const int src = sorted_idx[p];
+  cluster[src] = c;
+  if (flags[p]) {
+    idx_ptr[c] = p;
+    head[c] = src;
+  }
+  if (p == n - 1) idx_ptr[c + 1] = n;
+}
+
+// new codes / grid / batch of the pooled point; keys for the combined sort
+__global__ void pool_gather_kernel(int m, int n, int R, const int* __restrict__ head, const int64_t* __restrict__ codes,
+                                   int pd, const int* __restrict__ grid, const int* __restrict__ batch,
+                                   const float* __restrict__ coord, int code_bits, int64_t* __restrict__ new_codes,
+                                   uint64_t* __restrict__ keys, int* __restrict__ new_grid,
+                                   int* __restrict__ new_batch) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= m) return;
+  const int hd = head[c];
+  for (int r = 0; r < R; ++r) {
+    const uint64_t code = ((uint64_t)codes[(long long)r * n + hd]) >> (3 * pd);
+    new_codes[(long long)r * m + c] = (int64_t)code;
+    keys[(long long)r * m + c] = ((uint64_t)r << code_bits) | code;
+  }
+  for (int k = 0; k < 3; ++k) new_grid[3 * c + k] = grid[3 * hd + k] >> pd;
+  if (new_batch) new_batch[c] = batch ? batch[hd] : 0;
+}
+
+// max over each run of X rows (X = proj(feat), [n, C]) -> BN affine -> act   (segment_csr 'max' + norm + act)
+__global__ void segment_max_affine_act_kernel(int m, int C, const int* __restrict__ idx_ptr,
+                                              const int* __restrict__ sorted_idx, const float* __restrict__ X,
+                                              const float* __restrict__ scale, const float* __restrict__ shift,
+                                              int act, float* __restrict__ Y) {
+  const int c = blockIdx.x;
+  const int beg = idx_ptr[c], end = idx_ptr[c + 1];
+  for (int col = threadIdx.x; col < C; col += blockDim.x) {
+    float v = -INFINITY;
+    for (int p = beg; p < end; ++p) v = fmaxf(v, X[(long long)sorted_idx[p] * C + col]);
+    if (scale) v = v * scale[col] + shift[col];
+    if (act == 1) v = 0.5f * v * (1.f + erff(v * 0.70710678118654752f));
+    Y[(long long)c * C + col] = v;
+  }
+}
+
+__global__ void segment_mean_kernel(int m, int D, const int* __restrict__ idx_ptr, const int* __restrict__ sorted_idx,
+                                    const float* __restrict__ X, float* __restrict__ Y) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= m) return;
+  const int beg = idx_ptr[c], end = idx_ptr[c + 1];
+  for (int d = 0; d < D; ++d) {
+    float s = 0.f;
+    for (int p = beg; p < end; ++p) s += X[(long long)sorted_idx[p] * D + d];
+    Y[(long long)c * D + d] = s / (float)max(end - beg, 1);
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+// codes[R][n] (int64, batch << 3*depth | code) and keys[R*n] = r << code_bits | code for sfx_sort_pairs_u64.
+// order_types: 0 "z", 1 "z-trans", 2 "hilbert", 3 "hilbert-trans".
+int sfx_serialize_keys(int n, const int* grid_coord, const int* batch, int depth, int num_orders, int t0, int t1,
+                       int t2, int t3, int code_bits, int64_t* codes, uint64_t* keys, void* stream) {
+  SFX_REQUIRE(n >= 0 && num_orders >= 1 && num_orders <= 4, "sfx_serialize_keys: bad sizes");
+  SFX_REQUIRE(depth >= 1 && depth <= 16, "sfx_serialize_keys: depth must be in [1, 16]");
+  SFX_REQUIRE(code_bits + 2 <= 64, "sfx_serialize_keys: code_bits too large");
+  if (n == 0) return SFX_OK;
+  SFX_REQUIRE(grid_coord && codes && keys, "sfx_serialize_keys: null buffer");
+  serialize_keys_kernel<<<sfx::ceil_div(n, 256), 256, 0, sfx::as_stream(stream)>>>(
+      n, grid_coord, batch, depth, num_orders, make_int4(t0, t1, t2, t3), code_bits, codes, keys);
+  return sfx::check_launch("sfx_serialize_keys");
+}
+
+int sfx_serialize_finalize(int n, int num_orders, const int* sorted_pos, int* order, int* inverse, void* stream) {
+  SFX_REQUIRE(n >= 0 && num_orders >= 1, "sfx_serialize_finalize: bad sizes");
+  if (n == 0) return SFX_OK;
+  SFX_REQUIRE(sorted_pos && order && inverse, "sfx_serialize_finalize: null buffer");
+  const long long tot = (long long)n * num_orders;
+  serialize_finalize_kernel<<<sfx::ceil_div(tot, 256), 256, 0, sfx::as_stream(stream)>>>(n, num_orders, sorted_pos,
+                                                                                          order, inverse);
+  return sfx::check_launch("sfx_serialize_finalize");
+}
+
+int sfx_pool_flags(int n, const uint64_t* sorted_keys, int shift, int* flags, void* stream) {
+  SFX_REQUIRE(n >= 0 && shift >= 0 && shift < 64, "sfx_pool_flags: bad args");
+  if (n == 0) return SFX_OK;
+  SFX_REQUIRE(sorted_keys && flags, "sfx_pool_flags: null buffer");
+  pool_flags_kernel<<<sfx::ceil_div(n, 256), 256, 0, sfx::as_stream(stream)>>>(n, sorted_keys, shift, flags);
+  return sfx::check_launch("sfx_pool_flags");
+}
+
+int sfx_pool_assign(int n, const int* sorted_idx, const int* cid_inclusive, const int* flags, int* cluster,
+                    int* idx_ptr, int* head, void* stream) {
+  SFX_REQUIRE(n >= 0, "sfx_pool_assign: n < 0");
+  if (n == 0) return SFX_OK;
+  SFX_REQUIRE(sorted_idx && cid_inclusive && flags && cluster && idx_ptr && head, "sfx_pool_assign: null buffer");
+  pool_assign_kernel<<<sfx::ceil_div(n, 256), 256, 0, sfx::as_stream(stream)>>>(n, sorted_idx, cid_inclusive, flags,
+                                                                                 cluster, idx_ptr, head);
+  return sfx::check_launch("sfx_pool_assign");
+}
+
+int sfx_pool_gather(int m, int n, int num_orders, const int* head, const int64_t* codes, int pooling_depth,
+                    const int* grid_coord, const int* batch, int code_bits, int64_t* new_codes, uint64_t* keys,
+                    int* new_grid, int* new_batch, void* stream) {
+  SFX_REQUIRE(m >= 0 && n >= m && num_orders >= 1 && pooling_depth >= 0, "sfx_pool_gather: bad sizes");
+  if (m == 0) return SFX_OK;
+  SFX_REQUIRE(head && codes && grid_coord && new_codes && keys && new_grid, "sfx_pool_gather: null buffer");
+  pool_gather_kernel<<<sfx::ceil_div(m, 256), 256, 0, sfx::as_stream(stream)>>>(
+      m, n, num_orders, head, codes, pooling_depth, grid_coord, batch, nullptr, code_bits, new_codes, keys, new_grid,
+      new_batch);
+  return sfx::check_launch("sfx_pool_gather");
+}
+
+int sfx_segment_max_affine_act(int m, int C, const int* idx_ptr, const int* sorted_idx, const float* X,
+                               const float* scale, const float* shift, int act, float* Y, void* stream) {
+  SFX_REQUIRE(m >= 0 && C > 0 && (act == 0 || act == 1), "sfx_segment_max_affine_act: bad args");
+  if (m == 0) return SFX_OK;
+  SFX_REQUIRE(idx_ptr && sorted_idx && X && Y, "sfx_segment_max_affine_act: null buffer");
+  const int threads = C >= 256 ? 256 : (C >= 128 ? 128 : 64);
+  segment_max_affine_act_kernel<<<m, threads, 0, sfx::as_stream(stream)>>>(m, C, idx_ptr, sorted_idx, X, scale,
+                                                                          shift, act, Y);
+  return sfx::check_launch("sfx_segment_max_affine_act");
+}
+
+int sfx_segment_mean(int m, int D, const int* idx_ptr, const int* sorted_idx, const float* X, float* Y,
+                     void* stream) {
+  SFX_REQUIRE(m >= 0 && D > 0, "sfx_segment_mean: bad args");
+  if (m == 0) return SFX_OK;
+  SFX_REQUIRE(idx_ptr && sorted_idx && X && Y, "sfx_segment_mean: null buffer");
+  segment_mean_kernel<<<sfx::ceil_div(m, 256), 256, 0, sfx::as_stream(stream)>>>(m, D, idx_ptr, sorted_idx, X, Y);
+  return sfx::check_launch("sfx_segment_mean");
+}
+
+}  // extern "C"

@@ -67,23 +67,42 @@ def rasterize_gaussians_to_singleimg(gs_params, camera_to_world, cx, cy, fx, fy,
     return _render_fused(gs_params, camera_to_world, cx, cy, fx, fy, W, H, background_color)
 
 
+def _rowptr(t: Tensor, width: int):
+    """(pointer, row stride) of an [N, ...] attribute whose per-row `width` floats are contiguous."""
+    t2 = t.reshape(t.shape[0], -1) if t.is_contiguous() else t
+    if t2.dim() == 3:  # e.g. features_rest view [N, K, 3] of a packed record
+        if t2.stride(2) == 1 and t2.stride(1) == 3:
+            return t2.data_ptr(), t2.stride(0), t2
+        t2 = t2.contiguous().reshape(t.shape[0], -1)
+    if t2.dim() == 2 and t2.stride(1) == 1 and t2.shape[1] == width:
+        return t2.data_ptr(), t2.stride(0), t2
+    t2 = t.contiguous().reshape(t.shape[0], -1)
+    return t2.data_ptr(), t2.stride(0), t2
+
+
 def _render_fused(gs, c2w, cx, cy, fx, fy, W, H, background):
-    means = gs["means"].contiguous()
+    means = gs["means"]
     _lib.require_gpu(means)
     dev = means.device
     n = means.shape[0]
-    dc = gs["features_dc"].contiguous()
     rest = gs.get("features_rest")
     nb = 1 + (rest.shape[1] if rest is not None else 0)
+    keep = []
+    pm, lm, t = _rowptr(means, 3); keep.append(t)
+    ps, ls, t = _rowptr(gs["scales"], 3); keep.append(t)
+    pq, lq, t = _rowptr(gs["quats"], 4); keep.append(t)
+    po, lo, t = _rowptr(gs["opacities"], 1); keep.append(t)
+    pd, ldc, t = _rowptr(gs["features_dc"], 3); keep.append(t)
+    pr, lr = None, 0
     if rest is not None:
-        rest = rest.contiguous()
+        pr, lr, t = _rowptr(rest, 3 * (nb - 1)); keep.append(t)
     c2w = c2w.detach().float().contiguous()
     f = lambda *s, dt=torch.float32: torch.empty(*s, device=dev, dtype=dt)
     viewmat, rgbs, opac = f(3, 4), f(n, 3), f(n, 1)
     xys, depths, radii, conics, tiles = f(n, 2), f(n), f(n, dt=torch.int32), f(n, 3), f(n, dt=torch.int32)
-    call("sfx_render_prep_project", n, nb, ptr(means), ptr(gs["scales"].contiguous()), ptr(gs["quats"].contiguous()),
-         ptr(gs["opacities"].contiguous()), ptr(dc), ptr(rest), ptr(c2w), fx, fy, cx, cy, H, W, BLOCK_WIDTH,
-         ptr(viewmat), ptr(rgbs), ptr(opac), ptr(xys), ptr(depths), ptr(radii), ptr(conics), ptr(tiles), stream())
+    call("sfx_render_prep_project", n, nb, pm, lm, ps, ls, pq, lq, po, lo, pd, ldc, pr, lr, ptr(c2w), fx, fy, cx, cy,
+         H, W, BLOCK_WIDTH, ptr(viewmat), ptr(rgbs), ptr(opac), ptr(xys), ptr(depths), ptr(radii), ptr(conics),
+         ptr(tiles), stream())
     bg = background.to(device=dev, dtype=torch.float32).contiguous()
     rgb, alpha = _RasterizeGaussians.apply(xys, depths, radii, conics, tiles, rgbs, opac, H, W, BLOCK_WIDTH, bg, True)
     rgb = torch.clamp(rgb, max=1.0)

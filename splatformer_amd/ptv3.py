@@ -1,0 +1,364 @@
+"""PointTransformerV3Model on MI355X: module tree of the reference, HIP forward.
+
+Mirrors reference models/pointtransformer_v3.py:81-392 (the SplatFormer
+assembly of Pointcept's PTv3 m1): same constructor arguments, same
+submodule names and therefore the same state-dict keys
+(`backbone.embedding.0.weight`, `backbone.enc.enc0.block0.cpe.0.weight`
+([Cout,3,3,3,Cin] spconv layout), `...attn.qkv.weight`, `...mlp.0.fc1.weight`,
+`backbone.dec.dec0.up.proj_skip.1.running_var`, ...), and
+`forward(data_dict) -> Point` with `point["feat"]` the [N, dec_channels[0]]
+feature the FeaturePredictor reads (feature_predictor.py:184-188).
+
+The nn modules only hold parameters; forward runs entirely on libsfx HIP
+kernels (serialization radix sort, 27-neighbour hash map, fp32 MFMA GEMMs
+with fused gather/BN/GELU/residual, windowed attention, pooling runs).
+Eval/inference only in this build (the reference's eval path runs under
+torch.no_grad(), train.py:81); the training backward of the refiner is not
+implemented yet and calling forward with autograd-tracked parameters raises.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional, Sequence
+
+import torch
+import torch.nn as nn
+from torch import Tensor
+
+from . import _lib
+from . import ptv3_ops as ops
+
+ORDERS = ("z", "z-trans", "hilbert", "hilbert-trans")
+
+
+class Point(dict):
+    """addict-style dict (Pointcept `Point`) with attribute access."""
+
+    def __getattr__(self, k):
+        try:
+            return self[k]
+        except KeyError as e:
+            raise AttributeError(k) from e
+
+    def __setattr__(self, k, v):
+        self[k] = v
+
+
+class SubMConv3d(nn.Module):
+    """Parameter holder with spconv.SubMConv3d(C, C, kernel_size=3, bias=True) layout: weight [Cout,3,3,3,Cin]."""
+
+    def __init__(self, in_channels, out_channels, kernel_size=3, bias=True, indice_key=None):
+        super().__init__()
+        assert kernel_size == 3
+        self.in_channels, self.out_channels, self.indice_key = in_channels, out_channels, indice_key
+        self.weight = nn.Parameter(torch.empty(out_channels, 3, 3, 3, in_channels))
+        self.bias = nn.Parameter(torch.empty(out_channels)) if bias else None
+        fan_in = in_channels * 27
+        bound = 1.0 / math.sqrt(fan_in)
+        nn.init.uniform_(self.weight, -math.sqrt(3.0) * bound, math.sqrt(3.0) * bound)
+        if self.bias is not None:
+            nn.init.uniform_(self.bias, -bound, bound)
+
+
+class PointSequential(nn.Sequential):
+    pass
+
+
+class MLP(nn.Module):
+    def __init__(self, in_channels, hidden_channels, out_channels):
+        super().__init__()
+        self.fc1 = nn.Linear(in_channels, hidden_channels)
+        self.act = nn.GELU()
+        self.fc2 = nn.Linear(hidden_channels, out_channels)
+        self.drop = nn.Dropout(0.0)
+
+
+class SerializedAttention(nn.Module):
+    def __init__(self, channels, num_heads, patch_size, order_index=0):
+        super().__init__()
+        assert channels % num_heads == 0
+        self.channels, self.num_heads = channels, num_heads
+        self.scale = (channels // num_heads) ** -0.5
+        self.order_index = order_index
+        self.patch_size_max = patch_size
+        self.qkv = nn.Linear(channels, channels * 3, bias=True)
+        self.proj = nn.Linear(channels, channels)
+        self.attn_drop = nn.Dropout(0.0)
+        self.proj_drop = nn.Dropout(0.0)
+        self.softmax = nn.Softmax(dim=-1)
+
+
+class Block(nn.Module):
+    def __init__(self, channels, num_heads, patch_size=128, mlp_ratio=4.0, order_index=0, cpe_indice_key=None):
+        super().__init__()
+        self.channels = channels
+        self.pre_norm = True
+        self.cpe = PointSequential(SubMConv3d(channels, channels, 3, True, cpe_indice_key),
+                                   nn.Linear(channels, channels), nn.LayerNorm(channels))
+        self.norm1 = PointSequential(nn.LayerNorm(channels))
+        self.attn = SerializedAttention(channels, num_heads, patch_size, order_index)
+        self.norm2 = PointSequential(nn.LayerNorm(channels))
+        self.mlp = PointSequential(MLP(channels, int(channels * mlp_ratio), channels))
+        self.drop_path = PointSequential(nn.Identity())
+
+    def run(self, point: Point, conv_in: Optional[Tensor] = None, out: Optional[Tensor] = None) -> Point:
+        """Block.forward (calflops.py:45-82): x += LN(Lin(SubMConv(x))); x += attn(LN1 x); x += MLP(LN2 x)."""
+        x = point.feat
+        C = self.channels
+        conv, lin, ln_c = self.cpe[0], self.cpe[1], self.cpe[2]
+        t = ops.linear(x if conv_in is None else conv_in, conv.weight.reshape(C, 27 * C), conv.bias,
+                       gather_idx=point.nbr)
+        t = ops.linear(t, lin.weight, lin.bias)
+        ln1 = self.norm1[0]
+        x1, h = ops.cpe_residual_ln(t, x, ln_c.weight, ln_c.bias, ln1.weight, ln1.bias, ln1.eps)
+        qkv = ops.linear(h, self.attn.qkv.weight, self.attn.qkv.bias)
+        K, win, nw = point_windows(point, self.attn.patch_size_max)
+        oi = point.order_type[self.attn.order_index]
+        a = ops.window_attention(qkv, point.order_phys[oi], win, nw, K, self.attn.num_heads, C)
+        x2 = ops.linear(a, self.attn.proj.weight, self.attn.proj.bias, residual=x1)
+        ln2 = self.norm2[0]
+        h2 = ops.layernorm(x2, ln2.weight, ln2.bias, ln2.eps)
+        mlp = self.mlp[0]
+        m = ops.linear(h2, mlp.fc1.weight, mlp.fc1.bias, act=ops.ACT_GELU)
+        point.feat = ops.linear(m, mlp.fc2.weight, mlp.fc2.bias, residual=x2, out=out)
+        return point
+
+
+def bn_affine(bn: nn.BatchNorm1d):
+    """Eval BatchNorm1d as per-channel (scale, shift): y = x*scale + shift (cached until a tensor changes)."""
+    ts = (bn.weight, bn.bias, bn.running_mean, bn.running_var)
+    key = tuple((t.data_ptr(), t._version) for t in ts) + (bn.eps,)
+    cache = getattr(bn, "_sfx_affine", None)
+    if cache is not None and cache[0] == key:
+        return cache[1]
+    with torch.no_grad():
+        scale = bn.weight / torch.sqrt(bn.running_var + bn.eps)
+        shift = bn.bias - bn.running_mean * scale
+    val = (scale.detach().contiguous(), shift.detach().contiguous())
+    object.__setattr__(bn, "_sfx_affine", (key, val))
+    return val
+
+
+class SerializedPooling(nn.Module):
+    def __init__(self, in_channels, out_channels, stride=2, norm_layer=None, act_layer=None):
+        super().__init__()
+        assert stride == 2 ** (math.ceil(stride) - 1).bit_length()
+        self.stride = stride
+        self.proj = nn.Linear(in_channels, out_channels)
+        self.norm = PointSequential(norm_layer(out_channels))
+        self.act = PointSequential(act_layer())
+
+    def run(self, point: Point, perm: Sequence[int]) -> Point:
+        pd = (math.ceil(self.stride) - 1).bit_length()
+        if pd > point.serialized_depth:
+            pd = 0
+        dev = point.feat.device
+        row0 = point.order_type[0]
+        sidx, cluster, idx_ptr, head, m = ops.pool_clusters(point.codes_phys[row0], pd, point.code_bits)
+        depth = point.serialized_depth - pd
+        code_bits = point.code_bits - 3 * pd
+        codes, order, inverse, grid, batch = ops.pool_gather(head, m, point.codes_phys, pd, point.grid_coord,
+                                                             point.get("batch"), code_bits)
+        pf = ops.linear(point.feat, self.proj.weight, self.proj.bias)
+        sc, sh = bn_affine(self.norm[0])
+        feat = ops.segment_max_affine_act(pf, idx_ptr, sidx, m, sc, sh, ops.ACT_GELU)
+        coord = ops.segment_mean(point.coord, idx_ptr, sidx, m)
+        new = Point(feat=feat, coord=coord, grid_coord=grid, codes_phys=codes, order_phys=order,
+                    inverse_phys=inverse, order_type=[point.order_type[p] for p in perm],
+                    serialized_depth=depth, code_bits=code_bits, pooling_inverse=cluster, pooling_parent=point)
+        if batch is not None:
+            new.batch = batch
+            new.offset = torch.cumsum(torch.bincount(batch.long().cpu(), minlength=len(point.offset)), 0).tolist()
+        else:
+            new.offset = [m]
+        new.nbr = ops.subm_neighbors(grid, new.get("batch"))
+        return new
+
+
+class SerializedUnpooling(nn.Module):
+    def __init__(self, in_channels, skip_channels, out_channels, norm_layer=None, act_layer=None):
+        super().__init__()
+        self.proj = PointSequential(nn.Linear(in_channels, out_channels), norm_layer(out_channels), act_layer())
+        self.proj_skip = PointSequential(nn.Linear(skip_channels, out_channels), norm_layer(out_channels),
+                                         act_layer())
+
+    def run(self, point: Point) -> Point:
+        parent = point.pop("pooling_parent")
+        inverse = point.pop("pooling_inverse")
+        sc, sh = bn_affine(self.proj[1])
+        coarse = ops.linear(point.feat, self.proj[0].weight, self.proj[0].bias, scale=sc, shift=sh, act=ops.ACT_GELU)
+        sc2, sh2 = bn_affine(self.proj_skip[1])
+        skip = torch.empty(parent.feat.shape[0], coarse.shape[1], device=coarse.device)
+        parent.feat = ops.linear(parent.feat, self.proj_skip[0].weight, self.proj_skip[0].bias, scale=sc2, shift=sh2,
+                                 act=ops.ACT_GELU, residual=coarse, residual_idx=inverse, pre_out=skip)
+        # Pointcept quirk: SerializedUnpooling does not refresh sparse_conv_feat, so the next Block's
+        # SubMConv3d sees proj_skip(parent) only (PointSequential semantics, pointtransformer_v3.py:52-79)
+        parent.stale_conv_feat = skip
+        return parent
+
+
+def point_windows(point: Point, patch_size_max: int):
+    """K = min(min bincount, patch_size_max) and the device window table (cached per Point)."""
+    counts = [b - a for a, b in zip([0] + list(point.offset[:-1]), point.offset)]
+    K = min(min(counts), patch_size_max)
+    key = ("win", K)
+    if key not in point:
+        tab = ops.window_table(point.offset, K)
+        t = torch.tensor(tab, dtype=torch.int32).reshape(-1, 2)
+        point[key] = (t.to(point.feat.device, non_blocking=False), len(tab))
+    win, nw = point[key]
+    return K, win, nw
+
+
+class _Container(nn.Module):
+    def add(self, module, name):
+        self.add_module(name, module)
+
+
+class PointTransformerV3(nn.Module):
+    def __init__(self, in_channels=6, order=ORDERS, stride=(2, 2, 2, 2), enc_depths=(2, 2, 2, 6, 2),
+                 enc_channels=(32, 64, 128, 256, 512), enc_num_head=(2, 4, 8, 16, 32),
+                 enc_patch_size=(48, 48, 48, 48, 48), dec_depths=(2, 2, 2, 2), dec_channels=(64, 64, 128, 256),
+                 dec_num_head=(4, 4, 8, 16), dec_patch_size=(48, 48, 48, 48), mlp_ratio=4, turn_off_bn=False,
+                 shuffle_orders=True, embedding_type="MLP"):
+        super().__init__()
+        if turn_off_bn:
+            raise NotImplementedError("turn_off_bn=True is not on the SplatFormer path (ptv3_base.gin:30)")
+        if embedding_type != "MLP":
+            raise NotImplementedError("only embedding_type='MLP' (ptv3_base.gin:32) is on the path")
+        self.num_stages = len(enc_depths)
+        self.order = [order] if isinstance(order, str) else list(order)
+        self.shuffle_orders = shuffle_orders
+        self.enc_channels, self.dec_channels = list(enc_channels), list(dec_channels)
+        assert self.num_stages == len(stride) + 1 == len(enc_channels) == len(enc_num_head)
+        bn_layer = lambda c: nn.BatchNorm1d(c, eps=1e-3, momentum=0.01)
+        self.embedding = PointSequential(nn.Linear(in_channels, enc_channels[0]), bn_layer(enc_channels[0]),
+                                         nn.GELU())
+        self.enc = _Container()
+        for s in range(self.num_stages):
+            enc = _Container()
+            if s > 0:
+                enc.add(SerializedPooling(enc_channels[s - 1], enc_channels[s], stride[s - 1], bn_layer, nn.GELU),
+                        "down")
+            for i in range(enc_depths[s]):
+                enc.add(Block(enc_channels[s], enc_num_head[s], enc_patch_size[s], mlp_ratio, i % len(self.order),
+                              f"stage{s}"), f"block{i}")
+            self.enc.add(enc, f"enc{s}")
+        self.dec = _Container()
+        dch = list(dec_channels) + [enc_channels[-1]]
+        for s in reversed(range(self.num_stages - 1)):
+            dec = _Container()
+            dec.add(SerializedUnpooling(dch[s + 1], enc_channels[s], dch[s], bn_layer, nn.GELU), "up")
+            for i in range(dec_depths[s]):
+                dec.add(Block(dch[s], dec_num_head[s], dec_patch_size[s], mlp_ratio, i % len(self.order),
+                              f"stage{s}"), f"block{i}")
+            self.dec.add(dec, f"dec{s}")
+        self.last_perms: List[List[int]] = []
+
+    def _draw_perm(self, perms_override, k):
+        if perms_override is not None:
+            p = list(perms_override[k])
+        elif self.shuffle_orders:
+            p = torch.randperm(len(self.order)).tolist()  # same RNG draw as Point.serialization / pooling
+        else:
+            p = list(range(len(self.order)))
+        self.last_perms.append(p)
+        return p
+
+    @torch.no_grad()
+    def forward(self, data_dict, perms: Optional[List[Sequence[int]]] = None, out: Optional[Tensor] = None) -> Point:
+        feat = data_dict["feat"]
+        _lib.require_gpu(feat)
+        dev = feat.device
+        offset = data_dict["offset"]
+        offset = offset.tolist() if isinstance(offset, Tensor) else list(offset)
+        grid = data_dict["grid_coord"]
+        grid = grid if grid.dtype == torch.int32 else grid.int()
+        grid = grid.contiguous()
+        n = feat.shape[0]
+        B = len(offset)
+        batch = None
+        if B > 1:
+            batch = torch.empty(n, device=dev, dtype=torch.int32)
+            offs = torch.tensor(offset, dtype=torch.int64, device=dev)
+            _lib.call("sfx_offsets_to_batch", n, B, offs.data_ptr(), batch.data_ptr(), _lib.stream())
+        depth = int(data_dict["serialized_depth"]) if "serialized_depth" in data_dict else \
+            int(grid.max().item()).bit_length()
+        assert depth * 3 + len(offset).bit_length() <= 63 and depth <= 16
+        code_bits = 3 * depth + max(0, (B - 1).bit_length())
+        self.last_perms = []
+        codes, order, inverse = ops.serialize(grid, batch, depth, code_bits, self.order)
+        p0 = self._draw_perm(perms, 0)
+        point = Point(coord=data_dict["coord"].float().contiguous(), grid_coord=grid, offset=offset, codes_phys=codes,
+                      order_phys=order, inverse_phys=inverse, order_type=p0, serialized_depth=depth,
+                      code_bits=code_bits)
+        if batch is not None:
+            point.batch = batch
+        point.nbr = ops.subm_neighbors(grid, batch)
+        emb, bnm = self.embedding[0], self.embedding[1]
+        sc, sh = bn_affine(bnm)
+        point.feat = ops.linear(feat, emb.weight, emb.bias, scale=sc, shift=sh, act=ops.ACT_GELU)
+        k = 1
+        for s in range(self.num_stages):
+            stage = getattr(self.enc, f"enc{s}")
+            for name, mod in stage.named_children():
+                if name == "down":
+                    point = mod.run(point, self._draw_perm(perms, k))
+                    k += 1
+                else:
+                    point = mod.run(point)
+        dec_names = [f"dec{s}" for s in reversed(range(self.num_stages - 1))]
+        for di, dn in enumerate(dec_names):
+            stage = getattr(self.dec, dn)
+            children = list(stage.named_children())
+            for ci, (name, mod) in enumerate(children):
+                if name == "up":
+                    point = mod.run(point)
+                else:
+                    conv_in = point.pop("stale_conv_feat", None)
+                    last = di == len(dec_names) - 1 and ci == len(children) - 1
+                    point = mod.run(point, conv_in=conv_in, out=out if last else None)
+        return point
+
+
+class PointTransformerV3Model(nn.Module):
+    """reference models/pointtransformer_v3.py:81-182 (gin-configurable assembly), ptv3_base.gin defaults."""
+
+    def __init__(self, in_channels, enable_flash=False, enc_dim=64, output_dim=96, turn_off_bn=False,
+                 stride=(1, 2, 2, 2), embedding_type="MLP", enc_depths=(2, 2, 2, 6, 2), enc_num_head=(2, 4, 8, 16, 32),
+                 dec_depths=(2, 2, 2, 2), dec_num_head=(4, 4, 8, 16), dec_channels=None, enc_channels=None,
+                 pdnorm_bn=False, pdnorm_ln=False, pretrained_ckpt=None, additional_info=None):
+        super().__init__()
+        if pdnorm_bn or pdnorm_ln:
+            raise NotImplementedError("PDNorm is not on the SplatFormer path")
+        if additional_info and additional_info.get("tome") not in (None, "base") or \
+                (additional_info and float(additional_info.get("r", 0.0)) != 0.0):
+            raise NotImplementedError("token merging variants are out of scope (SURVEY.md §2); base r=0 only")
+        if dec_channels is None:
+            dec_channels = {64: (64, 64, 128, 256), 128: (128, 128, 256, 256), 96: (96, 96, 128, 256)}.get(output_dim)
+            if dec_channels is None:
+                raise ValueError("Unsupported output_dim")
+        if enc_channels is None:
+            enc_channels = {32: (32, 64, 128, 256, 512), 64: (64, 96, 128, 256, 512)}.get(enc_dim)
+            if enc_channels is None:
+                raise ValueError("Unsupported enc_dim")
+        self.dec_channels = tuple(dec_channels)
+        # the HIP attention kernel implements both paths with the non-flash math; flash would use K=1024
+        patch = 1024 if enable_flash else 128
+        self.backbone = PointTransformerV3(
+            in_channels=in_channels, order=ORDERS, stride=stride, enc_depths=enc_depths, enc_channels=enc_channels,
+            enc_num_head=enc_num_head, enc_patch_size=(patch,) * len(enc_channels), dec_depths=dec_depths,
+            dec_channels=dec_channels, dec_num_head=dec_num_head, dec_patch_size=(patch,) * len(dec_channels),
+            mlp_ratio=4, turn_off_bn=turn_off_bn, shuffle_orders=True, embedding_type=embedding_type)
+        if enable_flash:
+            raise NotImplementedError("enable_flash=True (K=1024 windows) exceeds the 128-key window kernel")
+        self.output_dim = self.dec_channels[0]
+        if pretrained_ckpt is not None:
+            sd = torch.load(pretrained_ckpt, map_location="cpu", weights_only=True)["state_dict"]
+            sd = {k.replace("module.backbone.", ""): v for k, v in sd.items() if "backbone." in k}
+            own = self.backbone.state_dict()
+            load = {k: v for k, v in sd.items() if k in own and own[k].shape == v.shape}
+            self.backbone.load_state_dict(load, strict=False)
+
+    def forward(self, x, perms=None, out=None):
+        return self.backbone(x, perms=perms, out=out)

@@ -1,1 +1,265 @@
-"""PTv3 device ops (placeholder; filled in with the PTv3 kernels)."""
+"""Device ops of the PTv3 refiner: thin typed wrappers over the libsfx C-ABI.
+
+Every function allocates its outputs with torch (device memory plumbing) and
+launches HIP kernels on the current stream.  No torch compute ops and no CPU
+fallback: a missing library or a CPU tensor raises.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+from torch import Tensor
+
+from . import _lib
+from ._lib import I, L, P, F, Z, call, ptr, stream
+
+_lib.register("sfx_linear", [I, I, I, P, L, P, I, P, L, P, P, P, I, I, P, L, P, P, L, P, L, I, L, L, L, L, P])
+_lib.register("sfx_layernorm", [I, I, P, L, P, P, F, P, L, P])
+_lib.register("sfx_cpe_residual_ln", [I, I, P, P, P, P, P, P, F, P, P, P])
+_lib.register("sfx_window_attention", [I, I, I, I, I, P, P, P, F, P, P])
+_lib.register("sfx_serialize_keys", [I, P, P, I, I, I, I, I, I, I, P, P, P])
+_lib.register("sfx_serialize_finalize", [I, I, P, P, P, P])
+_lib.register("sfx_pool_flags", [I, P, I, P, P])
+_lib.register("sfx_pool_assign", [I, P, P, P, P, P, P, P])
+_lib.register("sfx_pool_gather", [I, I, I, P, P, I, P, P, I, P, P, P, P, P])
+_lib.register("sfx_segment_max_affine_act", [I, I, P, P, P, P, P, I, P, P])
+_lib.register("sfx_segment_mean", [I, I, P, P, P, P, P])
+_lib.register("sfx_subm_table_log2", [I])
+_lib.register("sfx_subm_neighbors", [I, P, P, I, P, P, P, P])
+_lib.register("sfx_gs_pack", [I, P, L, P, L, P, L, P, L, P, L, P, L, I, F, P, L, P, P, P])
+_lib.register("sfx_offsets_to_batch", [I, I, P, P, P])
+
+ACT_NONE, ACT_GELU, ACT_RELU, ACT_TANH = 0, 1, 2, 3
+ORDER_TYPES = {"z": 0, "z-trans": 1, "hilbert": 2, "hilbert-trans": 3}
+
+
+def _rows(t: Tensor) -> Tuple[int, int]:
+    """(pointer, leading dimension) of a 2-D row-major (possibly column-sliced) float32 matrix."""
+    if t.dim() != 2 or t.stride(1) != 1:
+        raise RuntimeError("expected a 2-D tensor with unit column stride")
+    if not t.is_cuda:
+        raise RuntimeError("expected a device tensor")
+    if t.dtype != torch.float32:
+        raise RuntimeError(f"expected float32, got {t.dtype}")
+    return t.data_ptr(), t.stride(0)
+
+
+def linear(x: Tensor, weight: Tensor, bias: Optional[Tensor] = None, *, act: int = ACT_NONE, act_ncols: int = -1,
+           scale: Optional[Tensor] = None, shift: Optional[Tensor] = None, residual: Optional[Tensor] = None,
+           residual_idx: Optional[Tensor] = None, out: Optional[Tensor] = None, pre_out: Optional[Tensor] = None,
+           gather_idx: Optional[Tensor] = None, rows: Optional[int] = None) -> Tensor:
+    """y = act((x W^T + b) * scale + shift) + residual[residual_idx]  (fp32 MFMA GEMM, csrc/gemm.hip).
+
+    With `gather_idx` [M, S] (int32, -1 = empty) the A operand is the implicit
+    concatenation of S gathered rows of `x` (SubMConv3d as implicit GEMM)."""
+    N, K = weight.shape
+    if gather_idx is not None:
+        M = gather_idx.shape[0]
+        S = gather_idx.shape[1]
+        if K != S * x.shape[1]:
+            raise RuntimeError("gathered linear: weight K must be segments * x.shape[1]")
+    else:
+        M = x.shape[0] if rows is None else rows
+        S = 1
+        if x.shape[1] != K:
+            raise RuntimeError(f"linear: x has {x.shape[1]} features, weight expects {K}")
+    if out is None:
+        out = torch.empty(M, N, device=weight.device, dtype=torch.float32)
+    pa, lda = _rows(x)
+    pw, ldw = _rows(weight)
+    py, ldy = _rows(out)
+    pr, ldr = _rows(residual) if residual is not None else (None, 0)
+    pp, ldp = _rows(pre_out) if pre_out is not None else (None, 0)
+    call("sfx_linear", M, N, K, pa, lda, ptr(gather_idx), S, pw, ldw, ptr(bias), ptr(scale), ptr(shift), act,
+         act_ncols, pr, ldr, ptr(residual_idx), py, ldy, pp, ldp, 1, 0, 0, 0, 0, stream())
+    return out
+
+
+def grouped_linear(x: Tensor, weight: Tensor, bias: Tensor, groups: int, *, act: int = ACT_NONE,
+                   out: Optional[Tensor] = None) -> Tensor:
+    """Block-diagonal linear: x [M, G*K] -> [M, G*N] with weight [G, N, K], bias [G, N] (one launch)."""
+    G, N, K = weight.shape
+    M = x.shape[0]
+    if out is None:
+        out = torch.empty(M, G * N, device=x.device, dtype=torch.float32)
+    pa, lda = _rows(x)
+    py, ldy = _rows(out)
+    call("sfx_linear", M, N, K, pa, lda, None, 1, ptr(weight), K, ptr(bias), None, None, act, -1, None, 0, None, py,
+         ldy, None, 0, G, K, N * K, N, N, stream())
+    return out
+
+
+def layernorm(x: Tensor, gamma: Tensor, beta: Tensor, eps: float, out: Optional[Tensor] = None) -> Tensor:
+    M, C = x.shape
+    if out is None:
+        out = torch.empty(M, C, device=x.device, dtype=torch.float32)
+    px, ldx = _rows(x)
+    py, ldy = _rows(out)
+    call("sfx_layernorm", M, C, px, ldx, ptr(gamma), ptr(beta), float(eps), py, ldy, stream())
+    return out
+
+
+def cpe_residual_ln(t: Tensor, x: Tensor, g_cpe: Tensor, b_cpe: Tensor, g1: Tensor, b1: Tensor, eps: float,
+                    x_out: Optional[Tensor] = None) -> Tuple[Tensor, Tensor]:
+    """x' = x + LN_cpe(t); h = LN_norm1(x')  (Block cpe tail + shortcut + norm1)."""
+    M, C = x.shape
+    x_out = torch.empty_like(x) if x_out is None else x_out
+    h = torch.empty_like(x)
+    call("sfx_cpe_residual_ln", M, C, ptr(t), ptr(x), ptr(g_cpe), ptr(b_cpe), ptr(g1), ptr(b1), float(eps),
+         ptr(x_out), ptr(h), stream())
+    return x_out, h
+
+
+def window_table(offsets: Sequence[int], K: int) -> List[Tuple[int, int]]:
+    """Pointcept get_padding_and_inverse as (key_start, query_start) windows over serialized positions."""
+    tab = []
+    start = 0
+    for end in offsets:
+        n = end - start
+        nw = (n + K - 1) // K
+        for w in range(nw):
+            ks = start + w * K
+            qs = ks
+            if ks + K > end:  # ragged last window: padded with the preceding real points
+                ks = end - K
+            tab.append((ks, qs))
+        start = end
+    return tab
+
+
+def window_attention(qkv: Tensor, order: Tensor, win: Tensor, num_windows: int, K: int, heads: int, channels: int,
+                     out: Optional[Tensor] = None) -> Tensor:
+    n = qkv.shape[0]
+    d = channels // heads
+    if out is None:
+        out = torch.empty(n, channels, device=qkv.device, dtype=torch.float32)
+    call("sfx_window_attention", num_windows, K, heads, d, channels, ptr(qkv), ptr(order, torch.int32),
+         ptr(win, torch.int32), float(d ** -0.5), ptr(out), stream())
+    return out
+
+
+def _sort(keys: Tensor, vals: Optional[Tensor], begin: int, end: int) -> Tuple[Tensor, Tensor]:
+    n = keys.shape[0]
+    ko = torch.empty_like(keys)
+    vo = torch.empty(n, device=keys.device, dtype=torch.int32)
+    ws = _lib.workspace(_lib.fn("sfx_sort_workspace_bytes")(n), keys.device)
+    call("sfx_sort_pairs_u64", n, ptr(keys), ptr(vals), ptr(ko), ptr(vo), begin, end, ptr(ws), ws.numel(), stream())
+    return ko, vo
+
+
+def _finalize(keys: Tensor, n: int, R: int, code_bits: int) -> Tuple[Tensor, Tensor]:
+    _, pos = _sort(keys, None, 0, code_bits + 2)
+    order = torch.empty(R, n, device=keys.device, dtype=torch.int32)
+    inverse = torch.empty(R, n, device=keys.device, dtype=torch.int32)
+    call("sfx_serialize_finalize", n, R, ptr(pos), ptr(order), ptr(inverse), stream())
+    return order, inverse
+
+
+def serialize(grid_coord: Tensor, batch: Optional[Tensor], depth: int, code_bits: int,
+              orders: Sequence[str]) -> Tuple[Tensor, Tensor, Tensor]:
+    """Codes [R,n] int64 + stable argsort order / inverse [R,n] int32 for every order type (one radix sort)."""
+    n = grid_coord.shape[0]
+    R = len(orders)
+    t = [ORDER_TYPES[o] for o in orders] + [0] * (4 - R)
+    codes = torch.empty(R, n, device=grid_coord.device, dtype=torch.int64)
+    keys = torch.empty(R * n, device=grid_coord.device, dtype=torch.int64)
+    call("sfx_serialize_keys", n, ptr(grid_coord, torch.int32), ptr(batch), depth, R, t[0], t[1], t[2], t[3],
+         code_bits, ptr(codes), ptr(keys), stream())
+    order, inverse = _finalize(keys, n, R, code_bits)
+    return codes, order, inverse
+
+
+def scan_i32(x: Tensor, inclusive: bool = True) -> Tuple[Tensor, Tensor]:
+    n = x.shape[0]
+    out = torch.empty_like(x)
+    total = torch.zeros(1, device=x.device, dtype=torch.int32)
+    ws = _lib.workspace(_lib.fn("sfx_scan_workspace_bytes")(n), x.device)
+    call("sfx_scan_i32", n, ptr(x), ptr(out), 1 if inclusive else 0, ptr(ws), ws.numel(), ptr(total), stream())
+    return out, total
+
+
+def pool_clusters(code_row: Tensor, pooling_depth: int, code_bits: int):
+    """torch.unique(code >> 3pd) + sort(cluster) on device: returns (sorted_idx, cluster, idx_ptr, head, m)."""
+    n = code_row.shape[0]
+    dev = code_row.device
+    sk, sidx = _sort(code_row, None, 3 * pooling_depth, code_bits)
+    flags = torch.empty(n, device=dev, dtype=torch.int32)
+    call("sfx_pool_flags", n, ptr(sk), 3 * pooling_depth, ptr(flags), stream())
+    cid, total = scan_i32(flags)
+    m = int(total.item())  # host sync: the pooled point count sizes every later buffer
+    cluster = torch.empty(n, device=dev, dtype=torch.int32)
+    idx_ptr = torch.empty(m + 1, device=dev, dtype=torch.int32)
+    head = torch.empty(m, device=dev, dtype=torch.int32)
+    call("sfx_pool_assign", n, ptr(sidx), ptr(cid), ptr(flags), ptr(cluster), ptr(idx_ptr), ptr(head), stream())
+    return sidx, cluster, idx_ptr, head, m
+
+
+def pool_gather(head: Tensor, m: int, codes: Tensor, pooling_depth: int, grid_coord: Tensor, batch: Optional[Tensor],
+                code_bits: int):
+    R, n = codes.shape
+    dev = codes.device
+    new_codes = torch.empty(R, m, device=dev, dtype=torch.int64)
+    keys = torch.empty(R * m, device=dev, dtype=torch.int64)
+    new_grid = torch.empty(m, 3, device=dev, dtype=torch.int32)
+    new_batch = torch.empty(m, device=dev, dtype=torch.int32) if batch is not None else None
+    call("sfx_pool_gather", m, n, R, ptr(head), ptr(codes), pooling_depth, ptr(grid_coord), ptr(batch), code_bits,
+         ptr(new_codes), ptr(keys), ptr(new_grid), ptr(new_batch), stream())
+    order, inverse = _finalize(keys, m, R, code_bits)
+    return new_codes, order, inverse, new_grid, new_batch
+
+
+def segment_max_affine_act(x: Tensor, idx_ptr: Tensor, sorted_idx: Tensor, m: int, scale: Optional[Tensor],
+                           shift: Optional[Tensor], act: int) -> Tensor:
+    C = x.shape[1]
+    out = torch.empty(m, C, device=x.device, dtype=torch.float32)
+    call("sfx_segment_max_affine_act", m, C, ptr(idx_ptr), ptr(sorted_idx), ptr(x), ptr(scale), ptr(shift), act,
+         ptr(out), stream())
+    return out
+
+
+def segment_mean(x: Tensor, idx_ptr: Tensor, sorted_idx: Tensor, m: int) -> Tensor:
+    D = x.shape[1]
+    out = torch.empty(m, D, device=x.device, dtype=torch.float32)
+    call("sfx_segment_mean", m, D, ptr(idx_ptr), ptr(sorted_idx), ptr(x.contiguous()), ptr(out), stream())
+    return out
+
+
+def subm_neighbors(grid_coord: Tensor, batch: Optional[Tensor]) -> Tensor:
+    n = grid_coord.shape[0]
+    dev = grid_coord.device
+    l2 = _lib.fn("sfx_subm_table_log2")(n)
+    tk = torch.empty(1 << l2, device=dev, dtype=torch.int64)
+    tv = torch.empty(1 << l2, device=dev, dtype=torch.int32)
+    nbr = torch.empty(n, 27, device=dev, dtype=torch.int32)
+    call("sfx_subm_neighbors", n, ptr(grid_coord, torch.int32), ptr(batch), l2, ptr(tk), ptr(tv), ptr(nbr), stream())
+    return nbr
+
+
+def gs_pack(gs: dict, feat_out: Tensor, grid_resolution: float, grid_out: Optional[Tensor],
+            grid_max: Optional[Tensor] = None) -> None:
+    """FeaturePredictor batchify (feature_predictor.py:137-156) into a strided feature view."""
+    n = gs["means"].shape[0]
+
+    def rp(t):
+        t2 = t if t.dim() == 2 else t.reshape(t.shape[0], -1)
+        if t2.stride(-1) != 1:
+            t2 = t2.contiguous()
+        return t2.data_ptr(), t2.stride(0), t2
+
+    keep = []
+    args = []
+    for k in ["means", "scales", "opacities", "quats", "features_dc"]:
+        p_, l_, t_ = rp(gs[k])
+        keep.append(t_)
+        args += [p_, l_]
+    rest = gs.get("features_rest")
+    if rest is not None:
+        p_, l_, t_ = rp(rest if rest.is_contiguous() else rest.contiguous())
+        keep.append(t_)
+        rd = t_.shape[1]
+    else:
+        p_, l_, rd = None, 0, 0
+    pf, ldf = _rows(feat_out)
+    call("sfx_gs_pack", n, *args, p_, l_, rd, float(grid_resolution), pf, ldf, ptr(grid_out), ptr(grid_max),
+         stream())

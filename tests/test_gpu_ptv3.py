@@ -1,0 +1,192 @@
+"""HIP PTv3 refiner (libsfx) vs the CPU oracle (oracle/ptv3_ref.py, oracle/serialize_ref.py).
+
+Integer/index work (serialization codes/order/inverse, neighbour maps, pooling
+clusters) is compared bit-exactly; fp32 features within the north-star
+tolerance: relative L2 error <= 1e-5 on the backbone feature and the refined
+Gaussians, per-op 1e-5 relative.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import ptv3_ref, serialize_ref
+from splatformer_amd import ptv3_ops as ops
+from splatformer_amd.feature_predictor import FeaturePredictor
+from splatformer_amd.scenes import make_scene, to_device
+
+pytestmark = pytest.mark.gpu
+
+
+def rel_l2(a, b):
+    a, b = a.double(), b.double()
+    return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+
+# ---- ops --------------------------------------------------------------------------
+@pytest.mark.parametrize("M,N,K,act", [(1000, 64, 23, 1), (3000, 96, 64, 0), (517, 384, 128, 2), (257, 512, 2048, 0),
+                                       (100, 23, 768, 3)])
+def test_linear_vs_torch(device, M, N, K, act):
+    g = torch.Generator().manual_seed(M + N)
+    x = torch.randn(M, K, generator=g)
+    w = torch.randn(N, K, generator=g) / K ** 0.5
+    b = torch.randn(N, generator=g)
+    sc = torch.rand(N, generator=g) + 0.5
+    sh = torch.randn(N, generator=g)
+    res = torch.randn(M, N, generator=g)
+    ref = (x @ w.T + b) * sc + sh
+    ref = [ref, torch.nn.functional.gelu(ref), torch.relu(ref), torch.tanh(ref)][act] + res
+    y = ops.linear(x.to(device), w.to(device), b.to(device), act=act, scale=sc.to(device), shift=sh.to(device),
+                   residual=res.to(device))
+    assert rel_l2(y.cpu(), ref) < 2e-6
+
+
+def test_linear_gather_is_subm_conv(device):
+    n, C = 4000, 64
+    s = make_scene(n, 1, seed=3, unique_voxels=True)
+    grid = torch.floor(s["means"] * 384).int()
+    batch = torch.zeros(grid.shape[0], dtype=torch.int64)
+    nbr_ref = ptv3_ref.subm_neighbors(grid, batch)
+    nbr = ops.subm_neighbors(grid.to(device), None)
+    assert torch.equal(nbr.cpu().long(), nbr_ref)
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(grid.shape[0], C, generator=g)
+    w = torch.randn(C, 3, 3, 3, C, generator=g) * 0.05
+    b = torch.randn(C, generator=g)
+    ref = ptv3_ref.subm_conv(x, nbr_ref, w, b)
+    y = ops.linear(x.to(device), w.to(device).reshape(C, 27 * C), b.to(device), gather_idx=nbr)
+    assert rel_l2(y.cpu(), ref) < 2e-6
+
+
+def test_subm_neighbors_duplicates_lowest_index(device):
+    grid = torch.tensor([[5, 5, 5], [5, 5, 5], [6, 5, 5], [5, 5, 5], [0, 0, 0]], dtype=torch.int32)
+    nbr = ops.subm_neighbors(grid.to(device), None).cpu()
+    ref = ptv3_ref.subm_neighbors(grid, torch.zeros(5, dtype=torch.int64))
+    assert torch.equal(nbr.long(), ref)
+    assert nbr[3, 13] == 0 and nbr[0, 22] == 2  # centre -> lowest duplicate; +x neighbour
+    assert (nbr[4, :13] == -1).all()  # negative coordinates never match
+
+
+@pytest.mark.parametrize("dup", [False, True])
+def test_serialization_exact(device, dup):
+    s = make_scene(6000, 1, seed=7, unique_voxels=not dup)
+    grid = torch.floor(s["means"] * 384).int()
+    depth = int(grid.max()).bit_length()
+    codes, order, inverse = ops.serialize(grid.to(device), None, depth, 3 * depth, ptv3_ref.ORDERS)
+    c_ref, o_ref, i_ref, _ = serialize_ref.serialization(grid.numpy(), np.zeros(grid.shape[0], np.int64),
+                                                         ptv3_ref.ORDERS, None)
+    assert np.array_equal(codes.cpu().numpy(), c_ref)
+    assert np.array_equal(order.cpu().numpy(), o_ref)
+    assert np.array_equal(inverse.cpu().numpy(), i_ref)
+
+
+def test_serialization_batched(device):
+    s = make_scene(3000, 1, seed=8)
+    grid = torch.floor(s["means"] * 384).int()
+    offsets = torch.tensor([1000, 2200, 3000])
+    batch = torch.repeat_interleave(torch.arange(3), torch.diff(offsets, prepend=torch.tensor([0])))
+    depth = int(grid.max()).bit_length()
+    cb = 3 * depth + 2
+    codes, order, inverse = ops.serialize(grid.to(device), batch.int().to(device), depth, cb, ptv3_ref.ORDERS)
+    c_ref, o_ref, i_ref, _ = serialize_ref.serialization(grid.numpy(), batch.numpy(), ptv3_ref.ORDERS, None)
+    assert np.array_equal(codes.cpu().numpy(), c_ref)
+    assert np.array_equal(order.cpu().numpy(), o_ref)
+    assert np.array_equal(inverse.cpu().numpy(), i_ref)
+
+
+@pytest.mark.parametrize("n,heads,C", [(1000, 2, 64), (777, 4, 96), (300, 8, 128), (100, 2, 32)])
+def test_window_attention_vs_reference_padding(device, n, heads, C):
+    """Window table == Pointcept get_padding_and_inverse duplication semantics (incl. K = n < 128)."""
+    g = torch.Generator().manual_seed(n)
+    qkv = torch.randn(n, 3 * C, generator=g)
+    order = torch.randperm(n, generator=g)
+    inverse = torch.empty_like(order)
+    inverse[order] = torch.arange(n)
+    offset = torch.tensor([n])
+    K = min(n, 128)
+    pad, unpad = ptv3_ref.get_padding_and_inverse(offset, K)
+    o = order[pad]
+    inv = unpad[inverse]
+    q, k, v = qkv[o].reshape(-1, K, 3, heads, C // heads).permute(2, 0, 3, 1, 4).unbind(0)
+    att = torch.softmax((q * (C // heads) ** -0.5) @ k.transpose(-2, -1), -1)
+    ref = (att @ v).transpose(1, 2).reshape(-1, C)[inv]
+    tab = ops.window_table([n], K)
+    win = torch.tensor(tab, dtype=torch.int32).to(device)
+    out = ops.window_attention(qkv.to(device), order.int().to(device), win, len(tab), K, heads, C)
+    assert rel_l2(out.cpu(), ref) < 2e-6
+
+
+def test_layernorm_ops(device):
+    g = torch.Generator().manual_seed(2)
+    for C in (64, 96, 512):
+        x = torch.randn(777, C, generator=g) * 3 + 1
+        t = torch.randn(777, C, generator=g)
+        ga, be = torch.randn(C, generator=g), torch.randn(C, generator=g)
+        g1, b1 = torch.randn(C, generator=g), torch.randn(C, generator=g)
+        y = ops.layernorm(x.to(device), ga.to(device), be.to(device), 1e-5).cpu()
+        ref = torch.nn.functional.layer_norm(x, (C,), ga, be, 1e-5)
+        assert rel_l2(y, ref) < 1e-6
+        xo, h = ops.cpe_residual_ln(t.to(device), x.to(device), ga.to(device), be.to(device), g1.to(device),
+                                    b1.to(device), 1e-5)
+        xr = x + torch.nn.functional.layer_norm(t, (C,), ga, be, 1e-5)
+        hr = torch.nn.functional.layer_norm(xr, (C,), g1, b1, 1e-5)
+        assert rel_l2(xo.cpu(), xr) < 1e-6 and rel_l2(h.cpu(), hr) < 1e-6
+
+
+# ---- whole refiner ---------------------------------------------------------------
+def _randomize(model: torch.nn.Module, seed: int):
+    g = torch.Generator().manual_seed(seed)
+    with torch.no_grad():
+        for m in model.modules():
+            if isinstance(m, torch.nn.BatchNorm1d):
+                m.running_mean.copy_(torch.randn(m.num_features, generator=g) * 0.1)
+                m.running_var.copy_(torch.rand(m.num_features, generator=g) + 0.5)
+                m.weight.copy_(torch.rand(m.num_features, generator=g) + 0.5)
+                m.bias.copy_(torch.randn(m.num_features, generator=g) * 0.1)
+            if isinstance(m, torch.nn.LayerNorm):
+                m.weight.copy_(torch.rand(m.normalized_shape, generator=g) + 0.5)
+                m.bias.copy_(torch.randn(m.normalized_shape, generator=g) * 0.1)
+
+
+def _model(seed=0, **bk):
+    torch.manual_seed(seed)
+    m = FeaturePredictor(sh_degree=1, zeroinit=False, backbone_kwargs=bk)
+    _randomize(m, seed + 1)
+    return m.eval()
+
+
+@pytest.mark.parametrize("n,unique,bk", [
+    (3000, True, {}),
+    (5000, False, {}),
+    (2000, True, dict(enc_depths=(1, 1, 1, 1, 1), dec_depths=(1, 1, 1, 1))),  # config A shape (depth 1)
+])
+def test_feature_predictor_matches_oracle(device, n, unique, bk):
+    model = _model(3, **bk)
+    cfg = ptv3_ref.PTv3Config(**{k: v for k, v in bk.items()})
+    sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+    model = model.to(device)
+    s = make_scene(n, 1, seed=n, unique_voxels=unique)
+    sd_in = to_device(s, device)
+    torch.manual_seed(123)
+    out = model([sd_in], [0])[0]
+    perms = model.backbone.backbone.last_perms
+    assert len(perms) == 5
+    ref, point = ptv3_ref.feature_predictor_forward(sd, cfg, s, perms)
+    for k in ["means", "scales", "opacities", "quats", "features_dc", "features_rest"]:
+        got = out[k].cpu()
+        assert got.shape == ref[k].shape, k
+        err = rel_l2(got - s[k], ref[k] - s[k])  # error relative to the predicted residual
+        assert err < 1e-5, f"{k}: rel L2 of residual {err}"
+
+
+def test_backbone_feature_l2(device):
+    model = _model(5)
+    cfg = ptv3_ref.PTv3Config()
+    sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+    model = model.to(device)
+    s = make_scene(4000, 1, seed=11, unique_voxels=True)
+    data = ptv3_ref.batchify(s)
+    perms = [[1, 0, 3, 2], [2, 3, 0, 1], [0, 1, 2, 3], [3, 2, 1, 0], [1, 3, 0, 2]]
+    dd = {k: (v.to(device) if isinstance(v, torch.Tensor) else v) for k, v in data.items()}
+    p = model.backbone(dd, perms=perms)
+    ref = ptv3_ref.ptv3_forward(sd, cfg, data, perms, prefix="backbone.backbone.")
+    assert rel_l2(p.feat.cpu(), ref.feat) < 1e-5
