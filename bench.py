@@ -1,0 +1,236 @@
+"""Benchmark: refined renders/sec on 100k-Gaussian x 800x800 scenes (BASELINE.json config B).
+
+One step = one scene: FeaturePredictor forward (full ptv3_base PTv3 + heads,
+fp32) over 100k Gaussians, then the 9 OOD test views (800x800) of the refined
+Gaussians through the gsplat-v0.1.11-semantics renderer -- the reference's
+evaluation() hot loop (train.py:86-100).  Synthetic seeded scene and
+random-init weights of the ptv3_base architecture (no datasets/checkpoints
+offline).  Multi-GPU: one process per GPU, one scene per rank (weak scaling,
+no collective on the data path; barrier + max-over-ranks timing only).
+
+Prints ONE JSON line (rank 0) with `roofline` for the dominant kernel (the
+fp32 MFMA GEMM, replayed on its largest launch of the step between HIP events
+on the launch stream) and `cpu_baseline` (the CPU oracle on a bounded sample,
+rank 0 at N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--n", type=int, default=100_000)
+    ap.add_argument("--res", type=int, default=800)
+    ap.add_argument("--views", type=int, default=9)
+    ap.add_argument("--sh", type=int, default=1)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample", type=int, default=20_000, help="Gaussians in the CPU-oracle sample")
+    ap.add_argument("--profile-only", action="store_true", help="skip roofline probe and CPU baseline")
+    return ap.parse_args()
+
+
+class GemmRecorder:
+    """Records sfx_linear launches of one step (for the roofline probe)."""
+
+    def __init__(self):
+        self.calls = []
+
+    def __enter__(self):
+        from splatformer_amd import ptv3_ops
+        self._orig = ptv3_ops.linear
+        rec = self
+
+        def wrapped(x, weight, bias=None, **kw):
+            out = rec._orig(x, weight, bias, **kw)
+            rec.calls.append((x, weight, bias, dict(kw), out))
+            return out
+
+        ptv3_ops.linear = wrapped
+        return self
+
+    def __exit__(self, *a):
+        from splatformer_amd import ptv3_ops
+        ptv3_ops.linear = self._orig
+
+
+def roofline_probe(model, scene, reps=20):
+    """Replay the largest GEMM launch of one refine pass and time it with HIP events."""
+    from splatformer_amd import ptv3_ops
+    with GemmRecorder() as rec:
+        model.refine_packed(scene)
+    torch.cuda.synchronize()
+
+    def flops(c):
+        x, w, b, kw, out = c
+        N, K = w.shape
+        g = kw.get("gather_idx")
+        if g is not None:
+            M = g.shape[0]
+            cin = x.shape[1]
+            pairs = int((g >= 0).sum().item())  # active SubM (out,in) pairs: algorithmic work
+            return 2.0 * pairs * cin * N, 2.0 * M * N * K, M, N, K
+        M = out.shape[0]
+        return 2.0 * M * N * K, 2.0 * M * N * K, M, N, K
+
+    stats = [(flops(c), c) for c in rec.calls]
+    total_alg = sum(s[0][0] for s in stats)
+    (alg, exe, M, N, K), c = max(stats, key=lambda s: s[0][0])
+    x, w, b, kw, out = c
+    kw = dict(kw)
+    kw["out"] = torch.empty_like(out)
+    st = torch.cuda.current_stream()
+    for _ in range(3):
+        rec._orig(x, w, b, **kw)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(reps):
+        rec._orig(x, w, b, **kw)
+    e1.record(st)
+    torch.cuda.synchronize()
+    avg_ms = e0.elapsed_time(e1) / reps
+    achieved = alg / (avg_ms * 1e-3) / 1e12
+    return {
+        "bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+        "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+        "kernel": "gemm_kernel (sfx_linear, fp32 v_mfma_f32_32x32x2_f32)",
+        "launch": {"M": M, "N": N, "K": K, "gathered": kw.get("gather_idx") is not None,
+                   "algorithmic_flop": alg, "executed_flop": exe, "avg_ms": round(avg_ms, 4)},
+        "gemm_total_algorithmic_gflop_per_scene": round(total_alg / 1e9, 1),
+    }
+
+
+def cpu_baseline(scene_cpu, cams_cpu, model_cpu_sd, sample_n, n_total, views, threads):
+    """The CPU oracle (oracle/) on a bounded sample of the workload (test infrastructure, not the product)."""
+    from oracle import ptv3_ref, render_ref
+    torch.set_num_threads(threads)
+    idx = torch.arange(sample_n)
+    sub = {k: v[idx].contiguous() for k, v in scene_cpu.items()}
+    perms = [[0, 1, 2, 3]] * 5
+    t0 = time.perf_counter()
+    out, _ = ptv3_ref.feature_predictor_forward(model_cpu_sd, ptv3_ref.PTv3Config(), sub, perms)
+    t_fwd = time.perf_counter() - t0
+    c2w = cams_cpu["camera_to_worlds"][0]
+    t0 = time.perf_counter()
+    render_ref.rasterize_gaussians_to_singleimg(out, c2w, **cams_cpu)
+    t_view = time.perf_counter() - t0
+    scale = n_total / sample_n
+    t_scene = t_fwd * scale + views * t_view * scale
+    return {
+        "value": round(views / t_scene, 5), "unit": "renders/s", "cores": threads, "kind": "port",
+        "sample": (f"oracle FeaturePredictor fwd on the first {sample_n} of {n_total} Gaussians ({t_fwd:.2f}s) + 1 of "
+                   f"{views} views of that refined crop ({t_view:.2f}s); both scaled linearly by N "
+                   f"({scale:.1f}x) and the view time by {views}"),
+    }
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl")
+    dev = torch.device("cuda", local_rank if world > 1 else 0)
+    torch.cuda.set_device(dev)
+
+    from splatformer_amd import _lib
+    from splatformer_amd.feature_predictor import FeaturePredictor
+    from splatformer_amd.gs_render import rasterize_gaussians_to_multiimgs
+    from splatformer_amd.scenes import make_cameras, make_scene, to_device
+    _lib.load()
+
+    scene_cpu = make_scene(args.n, sh_degree=args.sh, seed=rank)
+    cams_cpu = make_cameras(args.res, args.res, n_views=args.views)
+    torch.manual_seed(0)
+    model = FeaturePredictor(sh_degree=args.sh, zeroinit=False).eval()
+    sd_cpu = {k: v.detach().clone() for k, v in model.state_dict().items()}
+    model = model.to(dev)
+    scene = to_device(scene_cpu, dev)
+    cams = to_device(cams_cpu, dev)
+
+    def step():
+        out = model([scene], [rank])[0]
+        rgbs, alphas = rasterize_gaussians_to_multiimgs(out, cams)
+        return rgbs
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    if dist:
+        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    renders = args.views * args.steps * world
+    value = renders / elapsed
+
+    roof = None
+    if not args.profile_only:
+        roof = roofline_probe(model, scene)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.profile_only:
+        try:
+            aff = len(os.sched_getaffinity(0))
+        except AttributeError:
+            aff = os.cpu_count() or 1
+        threads = max(1, min(16, aff))
+        cpu = cpu_baseline(scene_cpu, cams_cpu, sd_cpu, min(args.cpu_sample, args.n), args.n, args.views, threads)
+
+    if rank == 0:
+        line = {
+            "metric": "refined renders/sec (100k GS, 800x800) at 1/2/4/8 MI355X; PSNR vs ref",
+            "value": round(value, 3),
+            "unit": "renders/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic (seeded 100k-Gaussian scene per rank, random-init ptv3_base weights)",
+            "config": {"workload": f"B: {args.n} Gaussians SH{args.sh}, full PTv3 (ptv3_base) + heads, "
+                                   f"{args.views} views {args.res}x{args.res}, forward",
+                       "scenes_per_step": world, "views_per_scene": args.views, "parallelism": f"scene-dp{world}"},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
