@@ -108,6 +108,8 @@ int sfx_rasterize_bwd(int tiles_x, int tiles_y, int block_width, int img_h, int 
  * the concatenation of S gathered rows (SubMConv3d implicit GEMM).  act: 0 none, 1 GELU(erf), 2 ReLU,
  * 3 tanh, applied to columns < act_ncols (-1 = all).  Ypre (optional) receives the pre-residual value.
  * groups > 1 runs a grouped GEMM (block-diagonal heads) with the given per-group element strides.
+ * Sparse implicit GEMM: out_row_idx[m] maps tile row m to its output row and segment_mask[m] flags the
+ * non-empty gather segments of row m; each 128-row tile skips the segments absent from all its rows.
  * Replaces nn.Linear / BatchNorm1d(eval) / GELU / residual adds of Block, Embedding, SerializedPooling,
  * SerializedUnpooling and the FeaturePredictor heads (feature_predictor.py:74-94, :201-235), and
  * spconv.SubMConv3d (Block.cpe) through gather_idx. */
@@ -115,7 +117,8 @@ int sfx_linear(int M, int N, int K, const float* A, long long lda, const int* ga
                const float* W, long long ldw, const float* bias, const float* scale, const float* shift, int act,
                int act_ncols, const float* R, long long ldr, const int* residual_idx, float* Y, long long ldy,
                float* Ypre, long long ldypre, int groups, long long group_stride_A, long long group_stride_W,
-               long long group_stride_bias, long long group_stride_Y, void* stream);
+               long long group_stride_bias, long long group_stride_Y, const int* out_row_idx,
+               const unsigned* segment_mask, void* stream);
 
 /* nn.LayerNorm rows (C <= 512): Block.norm1 / norm2 */
 int sfx_layernorm(int M, int C, const float* X, long long ldx, const float* gamma, const float* beta, float eps,
@@ -150,10 +153,27 @@ int sfx_segment_mean(int m, int D, const int* idx_ptr, const int* sorted_idx, co
                      void* stream);
 
 /* spconv SubMConv3d indice pairs (indice_key=stage{s}): nbr[n][27], k = (dx+1)*9+(dy+1)*3+(dz+1), -1 absent,
- * duplicate voxels resolve to the lowest point index.  table_*: 2^log2cap scratch slots. */
+ * duplicate voxels resolve to the lowest point index; mask[n] (optional) = bit k set iff nbr[.][k] >= 0,
+ * mask_keys[n] (optional) the same mask widened to the u64 sort-key layout.
+ * table_*: 2^log2cap scratch slots.  sfx_subm_permute reorders nbr/mask rows by a permutation (the
+ * mask-sorted row order that keeps each GEMM tile's segment union small). */
 int sfx_subm_table_log2(int n);
 int sfx_subm_neighbors(int n, const int* grid_coord, const int* batch, int log2cap, unsigned long long* table_keys,
-                       int* table_vals, int* nbr, void* stream);
+                       int* table_vals, int* nbr, unsigned* mask, unsigned long long* mask_keys, void* stream);
+int sfx_subm_permute(int n, const int* perm, const int* nbr, const unsigned* mask, int* nbr_sorted,
+                     unsigned* mask_sorted, void* stream);
+/* Offset-major indice pairs (centre offset excluded, output rows ascending within an offset):
+ * pair_in/pair_out [<= 26 n], pair_off[28] (device) = per-offset prefix of the pair counts. */
+size_t sfx_subm_pairs_workspace_bytes(int n);
+int sfx_subm_pairs(int n, const int* nbr, void* ws, size_t ws_bytes, int* pair_in, int* pair_out, int* pair_off,
+                   void* stream);
+/* spconv SubMConv3d(Cin, Cout, 3, bias) forward on the pair lists: out = bias + x[nbr[:,13]] W_13^T (dense centre
+ * GEMM, plain stores), then one fp32 MFMA launch over the 26 other offsets' gathered rows whose partial products
+ * are atomically added into out (float atomics: summation order across offsets is not fixed).
+ * weight [Cout,3,3,3,Cin]; pair_off_host = the 28 pair_off values copied to the host. */
+int sfx_subm_conv(int n, int cin, int cout, const float* x, long long ldx, const int* nbr, const float* weight,
+                  const float* bias, const int* pair_in, const int* pair_out, const int* pair_off_host, float* out,
+                  long long ldo, void* stream);
 
 /* FeaturePredictor batchify (feature_predictor.py:134-156): strided attribute rows -> feat rows
  * [means,scales,opacities,quats,dc,rest], grid_coord = floor(means*res), optional atomic grid max. */

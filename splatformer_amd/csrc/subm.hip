@@ -45,31 +45,76 @@ __global__ void subm_insert_kernel(int n, const int* __restrict__ grid, const in
 
 __global__ void subm_query_kernel(int n, const int* __restrict__ grid, const int* __restrict__ batch,
                                   const unsigned long long* __restrict__ keys, const int* __restrict__ vals,
-                                  int log2cap, int* __restrict__ nbr) {
+                                  int log2cap, int* __restrict__ nbr, unsigned* __restrict__ mask_out,
+                                  unsigned long long* __restrict__ mask_keys) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int gx = grid[3 * i], gy = grid[3 * i + 1], gz = grid[3 * i + 2];
+  const int b = batch ? batch[i] : 0;
+  const unsigned cmask = (1u << log2cap) - 1u;
+  unsigned mask = 0u;
+  for (int k = 0; k < 27; ++k) {
+    const int x = gx + k / 9 - 1, y = gy + (k / 3) % 3 - 1, z = gz + k % 3 - 1;
+    int out = -1;
+    if (x >= 0 && y >= 0 && z >= 0) {
+      const unsigned long long key = pack(b, x, y, z);
+      unsigned s = slot_of(key, log2cap);
+      while (true) {
+        const unsigned long long kk = keys[s];
+        if (kk == key) {
+          out = vals[s];
+          break;
+        }
+        if (kk == EMPTY) break;
+        s = (s + 1) & cmask;
+      }
+    }
+    nbr[27ll * i + k] = out;
+    if (out >= 0) mask |= 1u << k;
+  }
+  if (mask_out) mask_out[i] = mask;
+  if (mask_keys) mask_keys[i] = mask;
+}
+
+// rows of nbr / mask in mask-sorted order (perm from a radix sort of the masks)
+__global__ void subm_permute_kernel(int n, const int* __restrict__ perm, const int* __restrict__ nbr,
+                                    const unsigned* __restrict__ mask, int* __restrict__ nbr_sorted,
+                                    unsigned* __restrict__ mask_sorted) {
   const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= 27ll * n) return;
-  const int i = (int)(t / 27), k = (int)(t - (long long)i * 27);
-  const int dx = k / 9 - 1, dy = (k / 3) % 3 - 1, dz = k % 3 - 1;
-  const int x = grid[3 * i] + dx, y = grid[3 * i + 1] + dy, z = grid[3 * i + 2] + dz;
-  int out = -1;
-  if (x >= 0 && y >= 0 && z >= 0) {
-    const unsigned long long key = pack(batch ? batch[i] : 0, x, y, z);
-    const unsigned mask = (1u << log2cap) - 1u;
-    unsigned s = slot_of(key, log2cap);
-    while (true) {
-      const unsigned long long kk = keys[s];
-      if (kk == key) {
-        out = vals[s];
-        break;
-      }
-      if (kk == EMPTY) break;
-      s = (s + 1) & mask;
-    }
+  const int p = (int)(t / 27), k = (int)(t - 27ll * p);
+  const int src = perm[p];
+  nbr_sorted[t] = nbr[27ll * src + k];
+  if (k == 0) mask_sorted[p] = mask[src];
+}
+
+// offset-major pair lists (spconv indice pairs, centre offset excluded): flags over [27][n]
+__global__ void subm_pair_flags_kernel(int n, const int* __restrict__ nbr, int* __restrict__ flags) {
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= 27ll * n) return;
+  const int k = (int)(t / n), i = (int)(t - (long long)k * n);
+  flags[t] = (k != 13 && nbr[27ll * i + k] >= 0) ? 1 : 0;
+}
+
+__global__ void subm_pair_fill_kernel(int n, const int* __restrict__ nbr, const int* __restrict__ flags,
+                                      const int* __restrict__ pos, int* __restrict__ pair_in,
+                                      int* __restrict__ pair_out, int* __restrict__ pair_off) {
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= 27ll * n) return;
+  const int k = (int)(t / n), i = (int)(t - (long long)k * n);
+  if (i == 0) pair_off[k] = pos[t];
+  if (flags[t]) {
+    const int p = pos[t];
+    pair_out[p] = i;
+    pair_in[p] = nbr[27ll * i + k];
   }
-  nbr[t] = out;
 }
 
 }  // namespace
+
+extern "C" int sfx_scan_i32(long long n, const int32_t* in, int32_t* out, int inclusive, void* ws, size_t ws_bytes,
+                            int32_t* total, void* stream);
+extern "C" size_t sfx_scan_workspace_bytes(long long n);
 
 extern "C" {
 
@@ -81,7 +126,7 @@ int sfx_subm_table_log2(int n) {
 
 // table_keys: 2^log2cap u64, table_vals: 2^log2cap i32 (both scratch); nbr: [n][27] i32
 int sfx_subm_neighbors(int n, const int* grid_coord, const int* batch, int log2cap, unsigned long long* table_keys,
-                       int* table_vals, int* nbr, void* stream) {
+                       int* table_vals, int* nbr, unsigned* mask, unsigned long long* mask_keys, void* stream) {
   SFX_REQUIRE(n >= 0, "sfx_subm_neighbors: n < 0");
   SFX_REQUIRE(log2cap >= 4 && log2cap <= 31 && (1ll << log2cap) >= 2ll * n, "sfx_subm_neighbors: table too small");
   if (n == 0) return SFX_OK;
@@ -91,9 +136,49 @@ int sfx_subm_neighbors(int n, const int* grid_coord, const int* batch, int log2c
   hipMemsetAsync(table_keys, 0xff, cap * sizeof(unsigned long long), st);
   hipMemsetAsync(table_vals, 0x7f, cap * sizeof(int), st);
   subm_insert_kernel<<<sfx::ceil_div(n, 256), 256, 0, st>>>(n, grid_coord, batch, table_keys, table_vals, log2cap);
-  subm_query_kernel<<<sfx::ceil_div(27ll * n, 256), 256, 0, st>>>(n, grid_coord, batch, table_keys, table_vals,
-                                                                  log2cap, nbr);
+  subm_query_kernel<<<sfx::ceil_div(n, 256), 256, 0, st>>>(n, grid_coord, batch, table_keys, table_vals, log2cap,
+                                                            nbr, mask, mask_keys);
   return sfx::check_launch("sfx_subm_neighbors");
+}
+
+// pair lists for sfx_subm_conv: pair_in/pair_out hold up to 26*n entries; pair_off[28] (device) receives the
+// per-offset prefix (centre slice empty).  ws: 2 * 27 * n int32 + sfx_scan_workspace_bytes(27 * n).
+size_t sfx_subm_pairs_workspace_bytes(int n) {
+  const long long e = 27ll * (n > 0 ? n : 1);
+  return (size_t)(2 * e * sizeof(int) + 256) + sfx_scan_workspace_bytes(e);
+}
+
+int sfx_subm_pairs(int n, const int* nbr, void* ws, size_t ws_bytes, int* pair_in, int* pair_out, int* pair_off,
+                   void* stream) {
+  SFX_REQUIRE(n >= 0, "sfx_subm_pairs: n < 0");
+  SFX_REQUIRE(ws_bytes >= sfx_subm_pairs_workspace_bytes(n), "sfx_subm_pairs: workspace too small");
+  SFX_REQUIRE(pair_off, "sfx_subm_pairs: null pair_off");
+  hipStream_t st = sfx::as_stream(stream);
+  if (n == 0) {
+    hipMemsetAsync(pair_off, 0, 28 * sizeof(int), st);
+    return sfx::check_launch("sfx_subm_pairs");
+  }
+  SFX_REQUIRE(nbr && ws && pair_in && pair_out, "sfx_subm_pairs: null buffer");
+  const long long e = 27ll * n;
+  int* flags = reinterpret_cast<int*>(ws);
+  int* pos = flags + e;
+  char* scan_ws = reinterpret_cast<char*>(pos + e);
+  scan_ws += (256 - (reinterpret_cast<uintptr_t>(scan_ws) & 255)) & 255;
+  subm_pair_flags_kernel<<<sfx::ceil_div(e, 256), 256, 0, st>>>(n, nbr, flags);
+  int rc = sfx_scan_i32(e, flags, pos, 0, scan_ws, sfx_scan_workspace_bytes(e), pair_off + 27, stream);
+  if (rc) return rc;
+  subm_pair_fill_kernel<<<sfx::ceil_div(e, 256), 256, 0, st>>>(n, nbr, flags, pos, pair_in, pair_out, pair_off);
+  return sfx::check_launch("sfx_subm_pairs");
+}
+
+int sfx_subm_permute(int n, const int* perm, const int* nbr, const unsigned* mask, int* nbr_sorted,
+                     unsigned* mask_sorted, void* stream) {
+  SFX_REQUIRE(n >= 0, "sfx_subm_permute: n < 0");
+  if (n == 0) return SFX_OK;
+  SFX_REQUIRE(perm && nbr && mask && nbr_sorted && mask_sorted, "sfx_subm_permute: null buffer");
+  subm_permute_kernel<<<sfx::ceil_div(27ll * n, 256), 256, 0, sfx::as_stream(stream)>>>(n, perm, nbr, mask,
+                                                                                        nbr_sorted, mask_sorted);
+  return sfx::check_launch("sfx_subm_permute");
 }
 
 }  // extern "C"

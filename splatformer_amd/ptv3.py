@@ -106,8 +106,7 @@ class Block(nn.Module):
         x = point.feat
         C = self.channels
         conv, lin, ln_c = self.cpe[0], self.cpe[1], self.cpe[2]
-        t = ops.linear(x if conv_in is None else conv_in, conv.weight.reshape(C, 27 * C), conv.bias,
-                       gather_idx=point.nbr)
+        t = ops.subm_conv(x if conv_in is None else conv_in, point.nbr, conv.weight, conv.bias)
         t = ops.linear(t, lin.weight, lin.bias)
         ln1 = self.norm1[0]
         x1, h = ops.cpe_residual_ln(t, x, ln_c.weight, ln_c.bias, ln1.weight, ln1.bias, ln1.eps)

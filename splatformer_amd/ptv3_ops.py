@@ -14,7 +14,7 @@ from torch import Tensor
 from . import _lib
 from ._lib import I, L, P, F, Z, call, ptr, stream
 
-_lib.register("sfx_linear", [I, I, I, P, L, P, I, P, L, P, P, P, I, I, P, L, P, P, L, P, L, I, L, L, L, L, P])
+_lib.register("sfx_linear", [I, I, I, P, L, P, I, P, L, P, P, P, I, I, P, L, P, P, L, P, L, I, L, L, L, L, P, P, P])
 _lib.register("sfx_layernorm", [I, I, P, L, P, P, F, P, L, P])
 _lib.register("sfx_cpe_residual_ln", [I, I, P, P, P, P, P, P, F, P, P, P])
 _lib.register("sfx_window_attention", [I, I, I, I, I, P, P, P, F, P, P])
@@ -26,7 +26,11 @@ _lib.register("sfx_pool_gather", [I, I, I, P, P, I, P, P, I, P, P, P, P, P])
 _lib.register("sfx_segment_max_affine_act", [I, I, P, P, P, P, P, I, P, P])
 _lib.register("sfx_segment_mean", [I, I, P, P, P, P, P])
 _lib.register("sfx_subm_table_log2", [I])
-_lib.register("sfx_subm_neighbors", [I, P, P, I, P, P, P, P])
+_lib.register("sfx_subm_neighbors", [I, P, P, I, P, P, P, P, P, P])
+_lib.register("sfx_subm_permute", [I, P, P, P, P, P, P])
+_lib.register("sfx_subm_pairs_workspace_bytes", [I], Z)
+_lib.register("sfx_subm_pairs", [I, P, P, Z, P, P, P, P])
+_lib.register("sfx_subm_conv", [I, I, I, P, L, P, P, P, P, P, P, P, L, P])
 _lib.register("sfx_gs_pack", [I, P, L, P, L, P, L, P, L, P, L, P, L, I, F, P, L, P, P, P])
 _lib.register("sfx_offsets_to_batch", [I, I, P, P, P])
 
@@ -48,7 +52,8 @@ def _rows(t: Tensor) -> Tuple[int, int]:
 def linear(x: Tensor, weight: Tensor, bias: Optional[Tensor] = None, *, act: int = ACT_NONE, act_ncols: int = -1,
            scale: Optional[Tensor] = None, shift: Optional[Tensor] = None, residual: Optional[Tensor] = None,
            residual_idx: Optional[Tensor] = None, out: Optional[Tensor] = None, pre_out: Optional[Tensor] = None,
-           gather_idx: Optional[Tensor] = None, rows: Optional[int] = None) -> Tensor:
+           gather_idx: Optional[Tensor] = None, rows: Optional[int] = None, out_rows: Optional[Tensor] = None,
+           segment_mask: Optional[Tensor] = None) -> Tensor:
     """y = act((x W^T + b) * scale + shift) + residual[residual_idx]  (fp32 MFMA GEMM, csrc/gemm.hip).
 
     With `gather_idx` [M, S] (int32, -1 = empty) the A operand is the implicit
@@ -72,7 +77,8 @@ def linear(x: Tensor, weight: Tensor, bias: Optional[Tensor] = None, *, act: int
     pr, ldr = _rows(residual) if residual is not None else (None, 0)
     pp, ldp = _rows(pre_out) if pre_out is not None else (None, 0)
     call("sfx_linear", M, N, K, pa, lda, ptr(gather_idx), S, pw, ldw, ptr(bias), ptr(scale), ptr(shift), act,
-         act_ncols, pr, ldr, ptr(residual_idx), py, ldy, pp, ldp, 1, 0, 0, 0, 0, stream())
+         act_ncols, pr, ldr, ptr(residual_idx), py, ldy, pp, ldp, 1, 0, 0, 0, 0, ptr(out_rows), ptr(segment_mask),
+         stream())
     return out
 
 
@@ -86,7 +92,7 @@ def grouped_linear(x: Tensor, weight: Tensor, bias: Tensor, groups: int, *, act:
     pa, lda = _rows(x)
     py, ldy = _rows(out)
     call("sfx_linear", M, N, K, pa, lda, None, 1, ptr(weight), K, ptr(bias), None, None, act, -1, None, 0, None, py,
-         ldy, None, 0, G, K, N * K, N, N, stream())
+         ldy, None, 0, G, K, N * K, N, N, None, None, stream())
     return out
 
 
@@ -225,15 +231,58 @@ def segment_mean(x: Tensor, idx_ptr: Tensor, sorted_idx: Tensor, m: int) -> Tens
     return out
 
 
-def subm_neighbors(grid_coord: Tensor, batch: Optional[Tensor]) -> Tensor:
+class SubmMap:
+    """Per-stage SubMConv3d indice map (indice_key=stage{s}): nbr [n,27] + offset-major pair lists."""
+
+    def __init__(self, nbr: Tensor, mask: Tensor, pair_in: Tensor, pair_out: Tensor, pair_off: List[int]):
+        self.nbr, self.mask, self.pair_in, self.pair_out = nbr, mask, pair_in, pair_out
+        self.pair_off = pair_off
+        import ctypes
+        self._off_host = (ctypes.c_int * 28)(*pair_off)
+
+    @property
+    def shape(self):
+        return self.nbr.shape
+
+    @property
+    def num_pairs(self) -> int:
+        return self.pair_off[27]
+
+
+def subm_neighbors(grid_coord: Tensor, batch: Optional[Tensor], with_pairs: bool = True):
+    """27-neighbour map; with_pairs also builds the offset-major pair lists (one host sync for their offsets)."""
     n = grid_coord.shape[0]
     dev = grid_coord.device
     l2 = _lib.fn("sfx_subm_table_log2")(n)
     tk = torch.empty(1 << l2, device=dev, dtype=torch.int64)
     tv = torch.empty(1 << l2, device=dev, dtype=torch.int32)
     nbr = torch.empty(n, 27, device=dev, dtype=torch.int32)
-    call("sfx_subm_neighbors", n, ptr(grid_coord, torch.int32), ptr(batch), l2, ptr(tk), ptr(tv), ptr(nbr), stream())
-    return nbr
+    mask = torch.empty(n, device=dev, dtype=torch.int32)
+    call("sfx_subm_neighbors", n, ptr(grid_coord, torch.int32), ptr(batch), l2, ptr(tk), ptr(tv), ptr(nbr), ptr(mask),
+         None, stream())
+    if not with_pairs:
+        return nbr
+    cap = max(1, 26 * n)
+    pin = torch.empty(cap, device=dev, dtype=torch.int32)
+    pout = torch.empty(cap, device=dev, dtype=torch.int32)
+    poff = torch.empty(28, device=dev, dtype=torch.int32)
+    ws = _lib.workspace(_lib.fn("sfx_subm_pairs_workspace_bytes")(n), dev)
+    call("sfx_subm_pairs", n, ptr(nbr), ptr(ws), ws.numel(), ptr(pin), ptr(pout), ptr(poff), stream())
+    return SubmMap(nbr, mask, pin, pout, poff.tolist())
+
+
+def subm_conv(x: Tensor, smap: "SubmMap", weight: Tensor, bias: Optional[Tensor],
+              out: Optional[Tensor] = None) -> Tensor:
+    """SubMConv3d(k=3): dense centre GEMM + offset-major pair GEMM with atomic accumulation."""
+    n, cin = x.shape
+    cout = weight.shape[0]
+    if out is None:
+        out = torch.empty(n, cout, device=x.device, dtype=torch.float32)
+    px, ldx = _rows(x)
+    po, ldo = _rows(out)
+    call("sfx_subm_conv", n, cin, cout, px, ldx, ptr(smap.nbr), ptr(weight), ptr(bias), ptr(smap.pair_in),
+         ptr(smap.pair_out), smap._off_host, po, ldo, stream())
+    return out
 
 
 def gs_pack(gs: dict, feat_out: Tensor, grid_resolution: float, grid_out: Optional[Tensor],

@@ -46,8 +46,17 @@ def test_linear_gather_is_subm_conv(device):
     grid = torch.floor(s["means"] * 384).int()
     batch = torch.zeros(grid.shape[0], dtype=torch.int64)
     nbr_ref = ptv3_ref.subm_neighbors(grid, batch)
-    nbr = ops.subm_neighbors(grid.to(device), None)
+    smap = ops.subm_neighbors(grid.to(device), None)
+    nbr = smap.nbr
     assert torch.equal(nbr.cpu().long(), nbr_ref)
+    # offset-major pair lists: exactly the non-centre (out, in) pairs, output rows ascending per offset
+    off = smap.pair_off
+    pin, pout = smap.pair_in.cpu().long(), smap.pair_out.cpu().long()
+    for k in range(27):
+        rows = torch.nonzero(nbr_ref[:, k] >= 0).flatten() if k != 13 else torch.zeros(0, dtype=torch.long)
+        assert torch.equal(pout[off[k]:off[k + 1]], rows)
+        assert torch.equal(pin[off[k]:off[k + 1]], nbr_ref[rows, k])
+    assert off[27] == int((nbr_ref >= 0).sum()) - grid.shape[0]
     g = torch.Generator().manual_seed(0)
     x = torch.randn(grid.shape[0], C, generator=g)
     w = torch.randn(C, 3, 3, 3, C, generator=g) * 0.05
@@ -55,11 +64,18 @@ def test_linear_gather_is_subm_conv(device):
     ref = ptv3_ref.subm_conv(x, nbr_ref, w, b)
     y = ops.linear(x.to(device), w.to(device).reshape(C, 27 * C), b.to(device), gather_idx=nbr)
     assert rel_l2(y.cpu(), ref) < 2e-6
+    for cin in (64, 96, 256):  # offset-major sparse conv (centre GEMM + atomic pair GEMM)
+        xx = torch.randn(grid.shape[0], cin, generator=g)
+        ww = torch.randn(cin, 3, 3, 3, cin, generator=g) * 0.05
+        bb = torch.randn(cin, generator=g)
+        ref2 = ptv3_ref.subm_conv(xx, nbr_ref, ww, bb)
+        y2 = ops.subm_conv(xx.to(device), smap, ww.to(device), bb.to(device))
+        assert rel_l2(y2.cpu(), ref2) < 2e-6
 
 
 def test_subm_neighbors_duplicates_lowest_index(device):
     grid = torch.tensor([[5, 5, 5], [5, 5, 5], [6, 5, 5], [5, 5, 5], [0, 0, 0]], dtype=torch.int32)
-    nbr = ops.subm_neighbors(grid.to(device), None).cpu()
+    nbr = ops.subm_neighbors(grid.to(device), None, with_pairs=False).cpu()
     ref = ptv3_ref.subm_neighbors(grid, torch.zeros(5, dtype=torch.int64))
     assert torch.equal(nbr.long(), ref)
     assert nbr[3, 13] == 0 and nbr[0, 22] == 2  # centre -> lowest duplicate; +x neighbour
