@@ -108,8 +108,8 @@ int sfx_rasterize_bwd(int tiles_x, int tiles_y, int block_width, int img_h, int 
  * the concatenation of S gathered rows (SubMConv3d implicit GEMM).  act: 0 none, 1 GELU(erf), 2 ReLU,
  * 3 tanh, applied to columns < act_ncols (-1 = all).  Ypre (optional) receives the pre-residual value.
  * groups > 1 runs a grouped GEMM (block-diagonal heads) with the given per-group element strides.
- * Sparse implicit GEMM: out_row_idx[m] maps tile row m to its output row and segment_mask[m] flags the
- * non-empty gather segments of row m; each 128-row tile skips the segments absent from all its rows.
+ * out_row_idx[m] (optional) maps GEMM row m to its output row (residual_idx is indexed by output row).
+ * Every operand must span < 2 GiB (raw buffer descriptors; out-of-range lanes read 0 / drop stores).
  * Replaces nn.Linear / BatchNorm1d(eval) / GELU / residual adds of Block, Embedding, SerializedPooling,
  * SerializedUnpooling and the FeaturePredictor heads (feature_predictor.py:74-94, :201-235), and
  * spconv.SubMConv3d (Block.cpe) through gather_idx. */
@@ -117,8 +117,7 @@ int sfx_linear(int M, int N, int K, const float* A, long long lda, const int* ga
                const float* W, long long ldw, const float* bias, const float* scale, const float* shift, int act,
                int act_ncols, const float* R, long long ldr, const int* residual_idx, float* Y, long long ldy,
                float* Ypre, long long ldypre, int groups, long long group_stride_A, long long group_stride_W,
-               long long group_stride_bias, long long group_stride_Y, const int* out_row_idx,
-               const unsigned* segment_mask, void* stream);
+               long long group_stride_bias, long long group_stride_Y, const int* out_row_idx, void* stream);
 
 /* nn.LayerNorm rows (C <= 512): Block.norm1 / norm2 */
 int sfx_layernorm(int M, int C, const float* X, long long ldx, const float* gamma, const float* beta, float eps,

@@ -1,14 +1,14 @@
 // fp32 MFMA GEMM with fused gather prologue and bias/affine/act/residual
 // epilogue -- the dense work of the PTv3 refiner (qkv/proj/MLP/CPE linears,
-// embedding, pooling/unpooling projections, output heads) and, through the
-// row-gather prologue, the SubMConv3d CPE as an implicit GEMM over the 27
-// neighbour offsets.
+// embedding, pooling/unpooling projections, output heads) and the
+// SubMConv3d CPE (centre offset as a gathered GEMM, the other 26 offsets as
+// an offset-major pair GEMM with atomic accumulation).
 //
 //   Y[m, n] = act( (sum_k A'[m, k] W[n, k] + bias[n]) * scale[n] + shift[n] ) + R[r(m), n]
 //
-// A' is A (row-major, lda) or, with a gather index G[M, S], the row
-// concatenation of S segments of width Kseg: A'[m, s*Kseg + c] =
-// A[G[m*S+s], c] (0 when G < 0).  W is torch's Linear layout [N, K].
+// A' is A (row-major, lda) or, with a gather index G (row stride gstride),
+// the row concatenation of S segments of width Kseg: A'[m, s*Kseg + c] =
+// A[G[m*gstride+s], c] (0 when G < 0).  W is torch's Linear layout [N, K].
 //
 // gfx950 mapping: v_mfma_f32_32x32x2_f32 (exact f32 FMA chains, 157 TF/s
 // peak, no xf32 on CDNA4), 256 threads = 4 waves in a 2x2 grid, each wave a
@@ -17,15 +17,24 @@
 // register prefetch of the next slab.  Lane half h of every MFMA step s
 // consumes k = 16h + s, so each lane reads its 16 k-values with 4 x
 // ds_read_b128 per 32-row block.
+//
+// Every global access is a raw buffer op on a wave-uniform descriptor: rows
+// or K columns out of range (and empty gather slots) get an offset beyond
+// the descriptor's extent, so loads return 0 and stores are dropped by the
+// hardware -- no per-element branches, which hipcc would otherwise turn into
+// one `s_waitcnt vmcnt(0)` per load and serialise the prefetch.
 #include "common.h"
 
 namespace {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 constexpr int BK = 32;
 constexpr int LDS_STRIDE = BK + 4;
 constexpr int THREADS = 256;
+constexpr unsigned OOB = 0x7ffffff0u;        // byte offset past every descriptor extent
+constexpr int RSRC_FLAGS = 0x00020000;       // gfx950 raw buffer, 32-bit data
 
 enum Act { ACT_NONE = 0, ACT_GELU = 1, ACT_RELU = 2, ACT_TANH = 3 };
 
@@ -33,9 +42,9 @@ struct GemmArgs {
   int M, N, K;         // K = S * Kseg when gathering
   const float* A;
   long long lda;
-  const int* gidx;     // [M, S] or null
-  int S, Kseg;
-  const float* W;      // [N, K]
+  const int* gidx;     // gather index, row stride gstride, or null
+  int S, Kseg, gstride;
+  const float* W;      // [N, K] (row stride ldw)
   long long ldw;
   const float* bias;   // [N] or null
   const float* scale;  // [N] or null  (folded BatchNorm)
@@ -43,19 +52,13 @@ struct GemmArgs {
   int act, act_ncols;  // act applies to columns < act_ncols
   const float* R;      // residual [*, ldr] or null
   long long ldr;
-  const int* ridx;     // residual row index [M] or null
+  const int* ridx;     // residual row index (by output row) or null
   float* Y;
   long long ldy;
   float* Ypre;         // optional copy of the pre-residual value
   long long ldypre;
-  // grouped GEMM (blockIdx.z): per-group pointer strides (elements)
-  long long gA, gW, gB, gY;
-  // sparse implicit GEMM: tile row m -> output row out_rows[m]; seg_mask[m] = bitmask of non-empty
-  // gather segments of row m (rows pre-sorted by mask so a tile's OR stays small); the K loop only
-  // visits the segments present in the tile's OR.
-  const int* out_rows;
-  const unsigned* seg_mask;
-  int gstride;  // row stride of the gather index (elements; == S unless a column of a wider map is used)
+  long long gA, gW, gB, gY;  // grouped GEMM (blockIdx.z): per-group element strides
+  const int* out_rows;       // tile row -> output row (or null)
   // offset-major sparse conv ("pair mode"): blockIdx.x walks a flat tile list over up to 27 slices;
   // slice k gathers A rows pair_in[pair_off[k] ..] and atomically adds into rows pair_out[...] with the
   // weight slice W + k * slice_w_stride.
@@ -70,6 +73,27 @@ struct GemmArgs {
 
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
 
+// descriptor from a pointer that is wave-uniform by construction; readfirstlane makes that provable to
+// hipcc, which otherwise wraps every buffer op in a waterfall loop (cdna_hip_programming.md T20)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p) {
+  const unsigned long long a = reinterpret_cast<unsigned long long>(p);
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+  void* u = reinterpret_cast<void*>(((unsigned long long)hi << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(u, (short)0, (int)OOB, RSRC_FLAGS);
+}
+
+__device__ __forceinline__ float4 bload4(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  const floatx4 v = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ float bload1(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+}
+__device__ __forceinline__ void bstore1(__amdgpu_buffer_rsrc_t r, unsigned off, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, off, 0, 0);
+}
+
 template <int BM, int BN, bool VEC>
 __global__ void __launch_bounds__(THREADS, 2) gemm_kernel(GemmArgs p) {
   constexpr int WM = BM / 2, WN = BN / 2;   // wave sub-tile
@@ -80,18 +104,19 @@ __global__ void __launch_bounds__(THREADS, 2) gemm_kernel(GemmArgs p) {
   __shared__ __attribute__((aligned(16))) float sW[2][BN * LDS_STRIDE];
 
   const int g = blockIdx.z;
-  const float* __restrict__ A = p.A + g * p.gA;
-  const float* __restrict__ Wt = p.W + g * p.gW;
-  const float* __restrict__ bias = p.bias ? p.bias + g * p.gB : nullptr;
-  float* __restrict__ Y = p.Y + g * p.gY;
+  const float* A = p.A + g * p.gA;
+  const float* Wt = p.W + g * p.gW;
+  const float* bias = p.bias ? p.bias + g * p.gB : nullptr;
+  float* Y = p.Y + g * p.gY;
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
   int m0 = blockIdx.x * BM;
   const int n0 = blockIdx.y * BN;
   int M = p.M;
-  const int* __restrict__ gidx = p.gidx;
-  const int* __restrict__ out_rows = p.out_rows;
+  const int* gidx = p.gidx;
+  int gstride = p.gstride;
+  const int* out_rows = p.out_rows;
   if (p.pair_mode) {
     int sl = 0;
     for (int q = 1; q < p.num_slices; ++q)
@@ -100,90 +125,74 @@ __global__ void __launch_bounds__(THREADS, 2) gemm_kernel(GemmArgs p) {
     M = p.slice_pair_off[sl + 1] - base;
     m0 = ((int)blockIdx.x - p.slice_tile_off[sl]) * BM;
     gidx = p.pair_in + base;
+    gstride = 1;
     out_rows = p.pair_out + base;
     Wt = p.W + sl * p.slice_w_stride;
   }
   const int K = p.K;
-  int nk = (K + BK - 1) / BK;
-  __shared__ unsigned tile_mask_s;
-  unsigned tile_mask = 0xffffffffu;
-  int cps = 1;  // K chunks per gather segment
-  if (p.seg_mask) {
-    if (tid == 0) tile_mask_s = 0u;
-    __syncthreads();
-    unsigned mk = 0u;
-    for (int r = tid; r < BM; r += THREADS)
-      if (m0 + r < M) mk |= p.seg_mask[m0 + r];
-    atomicOr(&tile_mask_s, mk);
-    __syncthreads();
-    tile_mask = tile_mask_s;
-    cps = p.Kseg / BK;
-    nk = __popc(tile_mask) * cps;
-  }
-  // logical K chunk -> physical chunk (skips segments absent from the whole tile)
-  auto phys_chunk = [&](int j) -> int {
-    if (!p.seg_mask) return j;
-    int t = j / cps;
-    unsigned mm = tile_mask;
-    for (int q = 0; q < t; ++q) mm &= mm - 1u;  // drop the t lowest set bits
-    return (__ffs(mm) - 1) * cps + (j - t * cps);
-  };
+  const int nk = (K + BK - 1) / BK;
+  const __amdgpu_buffer_rsrc_t rA = rsrc(A), rW = rsrc(Wt);
 
-  // this thread's staging coordinates: rows (tid>>3) + 32*i, cols (tid&7)*4
+  // staging coordinates of this thread: rows (tid>>3) + 32*i, cols (tid&7)*4
   const int lrow = tid >> 3, lcol = (tid & 7) * 4;
+  // per-row byte bases (plain rows) / row validity (gathered rows: looked up per segment)
+  unsigned a_base[A_ITERS], w_base[W_ITERS];
+  int a_m[A_ITERS];
+#pragma unroll
+  for (int i = 0; i < A_ITERS; ++i) {
+    const int m = m0 + lrow + 32 * i;
+    a_m[i] = m < M ? m : -1;
+    a_base[i] = (m < M) ? (unsigned)((long long)m * p.lda * 4) : OOB;
+  }
+#pragma unroll
+  for (int i = 0; i < W_ITERS; ++i) {
+    const int n = n0 + lrow + 32 * i;
+    w_base[i] = (n < p.N) ? (unsigned)((long long)n * p.ldw * 4) : OOB;
+  }
 
   float4 ra[A_ITERS], rw[W_ITERS];
-
   auto load_tiles = [&](int kt) {
-    const int k0 = phys_chunk(kt) * BK;
+    const int k = kt * BK + lcol;
+    const bool kin = k < K;
+    int seg = 0, kk = k;
+    if (gidx) {
+      seg = k / p.Kseg;
+      kk = k - seg * p.Kseg;
+    }
 #pragma unroll
     for (int i = 0; i < A_ITERS; ++i) {
-      const int m = m0 + lrow + 32 * i;
-      const int k = k0 + lcol;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (m < M) {
-        const float* src = nullptr;
-        int kk = k;
-        if (gidx) {
-          const int s = k / p.Kseg;
-          kk = k - s * p.Kseg;
-          if (s < p.S) {
-            const int r = gidx[(long long)m * p.gstride + s];
-            if (r >= 0) src = A + (long long)r * p.lda;
-          }
-        } else {
-          src = A + (long long)m * p.lda;
-        }
-        if (src) {
-          if (VEC) {
-            if (k < K) v = *reinterpret_cast<const float4*>(src + kk);
-          } else {
-            if (k + 0 < K) v.x = src[kk + 0];
-            if (k + 1 < K) v.y = src[kk + 1];
-            if (k + 2 < K) v.z = src[kk + 2];
-            if (k + 3 < K) v.w = src[kk + 3];
-          }
-        }
+      unsigned off;
+      if (gidx) {
+        const int mm = a_m[i] < 0 ? 0 : a_m[i];
+        const int r = gidx[(long long)mm * gstride + (seg < p.S ? seg : 0)];
+        off = (a_m[i] >= 0 && r >= 0 && kin && seg < p.S) ? (unsigned)(((long long)r * p.lda + kk) * 4) : OOB;
+      } else {
+        off = kin ? a_base[i] + (unsigned)(kk * 4) : OOB;
       }
-      ra[i] = v;
+      if (VEC) {
+        ra[i] = bload4(rA, off);
+      } else {
+        float4 v;
+        v.x = bload1(rA, (k + 0 < K) ? off : OOB);
+        v.y = bload1(rA, (k + 1 < K) ? off + 4 : OOB);
+        v.z = bload1(rA, (k + 2 < K) ? off + 8 : OOB);
+        v.w = bload1(rA, (k + 3 < K) ? off + 12 : OOB);
+        ra[i] = v;
+      }
     }
 #pragma unroll
     for (int i = 0; i < W_ITERS; ++i) {
-      const int n = n0 + lrow + 32 * i;
-      const int k = k0 + lcol;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (n < p.N) {
-        const float* src = Wt + (long long)n * p.ldw;
-        if (VEC) {
-          if (k < K) v = *reinterpret_cast<const float4*>(src + k);
-        } else {
-          if (k + 0 < K) v.x = src[k + 0];
-          if (k + 1 < K) v.y = src[k + 1];
-          if (k + 2 < K) v.z = src[k + 2];
-          if (k + 3 < K) v.w = src[k + 3];
-        }
+      const unsigned off = kin ? w_base[i] + (unsigned)(k * 4) : OOB;
+      if (VEC) {
+        rw[i] = bload4(rW, off);
+      } else {
+        float4 v;
+        v.x = bload1(rW, (k + 0 < K) ? off : OOB);
+        v.y = bload1(rW, (k + 1 < K) ? off + 4 : OOB);
+        v.z = bload1(rW, (k + 2 < K) ? off + 8 : OOB);
+        v.w = bload1(rW, (k + 3 < K) ? off + 12 : OOB);
+        rw[i] = v;
       }
-      rw[i] = v;
     }
   };
   auto store_tiles = [&](int buf) {
@@ -211,15 +220,15 @@ __global__ void __launch_bounds__(THREADS, 2) gemm_kernel(GemmArgs p) {
   int cur = 0;
   for (int kt = 0; kt < nk; ++kt) {
     if (kt + 1 < nk) load_tiles(kt + 1);
-    const float* a_base = &sA[cur][(wm * WM + l32) * LDS_STRIDE + h * 16];
-    const float* w_base = &sW[cur][(wn * WN + l32) * LDS_STRIDE + h * 16];
+    const float* a_lds = &sA[cur][(wm * WM + l32) * LDS_STRIDE + h * 16];
+    const float* w_lds = &sW[cur][(wn * WN + l32) * LDS_STRIDE + h * 16];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       float4 af[MB], wf[NB];
 #pragma unroll
-      for (int a = 0; a < MB; ++a) af[a] = *reinterpret_cast<const float4*>(a_base + a * 32 * LDS_STRIDE + 4 * c);
+      for (int a = 0; a < MB; ++a) af[a] = *reinterpret_cast<const float4*>(a_lds + a * 32 * LDS_STRIDE + 4 * c);
 #pragma unroll
-      for (int b = 0; b < NB; ++b) wf[b] = *reinterpret_cast<const float4*>(w_base + b * 32 * LDS_STRIDE + 4 * c);
+      for (int b = 0; b < NB; ++b) wf[b] = *reinterpret_cast<const float4*>(w_lds + b * 32 * LDS_STRIDE + 4 * c);
 #pragma unroll
       for (int a = 0; a < MB; ++a)
 #pragma unroll
@@ -235,39 +244,67 @@ __global__ void __launch_bounds__(THREADS, 2) gemm_kernel(GemmArgs p) {
     cur ^= 1;
   }
 
-  // epilogue
+  // epilogue: branch-free buffer stores (out-of-range rows/cols -> dropped).  Row indices and residuals
+  // are fetched in batches (all loads issued, one wait) -- an element-wise load->use chain would pay the
+  // full memory latency once per element.
+  const __amdgpu_buffer_rsrc_t rY = rsrc(Y);
+  const __amdgpu_buffer_rsrc_t rR = rsrc(p.R ? p.R : Y);
+  const __amdgpu_buffer_rsrc_t rP = rsrc(p.Ypre ? p.Ypre : Y);
+  int mrow[MB][16];
+  long long rrow[MB][16];
+#pragma unroll
+  for (int a = 0; a < MB; ++a)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int mt = m0 + wm * WM + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+      const int mtc = mt < M ? mt : 0;
+      mrow[a][r] = out_rows ? out_rows[mtc] : mtc;
+    }
+  if (p.R) {
+#pragma unroll
+    for (int a = 0; a < MB; ++a)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) rrow[a][r] = p.ridx ? (long long)p.ridx[mrow[a][r]] : (long long)mrow[a][r];
+  }
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
     const int n = n0 + wn * WN + b * 32 + l32;
-    if (n >= p.N) continue;
-    const float bv = bias ? bias[n] : 0.f;
-    const float sc = p.scale ? p.scale[n] : 1.f;
-    const float sh = p.shift ? p.shift[n] : 0.f;
+    const bool nok = n < p.N;
+    const int nc = nok ? n : 0;
+    const float bv = bias ? bias[nc] : 0.f;
+    const float sc = p.scale ? p.scale[nc] : 1.f;
+    const float sh = p.shift ? p.shift[nc] : 0.f;
     const bool do_act = n < p.act_ncols;
+    float rv[MB][16];
+    if (p.R) {
+#pragma unroll
+      for (int a = 0; a < MB; ++a)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int mt = m0 + wm * WM + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          rv[a][r] = bload1(rR, (nok && mt < M) ? (unsigned)((rrow[a][r] * p.ldr + n) * 4) : OOB);
+        }
+    }
 #pragma unroll
     for (int a = 0; a < MB; ++a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int mt = m0 + wm * WM + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (mt >= M) continue;
-        const int m = out_rows ? out_rows[mt] : mt;
+        const bool ok = nok && mt < M;
+        const long long m = mrow[a][r];
         if (p.pair_mode) {  // partial sum of one neighbour offset: accumulate into the output row
-          atomicAdd(&Y[(long long)m * p.ldy + n], acc[a][b][r]);
+          __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(acc[a][b][r], rY, ok ? (unsigned)((m * p.ldy + n) * 4) : OOB,
+                                                          0, 0);
           continue;
         }
         float v = acc[a][b][r] + bv;
         if (p.scale) v = v * sc + sh;
-        if (do_act) {
-          if (p.act == ACT_GELU) v = gelu_erf(v);
-          else if (p.act == ACT_RELU) v = fmaxf(v, 0.f);
-          else if (p.act == ACT_TANH) v = tanhf(v);
-        }
-        if (p.Ypre) p.Ypre[(long long)m * p.ldypre + n] = v;
-        if (p.R) {
-          const long long rr = p.ridx ? (long long)p.ridx[m] : (long long)m;
-          v += p.R[rr * p.ldr + n];
-        }
-        Y[(long long)m * p.ldy + n] = v;
+        if (p.act == ACT_GELU) v = do_act ? gelu_erf(v) : v;
+        else if (p.act == ACT_RELU) v = do_act ? fmaxf(v, 0.f) : v;
+        else if (p.act == ACT_TANH) v = do_act ? tanhf(v) : v;
+        if (p.Ypre) bstore1(rP, ok ? (unsigned)((m * p.ldypre + n) * 4) : OOB, v);
+        if (p.R) v += rv[a][r];
+        bstore1(rY, ok ? (unsigned)((m * p.ldy + n) * 4) : OOB, v);
       }
     }
   }
@@ -284,6 +321,18 @@ void launch(const GemmArgs& a, int groups, bool vec, hipStream_t st) {
 
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
+inline bool fits(long long rows, long long ld) { return rows * ld * 4 + 64 < (long long)OOB; }
+
+void dispatch(const GemmArgs& a, int groups, bool vec, hipStream_t st) {
+  const long long tiles128 = (long long)sfx::ceil_div(a.M, 128) * sfx::ceil_div(a.N, 128) * groups;
+  if (a.N <= 64)
+    launch<128, 64>(a, groups, vec, st);
+  else if (tiles128 >= 512)
+    launch<128, 128>(a, groups, vec, st);
+  else
+    launch<64, 128>(a, groups, vec, st);
+}
+
 }  // namespace
 
 extern "C" {
@@ -293,8 +342,7 @@ int sfx_linear(int M, int N, int K, const float* A, long long lda, const int* ga
                const float* W, long long ldw, const float* bias, const float* scale, const float* shift, int act,
                int act_ncols, const float* R, long long ldr, const int* residual_idx, float* Y, long long ldy,
                float* Ypre, long long ldypre, int groups, long long group_stride_A, long long group_stride_W,
-               long long group_stride_bias, long long group_stride_Y, const int* out_row_idx,
-               const unsigned* segment_mask, void* stream) {
+               long long group_stride_bias, long long group_stride_Y, const int* out_row_idx, void* stream) {
   SFX_REQUIRE(M >= 0 && N > 0 && K > 0, "sfx_linear: bad sizes M=%d N=%d K=%d", M, N, K);
   SFX_REQUIRE(act >= 0 && act <= 3, "sfx_linear: bad activation %d", act);
   SFX_REQUIRE(groups >= 1, "sfx_linear: groups < 1");
@@ -306,27 +354,17 @@ int sfx_linear(int M, int N, int K, const float* A, long long lda, const int* ga
   SFX_REQUIRE(!gather_idx || Kseg % 4 == 0, "sfx_linear: gathered segment width must be a multiple of 4");
   SFX_REQUIRE(ldw >= K && (gather_idx || lda >= K) && ldy >= N, "sfx_linear: leading dimension too small");
   SFX_REQUIRE(!(scale == nullptr) == !(shift == nullptr), "sfx_linear: scale and shift go together");
+  SFX_REQUIRE((gather_idx || fits(M, lda)) && fits(M, ldy) && fits(N, ldw),
+              "sfx_linear: operand exceeds the 2 GiB buffer-descriptor range");
   GemmArgs a{};
-  a.M = M; a.N = N; a.K = K; a.A = A; a.lda = lda; a.gidx = gather_idx; a.S = S; a.Kseg = Kseg;
+  a.M = M; a.N = N; a.K = K; a.A = A; a.lda = lda; a.gidx = gather_idx; a.S = S; a.Kseg = Kseg; a.gstride = S;
   a.W = W; a.ldw = ldw; a.bias = bias; a.scale = scale; a.shift = shift; a.act = act;
   a.act_ncols = act_ncols < 0 ? N : act_ncols; a.R = R; a.ldr = ldr; a.ridx = residual_idx; a.Y = Y; a.ldy = ldy;
   a.Ypre = Ypre; a.ldypre = ldypre; a.gA = group_stride_A; a.gW = group_stride_W; a.gB = group_stride_bias;
-  a.gY = group_stride_Y;
-  a.out_rows = out_row_idx;
-  a.seg_mask = segment_mask;
-  a.gstride = S;
-  SFX_REQUIRE(!segment_mask || (gather_idx && Kseg % BK == 0 && S <= 32),
-              "sfx_linear: segment_mask needs gather_idx, Kseg %% 32 == 0 and <= 32 segments");
+  a.gY = group_stride_Y; a.out_rows = out_row_idx;
   const bool vec = (K % 4 == 0) && (lda % 4 == 0) && (ldw % 4 == 0) && aligned16(A) && aligned16(W) &&
                    (group_stride_A % 4 == 0) && (group_stride_W % 4 == 0);
-  hipStream_t st = sfx::as_stream(stream);
-  const long long tiles128 = (long long)sfx::ceil_div(M, 128) * sfx::ceil_div(N, 128) * groups;
-  if (N <= 64)
-    launch<128, 64>(a, groups, vec, st);
-  else if (tiles128 >= 512)
-    launch<128, 128>(a, groups, vec, st);
-  else
-    launch<64, 128>(a, groups, vec, st);
+  dispatch(a, groups, vec, sfx::as_stream(stream));
   return sfx::check_launch("sfx_linear");
 }
 
@@ -341,16 +379,15 @@ int sfx_subm_conv(int n, int cin, int cout, const float* x, long long ldx, const
   if (n == 0) return SFX_OK;
   SFX_REQUIRE(x && nbr && weight && out && pair_off_host, "sfx_subm_conv: null buffer");
   SFX_REQUIRE(ldx >= cin && ldo >= cout, "sfx_subm_conv: leading dimension too small");
+  SFX_REQUIRE(fits(n, ldx) && fits(n, ldo) && fits(cout, 27ll * cin),
+              "sfx_subm_conv: operand exceeds the 2 GiB buffer-descriptor range");
   hipStream_t st = sfx::as_stream(stream);
   const bool vec = (cin % 4 == 0) && (ldx % 4 == 0) && aligned16(x) && aligned16(weight);
   // 1) centre offset: dense gathered GEMM with bias, plain stores
   GemmArgs a{};
   a.M = n; a.N = cout; a.K = cin; a.A = x; a.lda = ldx; a.gidx = nbr + 13; a.S = 1; a.Kseg = cin; a.gstride = 27;
   a.W = weight + 13ll * cin; a.ldw = 27ll * cin; a.bias = bias; a.act = 0; a.act_ncols = cout; a.Y = out; a.ldy = ldo;
-  const long long tiles128 = (long long)sfx::ceil_div(n, 128) * sfx::ceil_div(cout, 128);
-  if (cout <= 64) launch<128, 64>(a, 1, vec, st);
-  else if (tiles128 >= 512) launch<128, 128>(a, 1, vec, st);
-  else launch<64, 128>(a, 1, vec, st);
+  dispatch(a, 1, vec, st);
   int rc = sfx::check_launch("sfx_subm_conv(centre)");
   if (rc) return rc;
   if (!pair_in || pair_off_host[27] == 0) return SFX_OK;

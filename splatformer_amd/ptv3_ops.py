@@ -14,7 +14,7 @@ from torch import Tensor
 from . import _lib
 from ._lib import I, L, P, F, Z, call, ptr, stream
 
-_lib.register("sfx_linear", [I, I, I, P, L, P, I, P, L, P, P, P, I, I, P, L, P, P, L, P, L, I, L, L, L, L, P, P, P])
+_lib.register("sfx_linear", [I, I, I, P, L, P, I, P, L, P, P, P, I, I, P, L, P, P, L, P, L, I, L, L, L, L, P, P])
 _lib.register("sfx_layernorm", [I, I, P, L, P, P, F, P, L, P])
 _lib.register("sfx_cpe_residual_ln", [I, I, P, P, P, P, P, P, F, P, P, P])
 _lib.register("sfx_window_attention", [I, I, I, I, I, P, P, P, F, P, P])
@@ -52,8 +52,8 @@ def _rows(t: Tensor) -> Tuple[int, int]:
 def linear(x: Tensor, weight: Tensor, bias: Optional[Tensor] = None, *, act: int = ACT_NONE, act_ncols: int = -1,
            scale: Optional[Tensor] = None, shift: Optional[Tensor] = None, residual: Optional[Tensor] = None,
            residual_idx: Optional[Tensor] = None, out: Optional[Tensor] = None, pre_out: Optional[Tensor] = None,
-           gather_idx: Optional[Tensor] = None, rows: Optional[int] = None, out_rows: Optional[Tensor] = None,
-           segment_mask: Optional[Tensor] = None) -> Tensor:
+           gather_idx: Optional[Tensor] = None, rows: Optional[int] = None,
+           out_rows: Optional[Tensor] = None) -> Tensor:
     """y = act((x W^T + b) * scale + shift) + residual[residual_idx]  (fp32 MFMA GEMM, csrc/gemm.hip).
 
     With `gather_idx` [M, S] (int32, -1 = empty) the A operand is the implicit
@@ -77,8 +77,7 @@ def linear(x: Tensor, weight: Tensor, bias: Optional[Tensor] = None, *, act: int
     pr, ldr = _rows(residual) if residual is not None else (None, 0)
     pp, ldp = _rows(pre_out) if pre_out is not None else (None, 0)
     call("sfx_linear", M, N, K, pa, lda, ptr(gather_idx), S, pw, ldw, ptr(bias), ptr(scale), ptr(shift), act,
-         act_ncols, pr, ldr, ptr(residual_idx), py, ldy, pp, ldp, 1, 0, 0, 0, 0, ptr(out_rows), ptr(segment_mask),
-         stream())
+         act_ncols, pr, ldr, ptr(residual_idx), py, ldy, pp, ldp, 1, 0, 0, 0, 0, ptr(out_rows), stream())
     return out
 
 
@@ -92,7 +91,7 @@ def grouped_linear(x: Tensor, weight: Tensor, bias: Tensor, groups: int, *, act:
     pa, lda = _rows(x)
     py, ldy = _rows(out)
     call("sfx_linear", M, N, K, pa, lda, None, 1, ptr(weight), K, ptr(bias), None, None, act, -1, None, 0, None, py,
-         ldy, None, 0, G, K, N * K, N, N, None, None, stream())
+         ldy, None, 0, G, K, N * K, N, N, None, stream())
     return out
 
 
