@@ -47,72 +47,81 @@ def parse():
 
 
 class GemmRecorder:
-    """Records sfx_linear launches of one step (for the roofline probe)."""
+    """Records the GEMM-kernel launches (sfx_linear / sfx_subm_conv) of one refine pass."""
 
     def __init__(self):
         self.calls = []
 
     def __enter__(self):
         from splatformer_amd import ptv3_ops
-        self._orig = ptv3_ops.linear
+        self._lin, self._conv, self._grp = ptv3_ops.linear, ptv3_ops.subm_conv, ptv3_ops.grouped_linear
         rec = self
 
-        def wrapped(x, weight, bias=None, **kw):
-            out = rec._orig(x, weight, bias, **kw)
-            rec.calls.append((x, weight, bias, dict(kw), out))
+        def lin(x, weight, bias=None, **kw):
+            out = rec._lin(x, weight, bias, **kw)
+            M = out.shape[0]
+            N, K = weight.shape
+            kw2 = dict(kw)
+            kw2["out"] = torch.empty_like(out) if kw.get("out") is None else torch.empty_like(kw["out"])
+            rec.calls.append(("linear", 2.0 * M * N * K, lambda: rec._lin(x, weight, bias, **kw2), (M, N, K)))
             return out
 
-        ptv3_ops.linear = wrapped
+        def conv(x, smap, weight, bias, out=None):
+            o = rec._conv(x, smap, weight, bias, out=out)
+            n, cin = x.shape
+            cout = weight.shape[0]
+            scratch = torch.empty_like(o)
+            fl = 2.0 * (n + smap.num_pairs) * cin * cout
+            rec.calls.append(("subm_conv", fl, lambda: rec._conv(x, smap, weight, bias, out=scratch), (n, cout, cin)))
+            return o
+
+        def grp(x, weight, bias, groups, **kw):
+            out = rec._grp(x, weight, bias, groups, **kw)
+            G, N, K = weight.shape
+            scratch = torch.empty_like(out)
+            rec.calls.append(("grouped_linear", 2.0 * x.shape[0] * G * N * K,
+                              lambda: rec._grp(x, weight, bias, groups, act=kw.get("act", 0), out=scratch),
+                              (x.shape[0], G * N, K)))
+            return out
+
+        ptv3_ops.linear, ptv3_ops.subm_conv, ptv3_ops.grouped_linear = lin, conv, grp
         return self
 
     def __exit__(self, *a):
         from splatformer_amd import ptv3_ops
-        ptv3_ops.linear = self._orig
+        ptv3_ops.linear, ptv3_ops.subm_conv, ptv3_ops.grouped_linear = self._lin, self._conv, self._grp
 
 
-def roofline_probe(model, scene, reps=20):
-    """Replay the largest GEMM launch of one refine pass and time it with HIP events."""
-    from splatformer_amd import ptv3_ops
+def roofline_probe(model, scene, reps=5):
+    """Replay every GEMM-kernel launch of one refine pass between HIP events (on the launch stream):
+    achieved = algorithmic FLOP of all launches / summed average launch time."""
     with GemmRecorder() as rec:
         model.refine_packed(scene)
     torch.cuda.synchronize()
-
-    def flops(c):
-        x, w, b, kw, out = c
-        N, K = w.shape
-        g = kw.get("gather_idx")
-        if g is not None:
-            M = g.shape[0]
-            cin = x.shape[1]
-            pairs = int((g >= 0).sum().item())  # active SubM (out,in) pairs: algorithmic work
-            return 2.0 * pairs * cin * N, 2.0 * M * N * K, M, N, K
-        M = out.shape[0]
-        return 2.0 * M * N * K, 2.0 * M * N * K, M, N, K
-
-    stats = [(flops(c), c) for c in rec.calls]
-    total_alg = sum(s[0][0] for s in stats)
-    (alg, exe, M, N, K), c = max(stats, key=lambda s: s[0][0])
-    x, w, b, kw, out = c
-    kw = dict(kw)
-    kw["out"] = torch.empty_like(out)
     st = torch.cuda.current_stream()
-    for _ in range(3):
-        rec._orig(x, w, b, **kw)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(st)
-    for _ in range(reps):
-        rec._orig(x, w, b, **kw)
-    e1.record(st)
-    torch.cuda.synchronize()
-    avg_ms = e0.elapsed_time(e1) / reps
-    achieved = alg / (avg_ms * 1e-3) / 1e12
+    tot_fl, tot_ms, per = 0.0, 0.0, []
+    for kind, fl, fn, shape in rec.calls:
+        fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for _ in range(reps):
+            fn()
+        e1.record(st)
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / reps
+        tot_fl += fl
+        tot_ms += ms
+        per.append((ms, kind, shape, fl))
+    achieved = tot_fl / (tot_ms * 1e-3) / 1e12
+    top = max(per)
     return {
         "bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
         "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
-        "kernel": "gemm_kernel (sfx_linear, fp32 v_mfma_f32_32x32x2_f32)",
-        "launch": {"M": M, "N": N, "K": K, "gathered": kw.get("gather_idx") is not None,
-                   "algorithmic_flop": alg, "executed_flop": exe, "avg_ms": round(avg_ms, 4)},
-        "gemm_total_algorithmic_gflop_per_scene": round(total_alg / 1e9, 1),
+        "kernel": "gemm_kernel (sfx_linear / sfx_subm_conv, fp32 v_mfma_f32_32x32x2_f32), all launches of one scene",
+        "launches": len(per), "gemm_ms_per_scene": round(tot_ms, 3),
+        "algorithmic_gflop_per_scene": round(tot_fl / 1e9, 1),
+        "top_launch": {"op": top[1], "M_N_K": list(top[2]), "avg_ms": round(top[0], 4),
+                       "tflops": round(top[3] / (top[0] * 1e-3) / 1e12, 2)},
     }
 
 
