@@ -90,12 +90,22 @@ __device__ __forceinline__ float4 bload4(__amdgpu_buffer_rsrc_t r, unsigned off)
 __device__ __forceinline__ float bload1(__amdgpu_buffer_rsrc_t r, unsigned off) {
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
 }
+__device__ __forceinline__ int bload1i(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return (int)__builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
+}
 __device__ __forceinline__ void bstore1(__amdgpu_buffer_rsrc_t r, unsigned off, float v) {
   __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, off, 0, 0);
 }
 
-template <int BM, int BN, bool VEC>
-__global__ void __launch_bounds__(THREADS, 2) gemm_kernel(GemmArgs p) {
+// Persistent tile loop: each workgroup walks output tiles blockIdx.x, +gridDim.x, ... and prefetches
+// the first K-slab of its NEXT tile while it computes the last slab and runs the epilogue of the
+// current one, so the global-load latency of a tile start and the epilogue stores overlap (short-K
+// GEMMs -- K = 64..256 on most PTv3 layers -- are otherwise latency-bound).
+// MODE: how the A rows of a tile are found (compile-time so the load path has no runtime branches)
+enum Mode { MODE_DENSE = 0, MODE_GATHER1 = 1, MODE_GATHERS = 2, MODE_PAIR = 3 };
+
+template <int BM, int BN, bool VEC, int MODE>
+__global__ void __launch_bounds__(THREADS, 2) gemm_kernel(GemmArgs p, int tiles_n, int total_tiles) {
   constexpr int WM = BM / 2, WN = BN / 2;   // wave sub-tile
   constexpr int MB = WM / 32, NB = WN / 32; // 32x32 MFMA blocks per wave
   constexpr int A_ITERS = BM * BK / 4 / THREADS;
@@ -105,69 +115,94 @@ __global__ void __launch_bounds__(THREADS, 2) gemm_kernel(GemmArgs p) {
 
   const int g = blockIdx.z;
   const float* A = p.A + g * p.gA;
-  const float* Wt = p.W + g * p.gW;
   const float* bias = p.bias ? p.bias + g * p.gB : nullptr;
   float* Y = p.Y + g * p.gY;
+  const __amdgpu_buffer_rsrc_t rA = rsrc(A);
+  const __amdgpu_buffer_rsrc_t rY = rsrc(Y);
+  const __amdgpu_buffer_rsrc_t rR = rsrc(p.R ? p.R : Y);
+  const __amdgpu_buffer_rsrc_t rP = rsrc(p.Ypre ? p.Ypre : Y);
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
-  int m0 = blockIdx.x * BM;
-  const int n0 = blockIdx.y * BN;
-  int M = p.M;
-  const int* gidx = p.gidx;
-  int gstride = p.gstride;
-  const int* out_rows = p.out_rows;
-  if (p.pair_mode) {
-    int sl = 0;
-    for (int q = 1; q < p.num_slices; ++q)
-      if (p.slice_tile_off[q] <= (int)blockIdx.x) sl = q;
-    const int base = p.slice_pair_off[sl];
-    M = p.slice_pair_off[sl + 1] - base;
-    m0 = ((int)blockIdx.x - p.slice_tile_off[sl]) * BM;
-    gidx = p.pair_in + base;
-    gstride = 1;
-    out_rows = p.pair_out + base;
-    Wt = p.W + sl * p.slice_w_stride;
-  }
+  const int h = lane >> 5, l32 = lane & 31;
   const int K = p.K;
   const int nk = (K + BK - 1) / BK;
-  const __amdgpu_buffer_rsrc_t rA = rsrc(A), rW = rsrc(Wt);
+  // byte offsets fit 31 bits (host checks every operand against the 2 GiB buffer range)
+  const unsigned lda32 = (unsigned)p.lda, ldw32 = (unsigned)p.ldw, ldy32 = (unsigned)p.ldy;
+  const unsigned ldr32 = (unsigned)p.ldr, ldp32 = (unsigned)p.ldypre;
+  const int lrow = tid >> 3, lcol = (tid & 7) * 4;  // staging coordinates: rows lrow + 32 i, cols lcol..+3
 
-  // staging coordinates of this thread: rows (tid>>3) + 32*i, cols (tid&7)*4
-  const int lrow = tid >> 3, lcol = (tid & 7) * 4;
-  // per-row byte bases (plain rows) / row validity (gathered rows: looked up per segment)
-  unsigned a_base[A_ITERS], w_base[W_ITERS];
-  int a_m[A_ITERS];
+  // per-tile geometry (all wave-uniform)
+  struct Tile {
+    int m0, n0, M;
+    const int* gidx;
+    int gstride;
+    const int* out_rows;
+    const float* W;
+  };
+  auto tile_info = [&](int t) -> Tile {
+    Tile ti;
+    const int tm = t / tiles_n, tn = t - tm * tiles_n;
+    ti.n0 = tn * BN;
+    ti.m0 = tm * BM;
+    ti.M = p.M;
+    ti.gidx = MODE == MODE_DENSE ? nullptr : p.gidx;
+    ti.gstride = p.gstride;
+    ti.out_rows = p.out_rows;
+    ti.W = p.W + g * p.gW;
+    if constexpr (MODE == MODE_PAIR) {
+      int sl = 0;
+      for (int q = 1; q < p.num_slices; ++q)
+        if (p.slice_tile_off[q] <= tm) sl = q;
+      const int base = p.slice_pair_off[sl];
+      ti.M = p.slice_pair_off[sl + 1] - base;
+      ti.m0 = (tm - p.slice_tile_off[sl]) * BM;
+      ti.gidx = p.pair_in + base;
+      ti.gstride = 1;
+      ti.out_rows = p.pair_out + base;
+      ti.W = p.W + sl * p.slice_w_stride;
+    }
+    return ti;
+  };
+
+  // Gathered A rows: with one segment (S == 1, every gathered GEMM the model runs) the row index of a
+  // staging row is the same for all K-slabs of a tile, so it is fetched once per tile -- one tile ahead,
+  // together with the previous tile's work -- and the slab loads never wait on an index load.
+  // With S > 1 the index depends on the slab and is re-fetched per slab.
+  int grow[A_ITERS];
+  auto load_rows = [&](const Tile& ti, int kt, int (&rows)[A_ITERS]) {
+    if constexpr (MODE != MODE_DENSE) {
+      const __amdgpu_buffer_rsrc_t rG = rsrc(ti.gidx);
+      const int seg = MODE == MODE_GATHERS ? (kt * BK + lcol) / p.Kseg : 0;
 #pragma unroll
-  for (int i = 0; i < A_ITERS; ++i) {
-    const int m = m0 + lrow + 32 * i;
-    a_m[i] = m < M ? m : -1;
-    a_base[i] = (m < M) ? (unsigned)((long long)m * p.lda * 4) : OOB;
-  }
-#pragma unroll
-  for (int i = 0; i < W_ITERS; ++i) {
-    const int n = n0 + lrow + 32 * i;
-    w_base[i] = (n < p.N) ? (unsigned)((long long)n * p.ldw * 4) : OOB;
-  }
+      for (int i = 0; i < A_ITERS; ++i) {
+        const int m = ti.m0 + lrow + 32 * i;
+        rows[i] = bload1i(rG, (m < ti.M && seg < p.S) ? ((unsigned)m * (unsigned)ti.gstride + (unsigned)seg) * 4u
+                                                      : OOB);
+      }
+    }
+  };
 
   float4 ra[A_ITERS], rw[W_ITERS];
-  auto load_tiles = [&](int kt) {
+  auto load_tiles = [&](const Tile& ti, int kt) {
+    const __amdgpu_buffer_rsrc_t rW = rsrc(ti.W);
     const int k = kt * BK + lcol;
     const bool kin = k < K;
     int seg = 0, kk = k;
-    if (gidx) {
+    if constexpr (MODE == MODE_GATHERS) {
       seg = k / p.Kseg;
       kk = k - seg * p.Kseg;
     }
 #pragma unroll
     for (int i = 0; i < A_ITERS; ++i) {
+      const int m = ti.m0 + lrow + 32 * i;
+      const bool mok = m < ti.M;
       unsigned off;
-      if (gidx) {
-        const int mm = a_m[i] < 0 ? 0 : a_m[i];
-        const int r = gidx[(long long)mm * gstride + (seg < p.S ? seg : 0)];
-        off = (a_m[i] >= 0 && r >= 0 && kin && seg < p.S) ? (unsigned)(((long long)r * p.lda + kk) * 4) : OOB;
+      if constexpr (MODE != MODE_DENSE) {
+        const int r = grow[i];
+        off = (mok && r >= 0 && kin && seg < p.S) ? ((unsigned)r * lda32 + (unsigned)kk) * 4u : OOB;
       } else {
-        off = kin ? a_base[i] + (unsigned)(kk * 4) : OOB;
+        off = (mok && kin) ? ((unsigned)m * lda32 + (unsigned)kk) * 4u : OOB;
       }
       if (VEC) {
         ra[i] = bload4(rA, off);
@@ -182,7 +217,8 @@ __global__ void __launch_bounds__(THREADS, 2) gemm_kernel(GemmArgs p) {
     }
 #pragma unroll
     for (int i = 0; i < W_ITERS; ++i) {
-      const unsigned off = kin ? w_base[i] + (unsigned)(k * 4) : OOB;
+      const int n = ti.n0 + lrow + 32 * i;
+      const unsigned off = (n < p.N && kin) ? ((unsigned)n * ldw32 + (unsigned)k) * 4u : OOB;
       if (VEC) {
         rw[i] = bload4(rW, off);
       } else {
@@ -205,23 +241,138 @@ __global__ void __launch_bounds__(THREADS, 2) gemm_kernel(GemmArgs p) {
   };
 
   floatx16 acc[MB][NB];
+  auto zero_acc = [&]() {
 #pragma unroll
-  for (int a = 0; a < MB; ++a)
+    for (int a = 0; a < MB; ++a)
 #pragma unroll
-    for (int b = 0; b < NB; ++b)
+      for (int b = 0; b < NB; ++b)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+        for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+  };
 
-  load_tiles(0);
-  store_tiles(0);
-  __syncthreads();
+  // Epilogue operands of the current tile (bias/scale/shift per column, output row per accumulator row)
+  // are fetched BEFORE the next tile's prefetch is issued, so the epilogue never waits on the prefetch.
+  float ebias[NB], escale[NB], eshift[NB];
+  int mrow[MB][16];
+  auto pre_epilogue = [&](const Tile& ti) {
+    // branch-free: absent operands read through an out-of-range offset (-> 0) and are then selected away
+    const __amdgpu_buffer_rsrc_t rB = rsrc(bias ? bias : p.W);
+    const __amdgpu_buffer_rsrc_t rS = rsrc(p.scale ? p.scale : p.W);
+    const __amdgpu_buffer_rsrc_t rH = rsrc(p.shift ? p.shift : p.W);
+    const __amdgpu_buffer_rsrc_t rO = rsrc(ti.out_rows ? (const void*)ti.out_rows : (const void*)p.W);
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const int n = ti.n0 + wn * WN + b * 32 + l32;
+      const unsigned off = n < p.N ? (unsigned)n * 4u : OOB;
+      const float bv = bload1(rB, bias ? off : OOB);
+      const float sv = bload1(rS, p.scale ? off : OOB);
+      const float hv = bload1(rH, p.shift ? off : OOB);
+      ebias[b] = bv;
+      escale[b] = sv;  // raw loads; the defaults for absent operands are selected in the epilogue, so
+      eshift[b] = hv;  // nothing here waits on them
+    }
+    const bool remap = ti.out_rows != nullptr;
+    if (remap) {
+#pragma unroll
+      for (int a = 0; a < MB; ++a)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int mt = ti.m0 + wm * WM + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          mrow[a][r] = bload1i(rO, mt < ti.M ? (unsigned)mt * 4u : OOB);
+        }
+    }
+  };
+  // output row of accumulator row r of block a (-1: outside the tile)
+  auto resolve_rows = [&](const Tile& ti) {
+    const bool remap = ti.out_rows != nullptr;
+#pragma unroll
+    for (int a = 0; a < MB; ++a)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int mt = ti.m0 + wm * WM + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        mrow[a][r] = mt < ti.M ? (remap ? mrow[a][r] : mt) : -1;
+      }
+#pragma unroll
+    for (int b = 0; b < NB; ++b) escale[b] = p.scale ? escale[b] : 1.f;
+  };
 
-  const int h = lane >> 5, l32 = lane & 31;
-  int cur = 0;
-  for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 1 < nk) load_tiles(kt + 1);
-    const float* a_lds = &sA[cur][(wm * WM + l32) * LDS_STRIDE + h * 16];
-    const float* w_lds = &sW[cur][(wn * WN + l32) * LDS_STRIDE + h * 16];
+  // epilogue: branch-free buffer stores (row -1 / out-of-range column -> dropped); the runtime epilogue
+  // options are tested once per 16-element column strip, never per element.
+  auto epilogue = [&](const Tile& ti) {
+    resolve_rows(ti);
+    if constexpr (MODE == MODE_PAIR) {  // partial sums of one neighbour offset: accumulate into the output rows
+#pragma unroll
+      for (int a = 0; a < MB; ++a)
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+          const int n = ti.n0 + wn * WN + b * 32 + l32;
+          const bool nok = n < p.N;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int m = mrow[a][r];
+            __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(
+                acc[a][b][r], rY, (nok && m >= 0) ? ((unsigned)m * ldy32 + (unsigned)n) * 4u : OOB, 0, 0);
+          }
+        }
+      return;
+    }
+#pragma unroll
+    for (int a = 0; a < MB; ++a) {
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        const int n = ti.n0 + wn * WN + b * 32 + l32;
+        const bool nok = n < p.N;
+        const bool do_act = n < p.act_ncols;
+        float v[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] = (acc[a][b][r] + ebias[b]) * escale[b] + eshift[b];
+        if (p.act == ACT_GELU) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) v[r] = do_act ? gelu_erf(v[r]) : v[r];
+        } else if (p.act == ACT_RELU) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) v[r] = do_act ? fmaxf(v[r], 0.f) : v[r];
+        } else if (p.act == ACT_TANH) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) v[r] = do_act ? tanhf(v[r]) : v[r];
+        }
+        if (p.Ypre) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int m = mrow[a][r];
+            bstore1(rP, (nok && m >= 0) ? ((unsigned)m * ldp32 + (unsigned)n) * 4u : OOB, v[r]);
+          }
+        }
+        if (p.R) {
+          float rv[16];
+          const __amdgpu_buffer_rsrc_t rI = rsrc(p.ridx ? (const void*)p.ridx : (const void*)p.W);
+          int rr[16];
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int m = mrow[a][r];
+            const int ri = bload1i(rI, (p.ridx && m >= 0) ? (unsigned)m * 4u : OOB);
+            rr[r] = p.ridx ? ri : m;
+          }
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int m = mrow[a][r];
+            rv[r] = bload1(rR, (nok && m >= 0) ? ((unsigned)rr[r] * ldr32 + (unsigned)n) * 4u : OOB);
+          }
+#pragma unroll
+          for (int r = 0; r < 16; ++r) v[r] += rv[r];
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = mrow[a][r];
+          bstore1(rY, (nok && m >= 0) ? ((unsigned)m * ldy32 + (unsigned)n) * 4u : OOB, v[r]);
+        }
+      }
+    }
+  };
+
+  auto compute = [&](int buf) {
+    const float* a_lds = &sA[buf][(wm * WM + l32) * LDS_STRIDE + h * 16];
+    const float* w_lds = &sW[buf][(wn * WN + l32) * LDS_STRIDE + h * 16];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       float4 af[MB], wf[NB];
@@ -239,98 +390,106 @@ __global__ void __launch_bounds__(THREADS, 2) gemm_kernel(GemmArgs p) {
           acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[a].w, wf[b].w, acc[a][b], 0, 0, 0);
         }
     }
-    if (kt + 1 < nk) store_tiles(cur ^ 1);
-    __syncthreads();
-    cur ^= 1;
-  }
+  };
 
-  // epilogue: branch-free buffer stores (out-of-range rows/cols -> dropped).  Row indices and residuals
-  // are fetched in batches (all loads issued, one wait) -- an element-wise load->use chain would pay the
-  // full memory latency once per element.
-  const __amdgpu_buffer_rsrc_t rY = rsrc(Y);
-  const __amdgpu_buffer_rsrc_t rR = rsrc(p.R ? p.R : Y);
-  const __amdgpu_buffer_rsrc_t rP = rsrc(p.Ypre ? p.Ypre : Y);
-  int mrow[MB][16];
-  long long rrow[MB][16];
-#pragma unroll
-  for (int a = 0; a < MB; ++a)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int mt = m0 + wm * WM + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-      const int mtc = mt < M ? mt : 0;
-      mrow[a][r] = out_rows ? out_rows[mtc] : mtc;
+  int t = blockIdx.x;
+  if (t >= total_tiles) return;
+  constexpr bool per_tile_rows = MODE == MODE_GATHER1 || MODE == MODE_PAIR;
+  Tile ti = tile_info(t);
+  load_rows(ti, 0, grow);
+  load_tiles(ti, 0);
+  store_tiles(0);
+  __syncthreads();
+  int buf = 0;
+  while (true) {
+    const int nt = t + (int)gridDim.x;
+    const bool has_next = nt < total_tiles;
+    const Tile tn = has_next ? tile_info(nt) : ti;
+    int grow_next[A_ITERS];
+    if constexpr (per_tile_rows) load_rows(tn, 0, grow_next);  // next tile's gather rows, a whole tile ahead
+    zero_acc();
+    for (int kt = 0; kt + 1 < nk; ++kt) {
+      if constexpr (MODE == MODE_GATHERS) load_rows(ti, kt + 1, grow);
+      load_tiles(ti, kt + 1);
+      __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of the MFMAs it overlaps
+      compute(buf);
+      store_tiles(buf ^ 1);
+      __syncthreads();
+      buf ^= 1;
     }
-  if (p.R) {
+    // last slab of tile t: its epilogue operands, then the first slab of tile t+1 in flight while the
+    // last MFMAs and the epilogue run
+    pre_epilogue(ti);
+    if (has_next) {
+      if constexpr (per_tile_rows) {
 #pragma unroll
-    for (int a = 0; a < MB; ++a)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) rrow[a][r] = p.ridx ? (long long)p.ridx[mrow[a][r]] : (long long)mrow[a][r];
-  }
-#pragma unroll
-  for (int b = 0; b < NB; ++b) {
-    const int n = n0 + wn * WN + b * 32 + l32;
-    const bool nok = n < p.N;
-    const int nc = nok ? n : 0;
-    const float bv = bias ? bias[nc] : 0.f;
-    const float sc = p.scale ? p.scale[nc] : 1.f;
-    const float sh = p.shift ? p.shift[nc] : 0.f;
-    const bool do_act = n < p.act_ncols;
-    float rv[MB][16];
-    if (p.R) {
-#pragma unroll
-      for (int a = 0; a < MB; ++a)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int mt = m0 + wm * WM + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-          rv[a][r] = bload1(rR, (nok && mt < M) ? (unsigned)((rrow[a][r] * p.ldr + n) * 4) : OOB);
-        }
-    }
-#pragma unroll
-    for (int a = 0; a < MB; ++a) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int mt = m0 + wm * WM + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        const bool ok = nok && mt < M;
-        const long long m = mrow[a][r];
-        if (p.pair_mode) {  // partial sum of one neighbour offset: accumulate into the output row
-          __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(acc[a][b][r], rY, ok ? (unsigned)((m * p.ldy + n) * 4) : OOB,
-                                                          0, 0);
-          continue;
-        }
-        float v = acc[a][b][r] + bv;
-        if (p.scale) v = v * sc + sh;
-        if (p.act == ACT_GELU) v = do_act ? gelu_erf(v) : v;
-        else if (p.act == ACT_RELU) v = do_act ? fmaxf(v, 0.f) : v;
-        else if (p.act == ACT_TANH) v = do_act ? tanhf(v) : v;
-        if (p.Ypre) bstore1(rP, ok ? (unsigned)((m * p.ldypre + n) * 4) : OOB, v);
-        if (p.R) v += rv[a][r];
-        bstore1(rY, ok ? (unsigned)((m * p.ldy + n) * 4) : OOB, v);
+        for (int i = 0; i < A_ITERS; ++i) grow[i] = grow_next[i];
+      } else {
+        load_rows(tn, 0, grow);
       }
+      load_tiles(tn, 0);
     }
+    __builtin_amdgcn_sched_barrier(0);
+    compute(buf);
+    epilogue(ti);
+    if (!has_next) break;
+    store_tiles(buf ^ 1);
+    __syncthreads();
+    buf ^= 1;
+    t = nt;
+    ti = tn;
   }
 }
 
-template <int BM, int BN>
+int num_cus() {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+  }
+  return cus;
+}
+
+template <int BM, int BN, int MODE>
 void launch(const GemmArgs& a, int groups, bool vec, hipStream_t st) {
-  dim3 grid(a.pair_mode ? a.slice_tile_off[a.num_slices] : sfx::ceil_div(a.M, BM), sfx::ceil_div(a.N, BN), groups);
+  const int tiles_m = a.pair_mode ? a.slice_tile_off[a.num_slices] : (int)sfx::ceil_div(a.M, BM);
+  const int tiles_n = (int)sfx::ceil_div(a.N, BN);
+  const int total = tiles_m * tiles_n;
+  // persistent grid: 2 workgroups per CU (LDS/VGPR bound), balanced so every workgroup gets the same
+  // number of tiles (+-1)
+  const int slots = 2 * num_cus() / groups > 0 ? 2 * num_cus() / groups : 1;
+  const int per = (total + slots - 1) / slots;
+  const int grid_x = total > 0 ? (total + per - 1) / per : 1;
+  dim3 grid(grid_x, 1, groups);
   if (vec)
-    gemm_kernel<BM, BN, true><<<grid, THREADS, 0, st>>>(a);
+    gemm_kernel<BM, BN, true, MODE><<<grid, THREADS, 0, st>>>(a, tiles_n, total);
   else
-    gemm_kernel<BM, BN, false><<<grid, THREADS, 0, st>>>(a);
+    gemm_kernel<BM, BN, false, MODE><<<grid, THREADS, 0, st>>>(a, tiles_n, total);
 }
 
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 inline bool fits(long long rows, long long ld) { return rows * ld * 4 + 64 < (long long)OOB; }
 
-void dispatch(const GemmArgs& a, int groups, bool vec, hipStream_t st) {
+template <int MODE>
+void dispatch_shape(const GemmArgs& a, int groups, bool vec, hipStream_t st) {
   const long long tiles128 = (long long)sfx::ceil_div(a.M, 128) * sfx::ceil_div(a.N, 128) * groups;
   if (a.N <= 64)
-    launch<128, 64>(a, groups, vec, st);
+    launch<128, 64, MODE>(a, groups, vec, st);
   else if (tiles128 >= 512)
-    launch<128, 128>(a, groups, vec, st);
+    launch<128, 128, MODE>(a, groups, vec, st);
   else
-    launch<64, 128>(a, groups, vec, st);
+    launch<64, 128, MODE>(a, groups, vec, st);
+}
+
+void dispatch(const GemmArgs& a, int groups, bool vec, hipStream_t st) {
+  if (!a.gidx)
+    dispatch_shape<MODE_DENSE>(a, groups, vec, st);
+  else if (a.S == 1)
+    dispatch_shape<MODE_GATHER1>(a, groups, vec, st);
+  else
+    launch<64, 128, MODE_GATHERS>(a, groups, vec, st);  // multi-segment gather: test/reference path only
 }
 
 }  // namespace
@@ -354,7 +513,8 @@ int sfx_linear(int M, int N, int K, const float* A, long long lda, const int* ga
   SFX_REQUIRE(!gather_idx || Kseg % 4 == 0, "sfx_linear: gathered segment width must be a multiple of 4");
   SFX_REQUIRE(ldw >= K && (gather_idx || lda >= K) && ldy >= N, "sfx_linear: leading dimension too small");
   SFX_REQUIRE(!(scale == nullptr) == !(shift == nullptr), "sfx_linear: scale and shift go together");
-  SFX_REQUIRE((gather_idx || fits(M, lda)) && fits(M, ldy) && fits(N, ldw),
+  SFX_REQUIRE((gather_idx || fits(M, lda)) && fits(M, ldy) && fits(N, ldw) && (!R || residual_idx || fits(M, ldr)) &&
+                  (!Ypre || fits(M, ldypre)),
               "sfx_linear: operand exceeds the 2 GiB buffer-descriptor range");
   GemmArgs a{};
   a.M = M; a.N = N; a.K = K; a.A = A; a.lda = lda; a.gidx = gather_idx; a.S = S; a.Kseg = Kseg; a.gstride = S;
@@ -405,8 +565,8 @@ int sfx_subm_conv(int n, int cin, int cout, const float* x, long long ldx, const
   b.slice_pair_off[27] = pair_off_host[27];
   b.slice_tile_off[27] = t;
   b.M = pair_off_host[27];
-  if (cout <= 64) launch<128, 64>(b, 1, vec, st);
-  else launch<64, 128>(b, 1, vec, st);
+  if (cout <= 64) launch<128, 64, MODE_PAIR>(b, 1, vec, st);
+  else launch<64, 128, MODE_PAIR>(b, 1, vec, st);
   return sfx::check_launch("sfx_subm_conv(pairs)");
 }
 
