@@ -151,16 +151,11 @@ def cpu_baseline(scene_cpu, cams_cpu, model_cpu_sd, sample_n, n_total, views, th
 
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl")
+    from splatformer_amd import dist as sdist
+    rank, world, local_rank = sdist.env_rank()
     dev = torch.device("cuda", local_rank if world > 1 else 0)
     torch.cuda.set_device(dev)
+    multi = sdist.init("nccl")  # RCCL; only the barrier and the max-over-ranks timing use it
 
     from splatformer_amd import _lib
     from splatformer_amd.feature_predictor import FeaturePredictor
@@ -185,21 +180,15 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
+    sdist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
+    sdist.barrier()
     t1 = time.perf_counter()
-    elapsed = t1 - t0
-    if dist:
-        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    elapsed = sdist.max_over_ranks(t1 - t0, device=dev)
     renders = args.views * args.steps * world
     value = renders / elapsed
 
@@ -236,9 +225,9 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
-    if dist:
-        dist.barrier()
-        dist.destroy_process_group()
+    if multi:
+        sdist.barrier()
+        torch.distributed.destroy_process_group()
 
 
 if __name__ == "__main__":

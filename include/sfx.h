@@ -184,6 +184,15 @@ int sfx_gs_pack(int n, const float* means, long long ld_means, const float* scal
 /* Pointcept offset2batch */
 int sfx_offsets_to_batch(int n, int B, const long long* offsets, int* batch, void* stream);
 
+/* ---- evaluation post-processing ------------------------------------------------------------------
+ * Replaces train.py:104-113 `(x*255).to(torch.uint8)` of prediction (after the gs_utils.py:111
+ * clamp(max=1), applied when clamp_pred != 0) and ground truth, feeding utils/metrics.py:89-91 psnr.
+ * sums[img*3 + {0,1,2}] = exact sum(p^2), sum(g^2), sum(p*g) of the quantised values;
+ * maxes[img*2 + {0,1}] = max(p), max(g) (the metrics.py:26-29 "divide by 255 if max > 1" rule).
+ * Images are [num_images, elems_per_image] contiguous f32. */
+int sfx_image_stats_u8(int num_images, long long elems_per_image, const float* pred, const float* gt,
+                       int clamp_pred, unsigned long long* sums, int* maxes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

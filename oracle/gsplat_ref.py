@@ -428,8 +428,11 @@ def project_gaussians_backward(means3d, scales, glob_scale, quats, viewmat, fx, 
 
 def psnr_u8(pred: torch.Tensor, gt: torch.Tensor) -> torch.Tensor:
     """train.py:104-113 (x*255).to(uint8) then utils/metrics.py:26-29, :89-91 psnr on /255."""
-    p = (pred * 255).to(torch.uint8).to(f32) / 255.0
-    g = (gt * 255).to(torch.uint8).to(f32) / 255.0
+    p = (pred * 255).to(torch.uint8)
+    g = (gt * 255).to(torch.uint8)
+    # metrics.py:26-29: a batch is divided by 255 only when its max exceeds 1
+    p = p / 255.0 if p.max() > 1 else p.to(f32)
+    g = g / 255.0 if g.max() > 1 else g.to(f32)
     mse = ((p - g) ** 2).reshape(p.shape[0], -1).mean(1, keepdim=True)
     return 20 * torch.log10(1.0 / torch.sqrt(mse))
 

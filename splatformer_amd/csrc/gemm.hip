@@ -23,6 +23,8 @@
 // the descriptor's extent, so loads return 0 and stores are dropped by the
 // hardware -- no per-element branches, which hipcc would otherwise turn into
 // one `s_waitcnt vmcnt(0)` per load and serialise the prefetch.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
@@ -104,10 +106,13 @@ __device__ __forceinline__ void bstore1(__amdgpu_buffer_rsrc_t r, unsigned off, 
 // MODE: how the A rows of a tile are found (compile-time so the load path has no runtime branches)
 enum Mode { MODE_DENSE = 0, MODE_GATHER1 = 1, MODE_GATHERS = 2, MODE_PAIR = 3 };
 
-template <int BM, int BN, bool VEC, int MODE>
+template <int BM, int BN, int WGM, bool VEC, int MODE>
 __global__ void __launch_bounds__(THREADS, 2) gemm_kernel(GemmArgs p, int tiles_n, int total_tiles) {
-  constexpr int WM = BM / 2, WN = BN / 2;   // wave sub-tile
+  constexpr int WGN = 4 / WGM;                 // waves along N
+  constexpr int WM = BM / WGM, WN = BN / WGN;  // wave sub-tile
   constexpr int MB = WM / 32, NB = WN / 32; // 32x32 MFMA blocks per wave
+  static_assert(WM % 32 == 0 && WN % 32 == 0 && (BM * BK / 4) % THREADS == 0 && (BN * BK / 4) % THREADS == 0,
+                "tile shape must split into 32x32 MFMA blocks and whole staging passes");
   constexpr int A_ITERS = BM * BK / 4 / THREADS;
   constexpr int W_ITERS = BN * BK / 4 / THREADS;
   __shared__ __attribute__((aligned(16))) float sA[2][BM * LDS_STRIDE];
@@ -123,7 +128,7 @@ __global__ void __launch_bounds__(THREADS, 2) gemm_kernel(GemmArgs p, int tiles_
   const __amdgpu_buffer_rsrc_t rP = rsrc(p.Ypre ? p.Ypre : Y);
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
+  const int wm = wid / WGN, wn = wid % WGN;
   const int h = lane >> 5, l32 = lane & 31;
   const int K = p.K;
   const int nk = (K + BK - 1) / BK;
@@ -451,9 +456,25 @@ int num_cus() {
   return cus;
 }
 
-template <int BM, int BN, int MODE>
-void launch(const GemmArgs& a, int groups, bool vec, hipStream_t st) {
-  const int tiles_m = a.pair_mode ? a.slice_tile_off[a.num_slices] : (int)sfx::ceil_div(a.M, BM);
+inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+inline bool fits(long long rows, long long ld) { return rows * ld * 4 + 64 < (long long)OOB; }
+
+// M-tiles of a launch: plain ceil(M / BM), or per-slice rounding in pair mode (fills slice_tile_off)
+int tiles_m_of(GemmArgs& a, int BM) {
+  if (!a.pair_mode) return (int)sfx::ceil_div(a.M, BM);
+  int t = 0;
+  for (int k = 0; k < a.num_slices; ++k) {
+    a.slice_tile_off[k] = t;
+    t += (a.slice_pair_off[k + 1] - a.slice_pair_off[k] + BM - 1) / BM;
+  }
+  a.slice_tile_off[a.num_slices] = t;
+  return t;
+}
+
+template <int BM, int BN, int WGM, int MODE>
+void launch(GemmArgs a, int groups, bool vec, hipStream_t st) {
+  const int tiles_m = tiles_m_of(a, BM);
   const int tiles_n = (int)sfx::ceil_div(a.N, BN);
   const int total = tiles_m * tiles_n;
   // persistent grid: 2 workgroups per CU (LDS/VGPR bound), balanced so every workgroup gets the same
@@ -463,33 +484,64 @@ void launch(const GemmArgs& a, int groups, bool vec, hipStream_t st) {
   const int grid_x = total > 0 ? (total + per - 1) / per : 1;
   dim3 grid(grid_x, 1, groups);
   if (vec)
-    gemm_kernel<BM, BN, true, MODE><<<grid, THREADS, 0, st>>>(a, tiles_n, total);
+    gemm_kernel<BM, BN, WGM, true, MODE><<<grid, THREADS, 0, st>>>(a, tiles_n, total);
   else
-    gemm_kernel<BM, BN, false, MODE><<<grid, THREADS, 0, st>>>(a, tiles_n, total);
+    gemm_kernel<BM, BN, WGM, false, MODE><<<grid, THREADS, 0, st>>>(a, tiles_n, total);
 }
 
-inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+// Tile shapes.  The choice minimises (rounds of 2-per-CU slots) x (tile area / relative MFMA efficiency):
+// with K = 64..2048 and M = 15k..100k every layer is a few rounds of tiles, so wave quantisation and
+// N-padding (N = 96, 288 on the C=96 stages) decide more than peak per-tile efficiency.
+struct TileCfg {
+  int bm, bn;
+  float eff;
+};
+constexpr TileCfg kCfgs[] = {{128, 128, 1.0f}, {128, 96, 0.95f}, {128, 64, 0.8f}, {64, 128, 0.95f}, {64, 64, 0.8f}};  // eff fitted to tools/gemm_calls.py sweeps
+constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
 
-inline bool fits(long long rows, long long ld) { return rows * ld * 4 + 64 < (long long)OOB; }
+int pick_cfg(GemmArgs a, int groups) {
+  static int forced = -2;
+  if (forced == -2) {  // tuning hook: SFX_GEMM_CFG=<index into kCfgs>
+    const char* e = getenv("SFX_GEMM_CFG");
+    forced = (e && *e) ? atoi(e) : -1;
+    if (forced >= kNumCfgs) forced = -1;
+  }
+  if (forced >= 0) return forced;
+  const long long slots = 2ll * num_cus();
+  int best = 0;
+  double best_cost = 1e300;
+  for (int c = 0; c < kNumCfgs; ++c) {
+    const long long tiles = (long long)tiles_m_of(a, kCfgs[c].bm) * sfx::ceil_div(a.N, kCfgs[c].bn) * groups;
+    const long long rounds = (tiles + slots - 1) / slots;
+    const double cost = (double)rounds * kCfgs[c].bm * kCfgs[c].bn / kCfgs[c].eff;
+    if (cost < best_cost) {
+      best_cost = cost;
+      best = c;
+    }
+  }
+  return best;
+}
 
 template <int MODE>
-void dispatch_shape(const GemmArgs& a, int groups, bool vec, hipStream_t st) {
-  const long long tiles128 = (long long)sfx::ceil_div(a.M, 128) * sfx::ceil_div(a.N, 128) * groups;
-  if (a.N <= 64)
-    launch<128, 64, MODE>(a, groups, vec, st);
-  else if (tiles128 >= 512)
-    launch<128, 128, MODE>(a, groups, vec, st);
-  else
-    launch<64, 128, MODE>(a, groups, vec, st);
+void dispatch_mode(const GemmArgs& a, int groups, bool vec, hipStream_t st) {
+  switch (pick_cfg(a, groups)) {
+    case 0: launch<128, 128, 2, MODE>(a, groups, vec, st); break;
+    case 1: launch<128, 96, 4, MODE>(a, groups, vec, st); break;
+    case 2: launch<128, 64, 2, MODE>(a, groups, vec, st); break;
+    case 3: launch<64, 128, 2, MODE>(a, groups, vec, st); break;
+    default: launch<64, 64, 2, MODE>(a, groups, vec, st); break;
+  }
 }
 
 void dispatch(const GemmArgs& a, int groups, bool vec, hipStream_t st) {
-  if (!a.gidx)
-    dispatch_shape<MODE_DENSE>(a, groups, vec, st);
+  if (a.pair_mode)
+    dispatch_mode<MODE_PAIR>(a, groups, vec, st);
+  else if (!a.gidx)
+    dispatch_mode<MODE_DENSE>(a, groups, vec, st);
   else if (a.S == 1)
-    dispatch_shape<MODE_GATHER1>(a, groups, vec, st);
+    dispatch_mode<MODE_GATHER1>(a, groups, vec, st);
   else
-    launch<64, 128, MODE_GATHERS>(a, groups, vec, st);  // multi-segment gather: test/reference path only
+    launch<64, 128, 2, MODE_GATHERS>(a, groups, vec, st);  // multi-segment gather: test/reference path only
 }
 
 }  // namespace
@@ -555,18 +607,9 @@ int sfx_subm_conv(int n, int cin, int cout, const float* x, long long ldx, const
   GemmArgs b = a;
   b.gidx = nullptr; b.bias = nullptr; b.gstride = 1; b.pair_mode = 1; b.pair_in = pair_in; b.pair_out = pair_out;
   b.W = weight; b.slice_w_stride = cin; b.num_slices = 27;
-  const int BMp = (cout <= 64) ? 128 : 64;
-  int t = 0;
-  for (int k = 0; k < 27; ++k) {
-    b.slice_pair_off[k] = pair_off_host[k];
-    b.slice_tile_off[k] = t;
-    t += (pair_off_host[k + 1] - pair_off_host[k] + BMp - 1) / BMp;
-  }
-  b.slice_pair_off[27] = pair_off_host[27];
-  b.slice_tile_off[27] = t;
+  for (int k = 0; k <= 27; ++k) b.slice_pair_off[k] = pair_off_host[k];
   b.M = pair_off_host[27];
-  if (cout <= 64) launch<128, 64, MODE_PAIR>(b, 1, vec, st);
-  else launch<64, 128, MODE_PAIR>(b, 1, vec, st);
+  dispatch(b, 1, vec, st);
   return sfx::check_launch("sfx_subm_conv(pairs)");
 }
 
