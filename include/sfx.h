@@ -119,6 +119,69 @@ int sfx_linear(int M, int N, int K, const float* A, long long lda, const int* ga
                float* Ypre, long long ldypre, int groups, long long group_stride_A, long long group_stride_W,
                long long group_stride_bias, long long group_stride_Y, const int* out_row_idx, void* stream);
 
+/* ---- training (configs C/D): backward of the nn.Linear layers -------------------------------------
+ * dX[M,K] (=|+=) rowscale[m] * (dY[M,N] W[N,K]) * act'(dact_pre[m,k]) for k < dact_ncols (-1 = all);
+ * Wt = W^T stored [K, N] (ldwt); dact: 0 none, 1 GELU(erf) on the pre-activation, 2 ReLU, 3 tanh given
+ * its output; rowscale = DropPath keep/(1-p) mask or NULL.  Autograd of F.linear + the activation that
+ * feeds it (reference models run under train.py:240-289 `total_loss.backward()`). */
+int sfx_linear_bwd_data(int M, int N, int K, const float* dY, long long ldy, const float* Wt, long long ldwt,
+                        const float* rowscale, int dact, int dact_ncols, const float* dact_pre, long long ld_pre,
+                        float* dX, long long lddx, int accumulate, void* stream);
+/* dW[N,K] += dY[M,N]^T X[M,K]; db[N] += sum_m dY[m,:] (db may be NULL).  Accumulates (float atomics). */
+int sfx_linear_wgrad(int M, int N, int K, const float* dY, long long ldy, const float* X, long long ldx, float* dW,
+                     long long ldw, float* db, void* stream);
+/* dst[c, r] = src[r, c] */
+int sfx_transpose(int rows, int cols, const float* src, long long lds, float* dst, long long ldd, void* stream);
+/* spconv SubMConv3d backward w.r.t. the input (the cpe.0 conv of every Block): dX[in] += dY[out] W_k over
+ * the centre offset and every (in, out, k) pair of sfx_subm_pairs; weight_t = weight [Cout, 27*Cin]
+ * transposed to [27*Cin, Cout]; centre_ws = 2n ints scratch; dX accumulates (float atomics). */
+int sfx_subm_conv_bwd_data(int n, int cin, int cout, const float* dy, long long ldy, const int* nbr,
+                           const float* weight_t, const int* pair_in, const int* pair_out, const int* pair_off_host,
+                           int* centre_ws, float* dx, long long lddx, void* stream);
+/* non-flash SerializedAttention backward (visualize.py:140-179 math): dout [N, C] = grad of the attention
+ * output rows; dqkv [N, 3C] must be zero-filled (dK/dV accumulate across overlapping windows). */
+int sfx_window_attention_bwd(int num_windows, int window, int heads, int head_dim, int channels, const float* qkv,
+                             const int* order, const int* win, float scale, const float* dout, float* dqkv,
+                             void* stream);
+/* nn.LayerNorm backward w.r.t. the input: dX = LN'(X) dY (+ dR) */
+int sfx_layernorm_bwd(int M, int C, const float* X, long long ldx, const float* gamma, const float* dY,
+                      long long ldgy, const float* dR, long long ldr, float eps, float* dX, long long lddx,
+                      void* stream);
+/* Block tail backward: dX1 = dX2 + LN1'(X1) dH ; dU = LN_cpe'(U) dX1   (rows of C contiguous floats) */
+int sfx_cpe_ln_bwd(int M, int C, const float* U, const float* X1, const float* gamma_cpe, const float* gamma1,
+                   const float* dX2, const float* dH, float eps, float* dX1, float* dU, void* stream);
+/* train-mode nn.BatchNorm1d(eps 1e-3, momentum 0.01) [+ GELU]; SyncBatchNorm: all-reduce `sums` between the
+ * reduce and the finalize/apply calls.  sums = double[2C]. */
+size_t sfx_colsum2_workspace_bytes(int M, int C);
+int sfx_bn_stats(int M, int C, const float* X, long long ldx, void* ws, size_t ws_bytes, double* sums, void* stream);
+int sfx_bn_finalize(int C, double count, const double* sums, const float* gamma, const float* beta, float eps,
+                    float momentum, float* running_mean, float* running_var, float* mean_out, float* rstd_out,
+                    float* scale_out, float* shift_out, void* stream);
+int sfx_affine_act(int M, int C, const float* X, long long ldx, const float* scale, const float* shift, int act,
+                   const float* R, long long ldr, const int* ridx, float* Y, long long ldy, void* stream);
+int sfx_bn_act_bwd_reduce(int M, int C, const float* X, long long ldx, const float* mean, const float* rstd,
+                          const float* gamma, const float* beta, int act, const float* dY, long long ldgy, void* ws,
+                          size_t ws_bytes, double* sums, void* stream);
+int sfx_bn_act_bwd_apply(int M, int C, const float* X, long long ldx, const float* mean, const float* rstd,
+                         const float* gamma, const float* beta, int act, const float* dY, long long ldgy,
+                         const double* sums, double count, float* dX, long long lddx, int accumulate, void* stream);
+/* SerializedPooling segment_csr(max) with arg-max (train) and its backward (dX rows pre-zeroed) */
+int sfx_segment_max_arg(int m, int C, const int* idx_ptr, const int* sorted_idx, const float* X, float* Y, int* arg,
+                        void* stream);
+int sfx_segment_max_bwd(int m, int C, const float* dY, const int* arg, float* dX, void* stream);
+/* SerializedUnpooling backward of feat[inverse]: Y[s] = sum of the rows of cluster s */
+int sfx_segment_sum(int m, int C, const int* idx_ptr, const int* sorted_idx, const float* X, long long ldx, float* Y,
+                    void* stream);
+/* dX = dY * act'(pre) on cols < ncols (1 GELU pre-act, 2 ReLU, 3 tanh given its output) */
+int sfx_act_bwd(int M, int N, const float* dY, long long ldgy, const float* pre, long long ldp, int act, int ncols,
+                float* dX, long long lddx, void* stream);
+/* clip_grad_norm_(max_norm) + torch.optim.Adam (train.py:292-302, utils/optimizers.py) */
+int sfx_sumsq(long long n, const float* x, double* out, void* stream);
+int sfx_clip_coef(const double* sumsq, float max_norm, float* coef, float* norm_out, void* stream);
+int sfx_adam_step(long long n, float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+                  const float* grad_scale, float lr, float beta1, float beta2, float eps, float weight_decay,
+                  int step, void* stream);
+
 /* nn.LayerNorm rows (C <= 512): Block.norm1 / norm2 */
 int sfx_layernorm(int M, int C, const float* X, long long ldx, const float* gamma, const float* beta, float eps,
                   float* Y, long long ldy, void* stream);

@@ -140,6 +140,225 @@ window_attn_kernel(const float* __restrict__ qkv, const int* __restrict__ order,
   }
 }
 
+
+// ---- backward (training, configs C/D) ---------------------------------------------------------------
+// Autograd of the non-flash attention math of visualize.py:140-179 for one (window, head):
+//   dV = P^T dO ; dP = dO V^T ; dS = P * (dP - rowsum(dO * O)) ; dQ = scale * dS K ; dK = dS^T (scale*Q)
+// Phase A (query on the lane column, S^T = K Q^T as in the forward): softmax statistics, O, Delta, dS^T
+// and dQ -- every query row belongs to exactly one window, so dQ is a plain store.  Phase B (key on the
+// lane column, S = Q K^T recomputed): dV and dK summed over the window's queries; a key can sit in two
+// windows (the ragged last window re-uses the K - n%K points before it), so they are accumulated with
+// float atomics into dqkv, which the caller zero-fills.  Padding queries (positions < query_start of the
+// last window) carry dO = 0 and contribute nothing, exactly as their discarded outputs in the reference.
+template <int D>
+__global__ void __launch_bounds__(256, 1)
+window_attn_bwd_kernel(const float* __restrict__ qkv, const int* __restrict__ order, const int* __restrict__ win,
+                       int Kwin, int C, float scale, const float* __restrict__ dout, float* __restrict__ dqkv) {
+  constexpr int DP = D + 4;
+  constexpr int HALF = D / 2;
+  __shared__ __attribute__((aligned(16))) float Qs[KMAX * DP];
+  __shared__ __attribute__((aligned(16))) float Ks[KMAX * DP];
+  __shared__ __attribute__((aligned(16))) float Vs[KMAX * DP];
+  __shared__ __attribute__((aligned(16))) float dOs[KMAX * DP];
+  __shared__ float st_max[KMAX], st_rinv[KMAX], st_delta[KMAX];
+  __shared__ int rows[KMAX];
+
+  const int w = blockIdx.x, head = blockIdx.y;
+  const int key_start = win[2 * w], query_start = win[2 * w + 1];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, h = lane >> 5, l32 = lane & 31;
+  const long long ld = 3ll * C;
+
+  if (tid < KMAX) rows[tid] = tid < Kwin ? order[key_start + tid] : -1;
+  __syncthreads();
+  constexpr int CH = D / 4;
+  for (int e = tid; e < KMAX * 4 * CH; e += 256) {
+    const int row = e / (4 * CH);
+    const int rem = e - row * 4 * CH;
+    const int mat = rem / CH, ch = rem - mat * CH;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    const int src = rows[row];
+    if (mat < 3) {
+      if (src >= 0) v = *reinterpret_cast<const float4*>(qkv + (long long)src * ld + mat * C + head * D + 4 * ch);
+    } else if (src >= 0 && key_start + row >= query_start) {
+      v = *reinterpret_cast<const float4*>(dout + (long long)src * C + head * D + 4 * ch);
+    }
+    float* dst = mat == 0 ? Qs : mat == 1 ? Ks : mat == 2 ? Vs : dOs;
+    if (mat == 0) {
+      v.x *= scale; v.y *= scale; v.z *= scale; v.w *= scale;
+    }
+    *reinterpret_cast<float4*>(&dst[row * DP + 4 * ch]) = v;
+  }
+  __syncthreads();
+
+  // ---------------- phase A: this wave's 32 queries on the lane columns ----------------
+  floatx16 s[4], dp[4];
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s[kb][r] = dp[kb][r] = 0.f;
+  {
+    const float* qrow = &Qs[(32 * wid + l32) * DP + h * HALF];
+    const float* grow = &dOs[(32 * wid + l32) * DP + h * HALF];
+#pragma unroll
+    for (int c = 0; c < HALF / 4; ++c) {
+      const float4 qv = *reinterpret_cast<const float4*>(qrow + 4 * c);
+      const float4 gv = *reinterpret_cast<const float4*>(grow + 4 * c);
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) {
+        const float4 kv = *reinterpret_cast<const float4*>(&Ks[(kb * 32 + l32) * DP + h * HALF + 4 * c]);
+        const float4 vv = *reinterpret_cast<const float4*>(&Vs[(kb * 32 + l32) * DP + h * HALF + 4 * c]);
+        s[kb] = __builtin_amdgcn_mfma_f32_32x32x2f32(kv.x, qv.x, s[kb], 0, 0, 0);
+        s[kb] = __builtin_amdgcn_mfma_f32_32x32x2f32(kv.y, qv.y, s[kb], 0, 0, 0);
+        s[kb] = __builtin_amdgcn_mfma_f32_32x32x2f32(kv.z, qv.z, s[kb], 0, 0, 0);
+        s[kb] = __builtin_amdgcn_mfma_f32_32x32x2f32(kv.w, qv.w, s[kb], 0, 0, 0);
+        dp[kb] = __builtin_amdgcn_mfma_f32_32x32x2f32(vv.x, gv.x, dp[kb], 0, 0, 0);
+        dp[kb] = __builtin_amdgcn_mfma_f32_32x32x2f32(vv.y, gv.y, dp[kb], 0, 0, 0);
+        dp[kb] = __builtin_amdgcn_mfma_f32_32x32x2f32(vv.z, gv.z, dp[kb], 0, 0, 0);
+        dp[kb] = __builtin_amdgcn_mfma_f32_32x32x2f32(vv.w, gv.w, dp[kb], 0, 0, 0);
+      }
+    }
+  }
+  float mx = -INFINITY;
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int key = kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (key >= Kwin) s[kb][r] = -INFINITY;
+      mx = fmaxf(mx, s[kb][r]);
+    }
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  float sum = 0.f;
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float e = expf(s[kb][r] - mx);
+      s[kb][r] = e;
+      sum += e;
+    }
+  sum += __shfl_xor(sum, 32, 64);
+  const float rinv = 1.f / sum;
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s[kb][r] = s[kb][r] / sum;  // same rounding as the forward
+  // O^T[dd][q] (forward recompute) and Delta_q = sum_dd O[q][dd] dO[q][dd]
+  floatx16 o;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) o[r] = 0.f;
+  const bool dd_ok = l32 < D;
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+    for (int st = 0; st < 16; ++st) {
+      const int key = kb * 32 + (st & 3) + 8 * (st >> 2) + 4 * h;
+      const float a = dd_ok ? Vs[key * DP + l32] : 0.f;
+      o = __builtin_amdgcn_mfma_f32_32x32x2f32(a, s[kb][st], o, 0, 0, 0);
+    }
+  const int qi = 32 * wid + l32;
+  float delta = 0.f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int dd = (r & 3) + 8 * (r >> 2) + 4 * h;
+    if (dd < D) delta += o[r] * dOs[qi * DP + dd];
+  }
+  delta += __shfl_xor(delta, 32, 64);
+  // dS^T = P^T (dP^T - Delta); dQ^T[dd][q] = sum_key K^T[dd][key] dS^T[key][q]
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s[kb][r] = s[kb][r] * (dp[kb][r] - delta);
+  floatx16 dq;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) dq[r] = 0.f;
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+    for (int st = 0; st < 16; ++st) {
+      const int key = kb * 32 + (st & 3) + 8 * (st >> 2) + 4 * h;
+      const float a = dd_ok ? Ks[key * DP + l32] : 0.f;
+      dq = __builtin_amdgcn_mfma_f32_32x32x2f32(a, s[kb][st], dq, 0, 0, 0);
+    }
+  const int qpos = key_start + qi;
+  if (qi < Kwin && qpos >= query_start) {
+    float* dst = dqkv + (long long)rows[qi] * ld + head * D;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int dd = 8 * g + 4 * h;
+      if (dd + 3 < D)
+        *reinterpret_cast<float4*>(dst + dd) =
+            make_float4(dq[4 * g + 0] * scale, dq[4 * g + 1] * scale, dq[4 * g + 2] * scale, dq[4 * g + 3] * scale);
+    }
+  }
+  if (h == 0) {
+    st_max[qi] = mx;
+    st_rinv[qi] = rinv;
+    st_delta[qi] = delta;
+  }
+  __syncthreads();
+
+  // ---------------- phase B: this wave's 32 keys on the lane columns ----------------
+  const int kk = 32 * wid + l32;
+  floatx16 dk, dv;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) dk[r] = dv[r] = 0.f;
+  const bool key_ok = kk < Kwin;
+#pragma unroll 1
+  for (int qb = 0; qb < 4; ++qb) {
+    floatx16 sb, pb;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sb[r] = pb[r] = 0.f;
+    const float* qrow = &Qs[(qb * 32 + l32) * DP + h * HALF];
+    const float* grow = &dOs[(qb * 32 + l32) * DP + h * HALF];
+    const float* krow = &Ks[kk * DP + h * HALF];
+    const float* vrow = &Vs[kk * DP + h * HALF];
+#pragma unroll
+    for (int c = 0; c < HALF / 4; ++c) {
+      const float4 qv = *reinterpret_cast<const float4*>(qrow + 4 * c);
+      const float4 gv = *reinterpret_cast<const float4*>(grow + 4 * c);
+      const float4 kv = *reinterpret_cast<const float4*>(krow + 4 * c);
+      const float4 vv = *reinterpret_cast<const float4*>(vrow + 4 * c);
+      sb = __builtin_amdgcn_mfma_f32_32x32x2f32(qv.x, kv.x, sb, 0, 0, 0);
+      sb = __builtin_amdgcn_mfma_f32_32x32x2f32(qv.y, kv.y, sb, 0, 0, 0);
+      sb = __builtin_amdgcn_mfma_f32_32x32x2f32(qv.z, kv.z, sb, 0, 0, 0);
+      sb = __builtin_amdgcn_mfma_f32_32x32x2f32(qv.w, kv.w, sb, 0, 0, 0);
+      pb = __builtin_amdgcn_mfma_f32_32x32x2f32(gv.x, vv.x, pb, 0, 0, 0);
+      pb = __builtin_amdgcn_mfma_f32_32x32x2f32(gv.y, vv.y, pb, 0, 0, 0);
+      pb = __builtin_amdgcn_mfma_f32_32x32x2f32(gv.z, vv.z, pb, 0, 0, 0);
+      pb = __builtin_amdgcn_mfma_f32_32x32x2f32(gv.w, vv.w, pb, 0, 0, 0);
+    }
+    // sb[r] = S[q][kk], pb[r] = dP[q][kk] for q = qb*32 + (r&3) + 8(r>>2) + 4h
+    float P[16], dS[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int q = qb * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+      const float e = key_ok ? expf(sb[r] - st_max[q]) : 0.f;
+      P[r] = e * st_rinv[q];
+      dS[r] = P[r] * (pb[r] - st_delta[q]);
+    }
+#pragma unroll
+    for (int st = 0; st < 16; ++st) {
+      const int q = qb * 32 + (st & 3) + 8 * (st >> 2) + 4 * h;
+      const float g = dd_ok ? dOs[q * DP + l32] : 0.f;
+      const float qs = dd_ok ? Qs[q * DP + l32] : 0.f;
+      dv = __builtin_amdgcn_mfma_f32_32x32x2f32(g, P[st], dv, 0, 0, 0);
+      dk = __builtin_amdgcn_mfma_f32_32x32x2f32(qs, dS[st], dk, 0, 0, 0);
+    }
+  }
+  if (key_ok) {
+    float* dst = dqkv + (long long)rows[kk] * ld + head * D;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int dd = (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (dd < D) {
+        atomicAdd(dst + C + dd, dk[r]);
+        atomicAdd(dst + 2 * C + dd, dv[r]);
+      }
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -163,6 +382,28 @@ int sfx_window_attention(int num_windows, int window, int heads, int head_dim, i
   else
     window_attn_kernel<32><<<grid, 256, 0, st>>>(qkv, order, win, window, channels, scale, out);
   return sfx::check_launch("sfx_window_attention");
+}
+
+// dout [N, C] = d(attention output); dqkv [N, 3C] zero-filled by the caller (dK/dV accumulate)
+int sfx_window_attention_bwd(int num_windows, int window, int heads, int head_dim, int channels, const float* qkv,
+                             const int* order, const int* win, float scale, const float* dout, float* dqkv,
+                             void* stream) {
+  SFX_REQUIRE(num_windows >= 0, "sfx_window_attention_bwd: num_windows < 0");
+  SFX_REQUIRE(window >= 1 && window <= KMAX, "sfx_window_attention_bwd: window must be in [1, 128]");
+  SFX_REQUIRE(heads * head_dim == channels, "sfx_window_attention_bwd: heads * head_dim != channels");
+  SFX_REQUIRE(head_dim == 16 || head_dim == 24 || head_dim == 32,
+              "sfx_window_attention_bwd: head_dim %d unsupported (16, 24, 32)", head_dim);
+  if (num_windows == 0) return SFX_OK;
+  SFX_REQUIRE(qkv && order && win && dout && dqkv, "sfx_window_attention_bwd: null buffer");
+  dim3 grid(num_windows, heads);
+  hipStream_t st = sfx::as_stream(stream);
+  if (head_dim == 16)
+    window_attn_bwd_kernel<16><<<grid, 256, 0, st>>>(qkv, order, win, window, channels, scale, dout, dqkv);
+  else if (head_dim == 24)
+    window_attn_bwd_kernel<24><<<grid, 256, 0, st>>>(qkv, order, win, window, channels, scale, dout, dqkv);
+  else
+    window_attn_bwd_kernel<32><<<grid, 256, 0, st>>>(qkv, order, win, window, channels, scale, dout, dqkv);
+  return sfx::check_launch("sfx_window_attention_bwd");
 }
 
 }  // extern "C"

@@ -71,9 +71,27 @@ struct GemmArgs {
   int slice_pair_off[28];
   int num_slices;
   long long slice_w_stride;
+  // backward-pass epilogue terms (applied after the activation): v *= rowscale[row] (drop-path masks),
+  // v *= act'(dact_pre[row, col]) for cols < act_ncols (GELU / ReLU on the pre-activation, tanh on its output)
+  const float* rowscale;
+  const float* dact_pre;
+  long long ld_dact;
+  int dact;
 };
 
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+// d/dx of the erf GELU (torch GeluBackward, approximate='none')
+__device__ __forceinline__ float gelu_erf_grad(float x) {
+  const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
+  const float pdf = 0.39894228040143268f * expf(-0.5f * x * x);
+  return cdf + x * pdf;
+}
+enum DAct { DACT_NONE = 0, DACT_GELU = 1, DACT_RELU = 2, DACT_TANH_OUT = 3 };
+__device__ __forceinline__ float dact_grad(int dact, float pre) {
+  if (dact == DACT_GELU) return gelu_erf_grad(pre);
+  if (dact == DACT_RELU) return pre > 0.f ? 1.f : 0.f;
+  return 1.f - pre * pre;  // DACT_TANH_OUT: pre holds tanh(z)
+}
 
 // descriptor from a pointer that is wave-uniform by construction; readfirstlane makes that provable to
 // hipcc, which otherwise wraps every buffer op in a waterfall loop (cdna_hip_programming.md T20)
@@ -341,6 +359,26 @@ __global__ void __launch_bounds__(THREADS, 2) gemm_kernel(GemmArgs p, int tiles_
 #pragma unroll
           for (int r = 0; r < 16; ++r) v[r] = do_act ? tanhf(v[r]) : v[r];
         }
+        if (p.rowscale) {
+          const __amdgpu_buffer_rsrc_t rRS = rsrc(p.rowscale);
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int m = mrow[a][r];
+            v[r] *= bload1(rRS, m >= 0 ? (unsigned)m * 4u : OOB);
+          }
+        }
+        if (p.dact) {
+          const __amdgpu_buffer_rsrc_t rD = rsrc(p.dact_pre);
+          const unsigned ldd = (unsigned)p.ld_dact;
+          float pre[16];
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int m = mrow[a][r];
+            pre[r] = bload1(rD, (nok && m >= 0) ? ((unsigned)m * ldd + (unsigned)n) * 4u : OOB);
+          }
+#pragma unroll
+          for (int r = 0; r < 16; ++r) v[r] = do_act ? v[r] * dact_grad(p.dact, pre[r]) : v[r];
+        }
         if (p.Ypre) {
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
@@ -450,7 +488,7 @@ int num_cus() {
   static int cus = 0;
   if (!cus) {
     int dev = 0;
-    hipGetDevice(&dev);
+    (void)hipGetDevice(&dev);
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
   }
   return cus;
@@ -544,6 +582,122 @@ void dispatch(const GemmArgs& a, int groups, bool vec, hipStream_t st) {
     launch<64, 128, 2, MODE_GATHERS>(a, groups, vec, st);  // multi-segment gather: test/reference path only
 }
 
+
+// ---- weight gradient: dW[N, K] += dY[M, N]^T X[M, K] (reduction over the point rows) ----------------
+// Output tiles are few (N x K of one layer), the reduction long (M = 10^4..10^5 rows): the M range is
+// split over grid.y and every split adds its partial tile with float atomics.  Operands are read
+// row-major (n / k contiguous) and transposed into the MFMA layout on the LDS store.
+constexpr int WG_TILE = 64;
+
+__global__ void __launch_bounds__(THREADS) wgrad_kernel(int M, int N, int K, const float* __restrict__ dY,
+                                                        long long ldy, const float* __restrict__ X, long long ldx,
+                                                        float* __restrict__ dW, long long ldw, int chunk) {
+  __shared__ __attribute__((aligned(16))) float sA[WG_TILE * LDS_STRIDE];
+  __shared__ __attribute__((aligned(16))) float sB[WG_TILE * LDS_STRIDE];
+  const int tiles_k = (K + WG_TILE - 1) / WG_TILE;
+  const int n0 = (blockIdx.x / tiles_k) * WG_TILE, k0 = (blockIdx.x % tiles_k) * WG_TILE;
+  const int m_begin = blockIdx.y * chunk;
+  const int m_end = min(M, m_begin + chunk);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1, h = lane >> 5, l32 = lane & 31;
+  const int lrow = tid & 31, lc4 = (tid >> 5) * 4;  // staging: slab row, 4-column group (+32 for the 2nd)
+  const __amdgpu_buffer_rsrc_t rY = rsrc(dY);
+  const __amdgpu_buffer_rsrc_t rX = rsrc(X);
+  const unsigned ldy32 = (unsigned)ldy, ldx32 = (unsigned)ldx;
+  floatx16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  for (int m0 = m_begin; m0 < m_end; m0 += BK) {
+    const int m = m0 + lrow;
+    const bool mok = m < m_end;
+    float4 ya[2], xb[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int n = n0 + lc4 + 32 * i, k = k0 + lc4 + 32 * i;
+      ya[i] = bload4(rY, (mok && n < N) ? ((unsigned)m * ldy32 + (unsigned)n) * 4u : OOB);
+      xb[i] = bload4(rX, (mok && k < K) ? ((unsigned)m * ldx32 + (unsigned)k) * 4u : OOB);
+    }
+    __syncthreads();  // previous slab fully consumed
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = lc4 + 32 * i;
+      sA[(c + 0) * LDS_STRIDE + lrow] = ya[i].x;
+      sA[(c + 1) * LDS_STRIDE + lrow] = ya[i].y;
+      sA[(c + 2) * LDS_STRIDE + lrow] = ya[i].z;
+      sA[(c + 3) * LDS_STRIDE + lrow] = ya[i].w;
+      sB[(c + 0) * LDS_STRIDE + lrow] = xb[i].x;
+      sB[(c + 1) * LDS_STRIDE + lrow] = xb[i].y;
+      sB[(c + 2) * LDS_STRIDE + lrow] = xb[i].z;
+      sB[(c + 3) * LDS_STRIDE + lrow] = xb[i].w;
+    }
+    __syncthreads();
+    const float* a_lds = &sA[(wm * 32 + l32) * LDS_STRIDE + h * 16];
+    const float* b_lds = &sB[(wn * 32 + l32) * LDS_STRIDE + h * 16];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const float4 af = *reinterpret_cast<const float4*>(a_lds + 4 * c);
+      const float4 bf = *reinterpret_cast<const float4*>(b_lds + 4 * c);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af.x, bf.x, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af.y, bf.y, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af.z, bf.z, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af.w, bf.w, acc, 0, 0, 0);
+    }
+  }
+  const __amdgpu_buffer_rsrc_t rW = rsrc(dW);
+  const int k = k0 + wn * 32 + l32;
+  const unsigned ldw32 = (unsigned)ldw;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int n = n0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+    __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(acc[r], rW, (n < N && k < K) ? ((unsigned)n * ldw32 + (unsigned)k) * 4u
+                                                                                 : OOB, 0, 0);
+  }
+}
+
+// column sums: db[N] += sum_m dY[m, n]  (one wave per 64-column strip x row chunk, atomics across chunks)
+__global__ void __launch_bounds__(256) colsum_kernel(int M, int N, const float* __restrict__ dY, long long ldy,
+                                                     float* __restrict__ db, int rows_per_block) {
+  const int n = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int part = threadIdx.x >> 6;
+  const int m0 = blockIdx.y * rows_per_block;
+  const int m1 = min(M, m0 + rows_per_block);
+  __shared__ float red[4][64];
+  float s = 0.f;
+  if (n < N)
+    for (int m = m0 + part; m < m1; m += 4) s += dY[(long long)m * ldy + n];
+  red[part][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (part == 0 && n < N) atomicAdd(&db[n], red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] +
+                                                red[3][threadIdx.x]);
+}
+
+// dst[c][r] = src[r][c]
+__global__ void __launch_bounds__(256) transpose_kernel(int rows, int cols, const float* __restrict__ src,
+                                                        long long lds, float* __restrict__ dst, long long ldd) {
+  __shared__ float t[32][33];
+  const int r0 = blockIdx.y * 32, c0 = blockIdx.x * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int i = ty; i < 32; i += 8) {
+    const int r = r0 + i, c = c0 + tx;
+    t[i][tx] = (r < rows && c < cols) ? src[(long long)r * lds + c] : 0.f;
+  }
+  __syncthreads();
+  for (int i = ty; i < 32; i += 8) {
+    const int c = c0 + i, r = r0 + tx;
+    if (c < cols && r < rows) dst[(long long)c * ldd + r] = t[tx][i];
+  }
+}
+
+
+// centre-offset pair lists for the SubM backward: gather row i of dY, add into row nbr[i][13] of dX
+__global__ void centre_pairs_kernel(int n, const int* __restrict__ nbr, int* __restrict__ gather,
+                                    int* __restrict__ scatter) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  gather[i] = i;
+  scatter[i] = nbr[(long long)i * 27 + 13];
+}
+
 }  // namespace
 
 extern "C" {
@@ -611,6 +765,100 @@ int sfx_subm_conv(int n, int cin, int cout, const float* x, long long ldx, const
   b.M = pair_off_host[27];
   dispatch(b, 1, vec, st);
   return sfx::check_launch("sfx_subm_conv(pairs)");
+}
+
+// SubMConv3d backward w.r.t. its input: dX[in] += dY[out] W_k for every pair (in, out, k), centre included.
+// weight_t = the [Cout, 27*Cin] weight transposed to [27*Cin, Cout] (sfx_transpose; cached by the caller);
+// centre_ws = 2n ints of scratch.  dX is accumulated into (float atomics): zero it or pass the residual
+// gradient it should be added to.
+int sfx_subm_conv_bwd_data(int n, int cin, int cout, const float* dy, long long ldy, const int* nbr,
+                           const float* weight_t, const int* pair_in, const int* pair_out, const int* pair_off_host,
+                           int* centre_ws, float* dx, long long lddx, void* stream) {
+  SFX_REQUIRE(n >= 0 && cin > 0 && cout > 0, "sfx_subm_conv_bwd_data: bad sizes");
+  if (n == 0) return SFX_OK;
+  SFX_REQUIRE(dy && nbr && weight_t && dx && pair_off_host && centre_ws, "sfx_subm_conv_bwd_data: null buffer");
+  SFX_REQUIRE(ldy >= cout && lddx >= cin, "sfx_subm_conv_bwd_data: leading dimension too small");
+  SFX_REQUIRE(fits(n, ldy) && fits(n, lddx) && fits(27ll * cin, cout),
+              "sfx_subm_conv_bwd_data: operand exceeds the 2 GiB buffer-descriptor range");
+  hipStream_t st = sfx::as_stream(stream);
+  const bool vec = (cout % 4 == 0) && (ldy % 4 == 0) && aligned16(dy) && aligned16(weight_t);
+  int* cg = centre_ws;
+  int* cs = centre_ws + n;
+  centre_pairs_kernel<<<sfx::ceil_div(n, 256), 256, 0, st>>>(n, nbr, cg, cs);
+  GemmArgs a{};
+  a.N = cin; a.K = cout; a.A = dy; a.lda = ldy; a.S = 1; a.Kseg = cout; a.gstride = 1;
+  a.ldw = cout; a.act = 0; a.act_ncols = cin; a.Y = dx; a.ldy = lddx;
+  a.pair_mode = 1; a.slice_w_stride = (long long)cin * cout;
+  // centre offset (k = 13) as a one-slice pair launch
+  GemmArgs c = a;
+  c.pair_in = cg; c.pair_out = cs; c.W = weight_t + 13ll * cin * cout; c.num_slices = 1;
+  c.slice_pair_off[0] = 0; c.slice_pair_off[1] = n; c.M = n;
+  dispatch(c, 1, vec, st);
+  int rc = sfx::check_launch("sfx_subm_conv_bwd_data(centre)");
+  if (rc || !pair_in || pair_off_host[27] == 0) return rc;
+  // the 26 other offsets: roles of the forward pair lists swapped
+  GemmArgs b = a;
+  b.pair_in = pair_out; b.pair_out = pair_in; b.W = weight_t; b.num_slices = 27;
+  for (int k = 0; k <= 27; ++k) b.slice_pair_off[k] = pair_off_host[k];
+  b.M = pair_off_host[27];
+  dispatch(b, 1, vec, st);
+  return sfx::check_launch("sfx_subm_conv_bwd_data(pairs)");
+}
+
+int sfx_linear_bwd_data(int M, int N, int K, const float* dY, long long ldy, const float* Wt, long long ldwt,
+                        const float* rowscale, int dact, int dact_ncols, const float* dact_pre, long long ld_pre,
+                        float* dX, long long lddx, int accumulate, void* stream) {
+  SFX_REQUIRE(M >= 0 && N > 0 && K > 0, "sfx_linear_bwd_data: bad sizes M=%d N=%d K=%d", M, N, K);
+  SFX_REQUIRE(dact >= 0 && dact <= 3, "sfx_linear_bwd_data: bad dact %d", dact);
+  if (M == 0) return SFX_OK;
+  SFX_REQUIRE(dY && Wt && dX && (!dact || dact_pre), "sfx_linear_bwd_data: null buffer");
+  SFX_REQUIRE(ldy >= N && ldwt >= N && lddx >= K && (!dact || ld_pre >= K), "sfx_linear_bwd_data: leading dim");
+  SFX_REQUIRE(fits(M, ldy) && fits(K, ldwt) && fits(M, lddx) && (!dact || fits(M, ld_pre)),
+              "sfx_linear_bwd_data: operand exceeds the 2 GiB buffer-descriptor range");
+  GemmArgs a{};
+  a.M = M; a.N = K; a.K = N; a.A = dY; a.lda = ldy; a.S = 1; a.Kseg = N; a.gstride = 1;
+  a.W = Wt; a.ldw = ldwt; a.act = 0; a.act_ncols = dact_ncols < 0 ? K : dact_ncols;
+  a.Y = dX; a.ldy = lddx;
+  if (accumulate) { a.R = dX; a.ldr = lddx; }
+  a.rowscale = rowscale; a.dact = dact; a.dact_pre = dact_pre; a.ld_dact = ld_pre;
+  const bool vec = (N % 4 == 0) && (ldy % 4 == 0) && (ldwt % 4 == 0) && aligned16(dY) && aligned16(Wt);
+  dispatch(a, 1, vec, sfx::as_stream(stream));
+  return sfx::check_launch("sfx_linear_bwd_data");
+}
+
+int sfx_linear_wgrad(int M, int N, int K, const float* dY, long long ldy, const float* X, long long ldx, float* dW,
+                     long long ldw, float* db, void* stream) {
+  SFX_REQUIRE(M >= 0 && N > 0 && K > 0, "sfx_linear_wgrad: bad sizes M=%d N=%d K=%d", M, N, K);
+  if (M == 0) return SFX_OK;
+  SFX_REQUIRE(dY && X && dW, "sfx_linear_wgrad: null buffer");
+  SFX_REQUIRE(N % 4 == 0 && K % 4 == 0 && ldy % 4 == 0 && ldx % 4 == 0 && aligned16(dY) && aligned16(X),
+              "sfx_linear_wgrad: N, K, leading dims must be multiples of 4 and operands 16-byte aligned");
+  SFX_REQUIRE(ldy >= N && ldx >= K && ldw >= K, "sfx_linear_wgrad: leading dim");
+  SFX_REQUIRE(fits(M, ldy) && fits(M, ldx) && fits(N, ldw), "sfx_linear_wgrad: operand exceeds 2 GiB range");
+  hipStream_t st = sfx::as_stream(stream);
+  const int tiles = (int)(sfx::ceil_div(N, WG_TILE) * sfx::ceil_div(K, WG_TILE));
+  const int slabs = (int)sfx::ceil_div(M, BK);
+  int splits = (int)sfx::ceil_div(4 * num_cus(), tiles);
+  if (splits > slabs) splits = slabs;
+  if (splits < 1) splits = 1;
+  const int chunk = (int)sfx::ceil_div(slabs, splits) * BK;
+  splits = (int)sfx::ceil_div(M, chunk);
+  wgrad_kernel<<<dim3(tiles, splits), THREADS, 0, st>>>(M, N, K, dY, ldy, X, ldx, dW, ldw, chunk);
+  int rc = sfx::check_launch("sfx_linear_wgrad");
+  if (rc || !db) return rc;
+  const int rows_per_block = 1024;
+  colsum_kernel<<<dim3(sfx::ceil_div(N, 64), sfx::ceil_div(M, rows_per_block)), 256, 0, st>>>(M, N, dY, ldy, db,
+                                                                                              rows_per_block);
+  return sfx::check_launch("sfx_linear_wgrad(bias)");
+}
+
+int sfx_transpose(int rows, int cols, const float* src, long long lds, float* dst, long long ldd, void* stream) {
+  SFX_REQUIRE(rows >= 0 && cols >= 0 && lds >= cols && ldd >= rows, "sfx_transpose: bad sizes");
+  if (rows == 0 || cols == 0) return SFX_OK;
+  SFX_REQUIRE(src && dst, "sfx_transpose: null buffer");
+  transpose_kernel<<<dim3(sfx::ceil_div(cols, 32), sfx::ceil_div(rows, 32)), 256, 0, sfx::as_stream(stream)>>>(
+      rows, cols, src, lds, dst, ldd);
+  return sfx::check_launch("sfx_transpose");
 }
 
 }  // extern "C"

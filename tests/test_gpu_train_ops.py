@@ -1,0 +1,209 @@
+"""Training-mode HIP ops vs torch autograd of the CPU oracle math (fp32, same inputs).
+
+Tolerance: relative L2 <= 1e-5 on every gradient (north-star fp32 tolerance), 1e-6 where the op is a
+single GEMM; integer arg-max outputs bit-exact."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import ptv3_ref
+from splatformer_amd import ptv3_ops as ops
+from splatformer_amd import train_ops as tops
+
+pytestmark = pytest.mark.gpu
+
+
+def rel_l2(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+
+@pytest.mark.parametrize("M,N,K,dact", [(1000, 64, 96, 0), (777, 384, 96, 1), (300, 128, 512, 2), (64, 23, 128, 3)])
+def test_linear_bwd_data(device, M, N, K, dact):
+    g = torch.Generator().manual_seed(M)
+    w = torch.randn(N, K, generator=g) / K ** 0.5
+    dy = torch.randn(M, N, generator=g)
+    pre = torch.randn(M, K, generator=g)
+    if dact == 3:
+        pre = torch.tanh(pre)
+    rs = (torch.rand(M, generator=g) > 0.3).float() / 0.7
+    base = torch.randn(M, K, generator=g)
+    ref = (dy @ w) * rs[:, None]
+    if dact == 1:
+        x = pre.clone().requires_grad_()
+        F.gelu(x).backward(torch.ones_like(x))
+        ref = ref * x.grad
+    elif dact == 2:
+        ref = ref * (pre > 0).float()
+    elif dact == 3:
+        ref = ref * (1 - pre * pre)
+    wt = tops.transpose(w.to(device))
+    assert torch.equal(wt.cpu(), w.T.contiguous())
+    out = base.to(device).clone()
+    tops.linear_bwd_data(dy.to(device), wt, rowscale=rs.to(device), dact=dact, dact_pre=pre.to(device), out=out,
+                         accumulate=True)
+    assert rel_l2(out, ref + base) < 2e-6
+
+
+@pytest.mark.parametrize("M,N,K", [(100000, 192, 64), (777, 384, 128), (33, 1536, 512)])
+def test_linear_wgrad(device, M, N, K):
+    g = torch.Generator().manual_seed(N)
+    dy = torch.randn(M, N, generator=g)
+    x = torch.randn(M, K, generator=g)
+    dw0 = torch.randn(N, K, generator=g)
+    db0 = torch.randn(N, generator=g)
+    dw, db = dw0.to(device), db0.to(device)
+    tops.linear_wgrad(dy.to(device), x.to(device), dw, db)
+    assert rel_l2(dw, dw0 + dy.double().T @ x.double()) < 1e-5
+    assert rel_l2(db, db0 + dy.double().sum(0)) < 1e-5
+
+
+@pytest.mark.parametrize("n,cin,cout,dup", [(3000, 64, 64, False), (2000, 96, 128, True), (500, 256, 256, False)])
+def test_subm_conv_bwd_data(device, n, cin, cout, dup):
+    g = torch.Generator().manual_seed(n)
+    grid = torch.randint(0, 24, (n, 3), generator=g).int()
+    if dup:
+        grid[n // 2:n // 2 + 50] = grid[:50]  # duplicate voxels -> centre maps to the lowest index
+    batch = torch.zeros(n, dtype=torch.int32)
+    nbr = ptv3_ref.subm_neighbors(grid, batch)
+    w = torch.randn(cout, 3, 3, 3, cin, generator=g) / (27 * cin) ** 0.5
+    b = torch.randn(cout, generator=g)
+    x = torch.randn(n, cin, generator=g, requires_grad=True)
+    dy = torch.randn(n, cout, generator=g)
+    ptv3_ref.subm_conv(x, nbr, w, b).backward(dy)
+    smap = ops.subm_neighbors(grid.to(device), None)
+    wt = tops.transpose(w.reshape(cout, 27 * cin).to(device))
+    base = torch.randn(n, cin, generator=g)
+    dx = base.to(device).clone()
+    tops.subm_conv_bwd_data(dy.to(device), smap, wt, dx)
+    assert rel_l2(dx, x.grad + base) < 1e-5
+
+
+@pytest.mark.parametrize("n,heads,C", [(1000, 2, 64), (777, 4, 96), (300, 8, 128), (100, 2, 32), (1500, 16, 256)])
+def test_window_attention_bwd(device, n, heads, C):
+    g = torch.Generator().manual_seed(n + C)
+    qkv = torch.randn(n, 3 * C, generator=g, requires_grad=True)
+    order = torch.randperm(n, generator=g)
+    inverse = torch.empty_like(order)
+    inverse[order] = torch.arange(n)
+    K = min(n, 128)
+    pad, unpad = ptv3_ref.get_padding_and_inverse(torch.tensor([n]), K)
+    q, k, v = qkv[order[pad]].reshape(-1, K, 3, heads, C // heads).permute(2, 0, 3, 1, 4).unbind(0)
+    att = torch.softmax((q * (C // heads) ** -0.5) @ k.transpose(-2, -1), -1)
+    ref = (att @ v).transpose(1, 2).reshape(-1, C)[unpad[inverse]]
+    dout = torch.randn(n, C, generator=g)
+    ref.backward(dout)
+    tab = ops.window_table([n], K)
+    win = torch.tensor(tab, dtype=torch.int32).to(device)
+    dqkv = tops.window_attention_bwd(qkv.detach().to(device), order.int().to(device), win, len(tab), K, heads, C,
+                                     dout.to(device))
+    assert rel_l2(dqkv, qkv.grad) < 1e-5
+
+
+def test_layernorm_bwd_ops(device):
+    g = torch.Generator().manual_seed(3)
+    for C in (64, 96, 256, 512):
+        M = 999
+        x = (torch.randn(M, C, generator=g) * 2 + 0.5).requires_grad_()
+        ga, be = torch.randn(C, generator=g), torch.randn(C, generator=g)
+        dy = torch.randn(M, C, generator=g)
+        dr = torch.randn(M, C, generator=g)
+        F.layer_norm(x, (C,), ga, be, 1e-5).backward(dy)
+        got = tops.layernorm_bwd(x.detach().to(device), ga.to(device), dy.to(device), 1e-5, dres=dr.to(device))
+        assert rel_l2(got, x.grad + dr) < 1e-5
+        # fused block tail: x1 = x + LN_c(u); h = LN1(x1)
+        u = torch.randn(M, C, generator=g, requires_grad=True)
+        xx = torch.randn(M, C, generator=g)
+        gc, bc = torch.randn(C, generator=g), torch.randn(C, generator=g)
+        g1, b1 = torch.randn(C, generator=g), torch.randn(C, generator=g)
+        x1 = (xx + F.layer_norm(u, (C,), gc, bc, 1e-5)).detach().requires_grad_()
+        h = F.layer_norm(x1, (C,), g1, b1, 1e-5)
+        dh = torch.randn(M, C, generator=g)
+        dx2 = torch.randn(M, C, generator=g)
+        h.backward(dh)
+        dx1_ref = x1.grad + dx2
+        F.layer_norm(u, (C,), gc, bc, 1e-5).backward(dx1_ref)
+        dx1, du = tops.cpe_ln_bwd(u.detach().to(device), x1.detach().to(device), gc.to(device), g1.to(device),
+                                  dx2.to(device), dh.to(device), 1e-5)
+        assert rel_l2(dx1, dx1_ref) < 1e-5
+        assert rel_l2(du, u.grad) < 1e-5
+
+
+@pytest.mark.parametrize("M,C", [(5000, 64), (777, 256), (3, 96)])
+def test_bn_train_fwd_bwd(device, M, C):
+    g = torch.Generator().manual_seed(M)
+    bn = torch.nn.BatchNorm1d(C, eps=1e-3, momentum=0.01)
+    with torch.no_grad():
+        bn.weight.copy_(torch.rand(C, generator=g) + 0.5)
+        bn.bias.copy_(torch.randn(C, generator=g))
+        bn.running_mean.copy_(torch.randn(C, generator=g))
+        bn.running_var.copy_(torch.rand(C, generator=g) + 0.5)
+    bn_dev = torch.nn.BatchNorm1d(C, eps=1e-3, momentum=0.01).to(device)
+    bn_dev.load_state_dict(bn.state_dict())
+    x = (torch.randn(M, C, generator=g) * 3 + 1).requires_grad_()
+    res = torch.randn(M // 2 + 1, C, generator=g)
+    ridx = torch.randint(0, M // 2 + 1, (M,), generator=g).int()
+    bn.train()
+    y_ref = F.gelu(bn(x)) + res[ridx.long()]
+    dy = torch.randn(M, C, generator=g)
+    y_ref.backward(dy)
+    y, st = tops.bn_train_forward(x.detach().to(device), bn_dev, 1, residual=res.to(device),
+                                  residual_idx=ridx.to(device))
+    assert rel_l2(y, y_ref) < 1e-5
+    assert rel_l2(bn_dev.running_mean, bn.running_mean) < 1e-6
+    assert rel_l2(bn_dev.running_var, bn.running_var) < 1e-6
+    dx = tops.bn_act_bwd(st, bn_dev, 1, dy.to(device))
+    assert rel_l2(dx, x.grad) < 1e-5
+
+
+def test_segment_ops(device):
+    g = torch.Generator().manual_seed(5)
+    n, C = 4000, 96
+    cluster = torch.randint(0, 900, (n,), generator=g)
+    _, cluster = torch.unique(cluster, return_inverse=True)
+    m = int(cluster.max()) + 1
+    sidx = torch.sort(cluster, stable=True).indices
+    counts = torch.bincount(cluster, minlength=m)
+    idx_ptr = torch.cat([torch.zeros(1, dtype=torch.long), torch.cumsum(counts, 0)])
+    x = torch.randn(n, C, generator=g, requires_grad=True)
+    seg = cluster
+    y_ref = torch.full((m, C), -float("inf")).scatter_reduce(0, seg[:, None].expand(n, C), x, reduce="amax",
+                                                            include_self=True)
+    dy = torch.randn(m, C, generator=g)
+    y_ref.backward(dy)
+    y, arg = tops.segment_max_arg(x.detach().to(device), idx_ptr.int().to(device), sidx.int().to(device), m)
+    assert torch.equal(y.cpu(), y_ref.detach())
+    dx = tops.segment_max_bwd(dy.to(device), arg, n)
+    assert rel_l2(dx, x.grad) < 1e-6
+    s = tops.segment_sum(x.detach().to(device), idx_ptr.int().to(device), sidx.int().to(device), m)
+    s_ref = torch.zeros(m, C).index_add_(0, seg, x.detach())
+    assert rel_l2(s, s_ref) < 1e-6
+
+
+def test_act_bwd_and_adam(device):
+    g = torch.Generator().manual_seed(6)
+    dy = torch.randn(500, 23, generator=g)
+    o = torch.tanh(torch.randn(500, 23, generator=g))
+    got = tops.act_bwd(dy.to(device), o.to(device), 3, ncols=3)
+    ref = dy.clone()
+    ref[:, :3] *= 1 - o[:, :3] ** 2
+    assert rel_l2(got, ref) < 1e-6
+    # clip_grad_norm_(2.0) + Adam(eps 1e-15) for 3 steps vs torch.optim
+    ps = [torch.randn(300, 64, generator=g), torch.randn(192, generator=g)]
+    ref_p = [p.clone().requires_grad_() for p in ps]
+    opt = torch.optim.Adam(ref_p, lr=3e-5, eps=1e-15)
+    dev_p = [p.to(device) for p in ps]
+    m1 = [torch.zeros_like(p) for p in dev_p]
+    m2 = [torch.zeros_like(p) for p in dev_p]
+    for step in range(1, 4):
+        grads = [torch.randn(p.shape, generator=g) * 3 for p in ps]
+        for p, gr in zip(ref_p, grads):
+            p.grad = gr.clone()
+        torch.nn.utils.clip_grad_norm_(ref_p, 2.0)
+        opt.step()
+        dg = [gr.to(device) for gr in grads]
+        coef, _ = tops.grad_clip_coef(dg, 2.0)
+        for p, gr, a, b in zip(dev_p, dg, m1, m2):
+            tops.adam_step(p, gr, a, b, step, 3e-5, eps=1e-15, grad_scale=coef)
+    for p, r in zip(dev_p, ref_p):
+        assert rel_l2(p, r) < 1e-6
