@@ -117,7 +117,8 @@ int sfx_linear(int M, int N, int K, const float* A, long long lda, const int* ga
                const float* W, long long ldw, const float* bias, const float* scale, const float* shift, int act,
                int act_ncols, const float* R, long long ldr, const int* residual_idx, float* Y, long long ldy,
                float* Ypre, long long ldypre, int groups, long long group_stride_A, long long group_stride_W,
-               long long group_stride_bias, long long group_stride_Y, const int* out_row_idx, void* stream);
+               long long group_stride_bias, long long group_stride_Y, const int* out_row_idx, const float* rowscale,
+               int pre_before_act, void* stream);
 
 /* ---- training (configs C/D): backward of the nn.Linear layers -------------------------------------
  * dX[M,K] (=|+=) rowscale[m] * (dY[M,N] W[N,K]) * act'(dact_pre[m,k]) for k < dact_ncols (-1 = all);

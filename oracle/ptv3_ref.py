@@ -54,9 +54,14 @@ def linear(x, sd, p):
     return F.linear(x, sd[p + ".weight"], sd.get(p + ".bias"))
 
 
-def bn(x, sd, p, eps):
+def bn(x, sd, p, eps, train=False):
+    """Eval: running statistics.  Train (model.train(), train.py:236): batch statistics; the running
+    statistics are updated on the state dict in place (momentum 0.01, pointtransformer_v3.py:252)."""
+    if not train:
+        return F.batch_norm(x, sd[p + ".running_mean"], sd[p + ".running_var"], sd[p + ".weight"], sd[p + ".bias"],
+                            False, 0.0, eps)
     return F.batch_norm(x, sd[p + ".running_mean"], sd[p + ".running_var"], sd[p + ".weight"], sd[p + ".bias"],
-                        False, 0.0, eps)
+                        True, 0.01, eps)
 
 
 def ln(x, sd, p, eps):
@@ -162,8 +167,10 @@ def serialized_attention(sd, p, point: Point, C, H, patch_size_max, order_index,
 
 
 # ---- Block ------------------------------------------------------------------
-def block(sd, p, point: Point, C, H, cfg: PTv3Config, order_index, conv_in=None):
-    """Block.forward (pre_norm=True, drop_path identity in eval; calflops.py:45-82)."""
+def block(sd, p, point: Point, C, H, cfg: PTv3Config, order_index, conv_in=None, masks=None):
+    """Block.forward (pre_norm=True; calflops.py:45-82).  DropPath (train): `masks[p + '.attn' / '.mlp']`
+    = the per-point keep/(1-p) multipliers timm's DropPath draws (identity in eval / when absent)."""
+    masks = masks or {}
     shortcut = point.feat
     x = subm_conv(point.feat if conv_in is None else conv_in, point.nbr, sd[p + ".cpe.0.weight"],
                   sd[p + ".cpe.0.bias"])
@@ -173,16 +180,20 @@ def block(sd, p, point: Point, C, H, cfg: PTv3Config, order_index, conv_in=None)
     shortcut = feat
     h = ln(feat, sd, p + ".norm1.0", cfg.ln_eps)
     h = serialized_attention(sd, p + ".attn", point, C, H, cfg.patch_size, order_index, h)
+    if masks.get(p + ".attn") is not None:
+        h = h * masks[p + ".attn"][:, None]
     feat = shortcut + h
     shortcut = feat
     h = ln(feat, sd, p + ".norm2.0", cfg.ln_eps)
     h = linear(gelu(linear(h, sd, p + ".mlp.0.fc1")), sd, p + ".mlp.0.fc2")
+    if masks.get(p + ".mlp") is not None:
+        h = h * masks[p + ".mlp"][:, None]
     point.feat = shortcut + h
     return point
 
 
 # ---- pooling / unpooling ------------------------------------------------------
-def serialized_pooling(sd, p, point: Point, stride, cfg: PTv3Config, perm):
+def serialized_pooling(sd, p, point: Point, stride, cfg: PTv3Config, perm, train=False):
     pooling_depth = (math.ceil(stride) - 1).bit_length()
     if pooling_depth > point.serialized_depth:
         pooling_depth = 0
@@ -208,15 +219,15 @@ def serialized_pooling(sd, p, point: Point, stride, cfg: PTv3Config, perm):
                 serialized_depth=point.serialized_depth - pooling_depth, batch=point.batch[head_indices],
                 pooling_inverse=cluster, pooling_parent=point)
     new.offset = torch.cumsum(torch.bincount(new.batch), 0)
-    new.feat = gelu(bn(new.feat, sd, p + ".norm.0", cfg.bn_eps))
+    new.feat = gelu(bn(new.feat, sd, p + ".norm.0", cfg.bn_eps, train))
     return new
 
 
-def serialized_unpooling(sd, p, point: Point, cfg: PTv3Config):
+def serialized_unpooling(sd, p, point: Point, cfg: PTv3Config, train=False):
     parent = point.pooling_parent
     inverse = point.pooling_inverse
-    coarse = gelu(bn(linear(point.feat, sd, p + ".proj.0"), sd, p + ".proj.1", cfg.bn_eps))
-    skip = gelu(bn(linear(parent.feat, sd, p + ".proj_skip.0"), sd, p + ".proj_skip.1", cfg.bn_eps))
+    coarse = gelu(bn(linear(point.feat, sd, p + ".proj.0"), sd, p + ".proj.1", cfg.bn_eps, train))
+    skip = gelu(bn(linear(parent.feat, sd, p + ".proj_skip.0"), sd, p + ".proj_skip.1", cfg.bn_eps, train))
     parent.feat = skip + coarse[inverse]
     parent.stale_conv_feat = skip  # sparse_conv_feat is not refreshed by SerializedUnpooling
     return parent
@@ -224,29 +235,32 @@ def serialized_unpooling(sd, p, point: Point, cfg: PTv3Config):
 
 # ---- whole backbone -----------------------------------------------------------
 def ptv3_forward(sd: Dict[str, torch.Tensor], cfg: PTv3Config, data: Dict[str, torch.Tensor],
-                 perms: List[Sequence[int]], prefix: str = "backbone.") -> Point:
-    """PointTransformerV3.forward (pointtransformer_v3.py:378-392); `perms` = the 5 randperm(4) draws."""
+                 perms: List[Sequence[int]], prefix: str = "backbone.", train: bool = False,
+                 masks: Optional[Dict[str, torch.Tensor]] = None) -> Point:
+    """PointTransformerV3.forward (pointtransformer_v3.py:378-392); `perms` = the 5 randperm(4) draws.
+    train=True: batch-statistics BatchNorm + the DropPath `masks` (keys '<enc.enc0.block1>.attn' / '.mlp')."""
     sd = {k[len(prefix):]: v for k, v in sd.items() if k.startswith(prefix)}
     point = Point(coord=data["coord"], grid_coord=data["grid_coord"], offset=data["offset"], feat=data["feat"])
     point.batch = offset2batch(point.offset)
     serialize(point, perms[0])
     point.nbr = subm_neighbors(point.grid_coord, point.batch)
     # embedding: Linear -> BN -> GELU
-    point.feat = gelu(bn(linear(point.feat, sd, "embedding.0"), sd, "embedding.1", cfg.bn_eps))
+    point.feat = gelu(bn(linear(point.feat, sd, "embedding.0"), sd, "embedding.1", cfg.bn_eps, train))
     pi = 1
     for s in range(cfg.num_stages):
         if s > 0:
-            point = serialized_pooling(sd, f"enc.enc{s}.down", point, cfg.stride[s - 1], cfg, perms[pi])
+            point = serialized_pooling(sd, f"enc.enc{s}.down", point, cfg.stride[s - 1], cfg, perms[pi], train)
             pi += 1
             point.nbr = subm_neighbors(point.grid_coord, point.batch)
         for i in range(cfg.enc_depths[s]):
-            point = block(sd, f"enc.enc{s}.block{i}", point, cfg.enc_channels[s], cfg.enc_num_head[s], cfg, i % 4)
+            point = block(sd, f"enc.enc{s}.block{i}", point, cfg.enc_channels[s], cfg.enc_num_head[s], cfg, i % 4,
+                          masks=masks)
     for s in reversed(range(cfg.num_stages - 1)):
-        point = serialized_unpooling(sd, f"dec.dec{s}.up", point, cfg)
+        point = serialized_unpooling(sd, f"dec.dec{s}.up", point, cfg, train)
         for i in range(cfg.dec_depths[s]):
             conv_in = point.pop("stale_conv_feat") if i == 0 else None
             point = block(sd, f"dec.dec{s}.block{i}", point, cfg.dec_channels[s], cfg.dec_num_head[s], cfg, i % 4,
-                          conv_in=conv_in)
+                          conv_in=conv_in, masks=masks)
     return point
 
 
@@ -285,7 +299,7 @@ def heads_forward(sd, y: torch.Tensor, feat: torch.Tensor, in_gs: Dict[str, torc
 
 
 def feature_predictor_forward(sd, cfg: PTv3Config, gs: Dict[str, torch.Tensor], perms, sh_degree=1,
-                              grid_resolution=384):
+                              grid_resolution=384, train=False, masks=None):
     data = batchify(gs, grid_resolution)
-    point = ptv3_forward(sd, cfg, data, perms, prefix="backbone.backbone.")
+    point = ptv3_forward(sd, cfg, data, perms, prefix="backbone.backbone.", train=train, masks=masks)
     return heads_forward(sd, point.feat, data["feat"], gs, sh_degree), point

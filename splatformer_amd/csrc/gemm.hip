@@ -74,6 +74,7 @@ struct GemmArgs {
   // backward-pass epilogue terms (applied after the activation): v *= rowscale[row] (drop-path masks),
   // v *= act'(dact_pre[row, col]) for cols < act_ncols (GELU / ReLU on the pre-activation, tanh on its output)
   const float* rowscale;
+  int pre_before_act;  // Ypre receives the pre-activation value (training forward saves it for act')
   const float* dact_pre;
   long long ld_dact;
   int dact;
@@ -349,6 +350,13 @@ __global__ void __launch_bounds__(THREADS, 2) gemm_kernel(GemmArgs p, int tiles_
         float v[16];
 #pragma unroll
         for (int r = 0; r < 16; ++r) v[r] = (acc[a][b][r] + ebias[b]) * escale[b] + eshift[b];
+        if (p.Ypre && p.pre_before_act) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int m = mrow[a][r];
+            bstore1(rP, (nok && m >= 0) ? ((unsigned)m * ldp32 + (unsigned)n) * 4u : OOB, v[r]);
+          }
+        }
         if (p.act == ACT_GELU) {
 #pragma unroll
           for (int r = 0; r < 16; ++r) v[r] = do_act ? gelu_erf(v[r]) : v[r];
@@ -379,7 +387,7 @@ __global__ void __launch_bounds__(THREADS, 2) gemm_kernel(GemmArgs p, int tiles_
 #pragma unroll
           for (int r = 0; r < 16; ++r) v[r] = do_act ? v[r] * dact_grad(p.dact, pre[r]) : v[r];
         }
-        if (p.Ypre) {
+        if (p.Ypre && !p.pre_before_act) {
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const int m = mrow[a][r];
@@ -707,7 +715,8 @@ int sfx_linear(int M, int N, int K, const float* A, long long lda, const int* ga
                const float* W, long long ldw, const float* bias, const float* scale, const float* shift, int act,
                int act_ncols, const float* R, long long ldr, const int* residual_idx, float* Y, long long ldy,
                float* Ypre, long long ldypre, int groups, long long group_stride_A, long long group_stride_W,
-               long long group_stride_bias, long long group_stride_Y, const int* out_row_idx, void* stream) {
+               long long group_stride_bias, long long group_stride_Y, const int* out_row_idx, const float* rowscale,
+               int pre_before_act, void* stream) {
   SFX_REQUIRE(M >= 0 && N > 0 && K > 0, "sfx_linear: bad sizes M=%d N=%d K=%d", M, N, K);
   SFX_REQUIRE(act >= 0 && act <= 3, "sfx_linear: bad activation %d", act);
   SFX_REQUIRE(groups >= 1, "sfx_linear: groups < 1");
@@ -727,7 +736,7 @@ int sfx_linear(int M, int N, int K, const float* A, long long lda, const int* ga
   a.W = W; a.ldw = ldw; a.bias = bias; a.scale = scale; a.shift = shift; a.act = act;
   a.act_ncols = act_ncols < 0 ? N : act_ncols; a.R = R; a.ldr = ldr; a.ridx = residual_idx; a.Y = Y; a.ldy = ldy;
   a.Ypre = Ypre; a.ldypre = ldypre; a.gA = group_stride_A; a.gW = group_stride_W; a.gB = group_stride_bias;
-  a.gY = group_stride_Y; a.out_rows = out_row_idx;
+  a.gY = group_stride_Y; a.out_rows = out_row_idx; a.rowscale = rowscale; a.pre_before_act = pre_before_act;
   const bool vec = (K % 4 == 0) && (lda % 4 == 0) && (ldw % 4 == 0) && aligned16(A) && aligned16(W) &&
                    (group_stride_A % 4 == 0) && (group_stride_W % 4 == 0);
   dispatch(a, groups, vec, sfx::as_stream(stream));

@@ -99,7 +99,8 @@ class Block(nn.Module):
         self.attn = SerializedAttention(channels, num_heads, patch_size, order_index)
         self.norm2 = PointSequential(nn.LayerNorm(channels))
         self.mlp = PointSequential(MLP(channels, int(channels * mlp_ratio), channels))
-        self.drop_path = PointSequential(nn.Identity())
+        self.drop_path = PointSequential(nn.Identity())  # DropPath has no parameters; rate in drop_prob
+        self.drop_prob = 0.0
 
     def run(self, point: Point, conv_in: Optional[Tensor] = None, out: Optional[Tensor] = None) -> Point:
         """Block.forward (calflops.py:45-82): x += LN(Lin(SubMConv(x))); x += attn(LN1 x); x += MLP(LN2 x)."""
@@ -147,22 +148,20 @@ class SerializedPooling(nn.Module):
         self.norm = PointSequential(norm_layer(out_channels))
         self.act = PointSequential(act_layer())
 
-    def run(self, point: Point, perm: Sequence[int]) -> Point:
+    def geometry(self, point: Point, perm: Sequence[int]):
+        """The integer half of SerializedPooling.forward: clusters (code >> 3*pd, unique), their sorted members
+        (sidx / idx_ptr CSR), the pooled coords, codes, orders and neighbour map.  -> (new Point, sidx, idx_ptr, m)"""
         pd = (math.ceil(self.stride) - 1).bit_length()
         if pd > point.serialized_depth:
             pd = 0
-        dev = point.feat.device
         row0 = point.order_type[0]
         sidx, cluster, idx_ptr, head, m = ops.pool_clusters(point.codes_phys[row0], pd, point.code_bits)
         depth = point.serialized_depth - pd
         code_bits = point.code_bits - 3 * pd
         codes, order, inverse, grid, batch = ops.pool_gather(head, m, point.codes_phys, pd, point.grid_coord,
                                                              point.get("batch"), code_bits)
-        pf = ops.linear(point.feat, self.proj.weight, self.proj.bias)
-        sc, sh = bn_affine(self.norm[0])
-        feat = ops.segment_max_affine_act(pf, idx_ptr, sidx, m, sc, sh, ops.ACT_GELU)
         coord = ops.segment_mean(point.coord, idx_ptr, sidx, m)
-        new = Point(feat=feat, coord=coord, grid_coord=grid, codes_phys=codes, order_phys=order,
+        new = Point(coord=coord, grid_coord=grid, codes_phys=codes, order_phys=order,
                     inverse_phys=inverse, order_type=[point.order_type[p] for p in perm],
                     serialized_depth=depth, code_bits=code_bits, pooling_inverse=cluster, pooling_parent=point)
         if batch is not None:
@@ -171,6 +170,13 @@ class SerializedPooling(nn.Module):
         else:
             new.offset = [m]
         new.nbr = ops.subm_neighbors(grid, new.get("batch"))
+        return new, sidx, idx_ptr, m
+
+    def run(self, point: Point, perm: Sequence[int]) -> Point:
+        new, sidx, idx_ptr, m = self.geometry(point, perm)
+        pf = ops.linear(point.feat, self.proj.weight, self.proj.bias)
+        sc, sh = bn_affine(self.norm[0])
+        new.feat = ops.segment_max_affine_act(pf, idx_ptr, sidx, m, sc, sh, ops.ACT_GELU)
         return new
 
 
@@ -219,7 +225,7 @@ class PointTransformerV3(nn.Module):
                  enc_channels=(32, 64, 128, 256, 512), enc_num_head=(2, 4, 8, 16, 32),
                  enc_patch_size=(48, 48, 48, 48, 48), dec_depths=(2, 2, 2, 2), dec_channels=(64, 64, 128, 256),
                  dec_num_head=(4, 4, 8, 16), dec_patch_size=(48, 48, 48, 48), mlp_ratio=4, turn_off_bn=False,
-                 shuffle_orders=True, embedding_type="MLP"):
+                 shuffle_orders=True, embedding_type="MLP", drop_path=0.3):
         super().__init__()
         if turn_off_bn:
             raise NotImplementedError("turn_off_bn=True is not on the SplatFormer path (ptv3_base.gin:30)")
@@ -243,6 +249,13 @@ class PointTransformerV3(nn.Module):
                 enc.add(Block(enc_channels[s], enc_num_head[s], enc_patch_size[s], mlp_ratio, i % len(self.order),
                               f"stage{s}"), f"block{i}")
             self.enc.add(enc, f"enc{s}")
+        # DropPath schedule (reference pointtransformer_v3.py:280-287, :330-339): linspace(0, p) over the
+        # encoder blocks in order, and over the decoder blocks with each stage's slice reversed
+        enc_dp = torch.linspace(0, drop_path, sum(enc_depths)).tolist()
+        for s in range(self.num_stages):
+            stage = getattr(self.enc, f"enc{s}")
+            for i in range(enc_depths[s]):
+                getattr(stage, f"block{i}").drop_prob = enc_dp[sum(enc_depths[:s]) + i]
         self.dec = _Container()
         dch = list(dec_channels) + [enc_channels[-1]]
         for s in reversed(range(self.num_stages - 1)):
@@ -252,6 +265,12 @@ class PointTransformerV3(nn.Module):
                 dec.add(Block(dch[s], dec_num_head[s], dec_patch_size[s], mlp_ratio, i % len(self.order),
                               f"stage{s}"), f"block{i}")
             self.dec.add(dec, f"dec{s}")
+        dec_dp = torch.linspace(0, drop_path, sum(dec_depths)).tolist()
+        for s in range(self.num_stages - 1):
+            sl = dec_dp[sum(dec_depths[:s]):sum(dec_depths[:s + 1])][::-1]
+            stage = getattr(self.dec, f"dec{s}")
+            for i in range(dec_depths[s]):
+                getattr(stage, f"block{i}").drop_prob = sl[i]
         self.last_perms: List[List[int]] = []
 
     def _draw_perm(self, perms_override, k):
@@ -264,8 +283,8 @@ class PointTransformerV3(nn.Module):
         self.last_perms.append(p)
         return p
 
-    @torch.no_grad()
-    def forward(self, data_dict, perms: Optional[List[Sequence[int]]] = None, out: Optional[Tensor] = None) -> Point:
+    def prepare(self, data_dict, perms: Optional[List[Sequence[int]]] = None) -> Point:
+        """Point + serialization (randperm draw 0) + stage-0 neighbour map; `feat` is not embedded yet."""
         feat = data_dict["feat"]
         _lib.require_gpu(feat)
         dev = feat.device
@@ -294,6 +313,12 @@ class PointTransformerV3(nn.Module):
         if batch is not None:
             point.batch = batch
         point.nbr = ops.subm_neighbors(grid, batch)
+        return point
+
+    @torch.no_grad()
+    def forward(self, data_dict, perms: Optional[List[Sequence[int]]] = None, out: Optional[Tensor] = None) -> Point:
+        point = self.prepare(data_dict, perms)
+        feat = data_dict["feat"]
         emb, bnm = self.embedding[0], self.embedding[1]
         sc, sh = bn_affine(bnm)
         point.feat = ops.linear(feat, emb.weight, emb.bias, scale=sc, shift=sh, act=ops.ACT_GELU)

@@ -14,7 +14,8 @@ from torch import Tensor
 from . import _lib
 from ._lib import I, L, P, F, Z, call, ptr, stream
 
-_lib.register("sfx_linear", [I, I, I, P, L, P, I, P, L, P, P, P, I, I, P, L, P, P, L, P, L, I, L, L, L, L, P, P])
+_lib.register("sfx_linear", [I, I, I, P, L, P, I, P, L, P, P, P, I, I, P, L, P, P, L, P, L, I, L, L, L, L, P, P, I,
+                              P])
 _lib.register("sfx_layernorm", [I, I, P, L, P, P, F, P, L, P])
 _lib.register("sfx_cpe_residual_ln", [I, I, P, P, P, P, P, P, F, P, P, P])
 _lib.register("sfx_window_attention", [I, I, I, I, I, P, P, P, F, P, P])
@@ -53,11 +54,14 @@ def linear(x: Tensor, weight: Tensor, bias: Optional[Tensor] = None, *, act: int
            scale: Optional[Tensor] = None, shift: Optional[Tensor] = None, residual: Optional[Tensor] = None,
            residual_idx: Optional[Tensor] = None, out: Optional[Tensor] = None, pre_out: Optional[Tensor] = None,
            gather_idx: Optional[Tensor] = None, rows: Optional[int] = None,
-           out_rows: Optional[Tensor] = None) -> Tensor:
+           out_rows: Optional[Tensor] = None, rowscale: Optional[Tensor] = None,
+           pre_before_act: bool = False) -> Tensor:
     """y = act((x W^T + b) * scale + shift) + residual[residual_idx]  (fp32 MFMA GEMM, csrc/gemm.hip).
 
     With `gather_idx` [M, S] (int32, -1 = empty) the A operand is the implicit
-    concatenation of S gathered rows of `x` (SubMConv3d as implicit GEMM)."""
+    concatenation of S gathered rows of `x` (SubMConv3d as implicit GEMM).
+    Training forward: `rowscale` multiplies each row's branch value before the residual add (DropPath),
+    `pre_out` + `pre_before_act` saves the pre-activation for the backward."""
     N, K = weight.shape
     if gather_idx is not None:
         M = gather_idx.shape[0]
@@ -77,7 +81,8 @@ def linear(x: Tensor, weight: Tensor, bias: Optional[Tensor] = None, *, act: int
     pr, ldr = _rows(residual) if residual is not None else (None, 0)
     pp, ldp = _rows(pre_out) if pre_out is not None else (None, 0)
     call("sfx_linear", M, N, K, pa, lda, ptr(gather_idx), S, pw, ldw, ptr(bias), ptr(scale), ptr(shift), act,
-         act_ncols, pr, ldr, ptr(residual_idx), py, ldy, pp, ldp, 1, 0, 0, 0, 0, ptr(out_rows), stream())
+         act_ncols, pr, ldr, ptr(residual_idx), py, ldy, pp, ldp, 1, 0, 0, 0, 0, ptr(out_rows), ptr(rowscale),
+         1 if pre_before_act else 0, stream())
     return out
 
 
@@ -91,7 +96,7 @@ def grouped_linear(x: Tensor, weight: Tensor, bias: Tensor, groups: int, *, act:
     pa, lda = _rows(x)
     py, ldy = _rows(out)
     call("sfx_linear", M, N, K, pa, lda, None, 1, ptr(weight), K, ptr(bias), None, None, act, -1, None, 0, None, py,
-         ldy, None, 0, G, K, N * K, N, N, None, stream())
+         ldy, None, 0, G, K, N * K, N, N, None, None, 0, stream())
     return out
 
 

@@ -124,11 +124,12 @@ def cpe_ln_bwd(u: Tensor, x1: Tensor, g_cpe: Tensor, g1: Tensor, dx2: Tensor, dh
 
 # ---- BatchNorm1d in train mode (+ GELU) ---------------------------------------------------------------
 class BNState:
-    """What the backward needs from a train-mode BN forward: input, batch mean/rstd, global row count."""
-    __slots__ = ("x", "mean", "rstd", "count")
+    """What the backward needs from a train-mode BN forward: input, batch mean/rstd, global row count
+    (and the folded scale/shift, to apply the same normalisation again)."""
+    __slots__ = ("x", "mean", "rstd", "count", "scale", "shift")
 
-    def __init__(self, x, mean, rstd, count):
-        self.x, self.mean, self.rstd, self.count = x, mean, rstd, count
+    def __init__(self, x, mean, rstd, count, scale, shift):
+        self.x, self.mean, self.rstd, self.count, self.scale, self.shift = x, mean, rstd, count, scale, shift
 
 
 def _colsum_ws(M: int, Cc: int, dev) -> Tuple[Tensor, int]:
@@ -173,7 +174,22 @@ def bn_train_forward(x: Tensor, bn: torch.nn.BatchNorm1d, act: int, residual: Op
     pr, ldr = (None, 0) if residual is None else _rows(residual)
     call("sfx_affine_act", M, Cc, px, ldx, ptr(scale), ptr(shift), act, pr, ldr, ptr(residual_idx, torch.int32),
          po, ldo, stream())
-    return out, BNState(x, mean, rstd, count)
+    return out, BNState(x, mean, rstd, count, scale, shift)
+
+
+def bn_apply(st: BNState, act: int, residual: Optional[Tensor] = None, residual_idx: Optional[Tensor] = None,
+             out: Optional[Tensor] = None) -> Tensor:
+    """act(x*scale + shift) (+ residual[residual_idx]) with the statistics of an earlier bn_train_forward."""
+    x = st.x
+    M, Cc = x.shape
+    if out is None:
+        out = torch.empty(M, Cc, device=x.device, dtype=torch.float32)
+    px, ldx = _rows(x)
+    po, ldo = _rows(out)
+    pr, ldr = (None, 0) if residual is None else _rows(residual)
+    call("sfx_affine_act", M, Cc, px, ldx, ptr(st.scale), ptr(st.shift), act, pr, ldr,
+         ptr(residual_idx, torch.int32), po, ldo, stream())
+    return out
 
 
 def bn_act_bwd(st: BNState, bn: torch.nn.BatchNorm1d, act: int, dy: Tensor, out: Optional[Tensor] = None,
