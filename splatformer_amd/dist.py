@@ -7,6 +7,10 @@ parallelism is the scene:
   `reduce` and divided by the global image count (train.py:170-176);
 - timing: barrier + max over ranks (the bench contract).
 
+Training (config D): one scene per rank per micro-step; the only exchanges are the gradient bucket
+all-reduce per optimiser step (DDP average, one flat fp32 bucket) and SyncBatchNorm's per-layer column
+sums (train.py:404) -- both below.
+
 Backend "nccl" is RCCL on ROCm; the CPU tests drive the same code with "gloo".
 """
 from __future__ import annotations
@@ -84,3 +88,22 @@ def reduce_metrics(metric_sums: Dict[str, torch.Tensor], num_images: int, num_sc
     out["num_images"] = int(n_img.item())
     out["num_scenes"] = int(n_scn.item())
     return out
+
+
+def allreduce_mean_(flat: torch.Tensor, group=None) -> torch.Tensor:
+    """DDP gradient averaging on one flat bucket: sum over ranks, divide by the world size (in place)."""
+    if not (tdist.is_available() and tdist.is_initialized()):
+        return flat
+    ws = tdist.get_world_size(group)
+    if ws > 1:
+        tdist.all_reduce(flat, group=group)
+        flat.div_(ws)
+    return flat
+
+
+def allreduce_sum_(t: torch.Tensor, group=None) -> torch.Tensor:
+    """SyncBatchNorm statistics: per-column sums (and the row count) summed over ranks, in place."""
+    if group is not None or (tdist.is_available() and tdist.is_initialized()):
+        if tdist.get_world_size(group) > 1:
+            tdist.all_reduce(t, group=group)
+    return t

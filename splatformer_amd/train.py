@@ -19,6 +19,7 @@ from torch import Tensor
 from . import ptv3_ops as ops
 from . import ptv3_train as pt
 from . import train_ops as tops
+from .dist import allreduce_mean_
 from .feature_predictor import ALL_FEATURES, FeaturePredictor
 from .gs_render import rasterize_gaussians_to_multiimgs
 
@@ -143,8 +144,7 @@ class Trainer:
 
     def optimizer_step(self) -> None:
         if self.group is not None and self.world > 1:
-            torch.distributed.all_reduce(self.flat_grad, group=self.group)  # DDP: average over ranks
-            self.flat_grad.div_(self.world)
+            allreduce_mean_(self.flat_grad, self.group)  # DDP: average over ranks, one bucket
         coef = None
         if self.clip > 0:
             coef, self.last_norm = tops.grad_clip_coef([self.flat_grad], self.clip)

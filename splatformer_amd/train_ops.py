@@ -139,7 +139,8 @@ def _colsum_ws(M: int, Cc: int, dev) -> Tuple[Tensor, int]:
 
 def _allreduce(t: Tensor, group) -> None:
     if group is not None:
-        torch.distributed.all_reduce(t, group=group)
+        from .dist import allreduce_sum_
+        allreduce_sum_(t, group)
 
 
 def bn_train_forward(x: Tensor, bn: torch.nn.BatchNorm1d, act: int, residual: Optional[Tensor] = None,

@@ -40,8 +40,13 @@ def _worker(rank, world, port, q):
         psnr_sum = torch.tensor(float(sum(3 * (10 + i) for i in mine)), dtype=torch.float64)
         out = dist.reduce_metrics({"psnr": psnr_sum}, 3 * len(mine), len(mine))
         t = dist.max_over_ranks(1.5 + r)
+        # DDP bucket average and SyncBN sums
+        flat = torch.arange(6, dtype=torch.float32) * (r + 1)
+        dist.allreduce_mean_(flat)
+        sums = torch.tensor([1.0 + r, 10.0 * r, float(100 + r)], dtype=torch.float64)
+        dist.allreduce_sum_(sums)
         dist.barrier()
-        q.put((r, mine, out, t))
+        q.put((r, mine, out, t, flat.tolist(), sums.tolist()))
     finally:
         if torch.distributed.is_initialized():
             torch.distributed.destroy_process_group()
@@ -58,7 +63,9 @@ def test_two_rank_reduce_and_timing():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    (r0, m0, o0, t0), (r1, m1, o1, t1) = res
+    (r0, m0, o0, t0, f0, s0), (r1, m1, o1, t1, f1, s1) = res
+    assert f0 == f1 == [1.5 * i for i in range(6)]
+    assert s0 == s1 == [3.0, 10.0, 201.0]
     assert m0 + m1 == list(range(7))
     assert o1 == {}
     assert o0["num_images"] == 21 and o0["num_scenes"] == 7
