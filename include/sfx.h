@@ -248,6 +248,25 @@ int sfx_gs_pack(int n, const float* means, long long ld_means, const float* scal
 /* Pointcept offset2batch */
 int sfx_offsets_to_batch(int n, int B, const long long* offsets, int* batch, void* stream);
 
+/* ---- batched views: the eval path of gs_utils.rasterize_gaussians_to_multiimgs (gs_utils.py:20-27) ------
+ * V cameras with shared intrinsics: records laid out [V, n, ...]; intersections of all views sorted once
+ * with tile ids offset by view * tiles; rasterizer grid (tiles_x, tiles_y, V); clamp_max1 = gs_utils.py:111. */
+int sfx_render_prep_project_views(int n, int views, int num_bases, const float* means, long long ld_means,
+                                  const float* log_scales, long long ld_scales, const float* quats_raw,
+                                  long long ld_quats, const float* opac_logit, long long ld_opac,
+                                  const float* features_dc, long long ld_dc, const float* features_rest,
+                                  long long ld_rest, const float* camera_to_worlds, float fx, float fy, float cx,
+                                  float cy, int img_h, int img_w, int block_width, float* rgbs, float* opacities,
+                                  float* xys, float* depths, int* radii, float* conics, int* num_tiles_hit,
+                                  void* stream);
+int sfx_isect_emit_views(int n_total, int n_per_view, const float* xys, const float* depths, const int* radii,
+                         const int* cum_tiles_hit, int tiles_x, int tiles_y, int block_width, int64_t* isect_ids,
+                         int32_t* gaussian_ids, void* stream);
+int sfx_rasterize_fwd_views(int views, int tiles_x, int tiles_y, int block_width, int img_h, int img_w,
+                            const int32_t* gids_sorted, const int* tile_bins, const float* xys, const float* conics,
+                            const float* colors, const float* opacity, const float* background, int clamp_max1,
+                            float* final_Ts, int* final_idx, float* out_img, float* out_alpha, void* stream);
+
 /* ---- evaluation post-processing ------------------------------------------------------------------
  * Replaces train.py:104-113 `(x*255).to(torch.uint8)` of prediction (after the gs_utils.py:111
  * clamp(max=1), applied when clamp_pred != 0) and ground truth, feeding utils/metrics.py:89-91 psnr.

@@ -443,7 +443,11 @@ __global__ void __launch_bounds__(THREADS, 2) gemm_kernel(GemmArgs p, int tiles_
     }
   };
 
-  int t = blockIdx.x;
+  // XCD-aware numbering: workgroups are dealt round-robin to the 8 XCDs (blockIdx % 8), so give each XCD
+  // a contiguous range of logical ids -- consecutive tiles (same A row-block, tn fastest) then run on one
+  // XCD and share its L2 instead of being fetched once per XCD.
+  const int nwg = (int)gridDim.x;
+  int t = (nwg % 8 == 0) ? (int)(blockIdx.x % 8) * (nwg / 8) + (int)(blockIdx.x / 8) : (int)blockIdx.x;
   if (t >= total_tiles) return;
   constexpr bool per_tile_rows = MODE == MODE_GATHER1 || MODE == MODE_PAIR;
   Tile ti = tile_info(t);
@@ -527,7 +531,8 @@ void launch(GemmArgs a, int groups, bool vec, hipStream_t st) {
   // number of tiles (+-1)
   const int slots = 2 * num_cus() / groups > 0 ? 2 * num_cus() / groups : 1;
   const int per = (total + slots - 1) / slots;
-  const int grid_x = total > 0 ? (total + per - 1) / per : 1;
+  int grid_x = total > 0 ? (total + per - 1) / per : 1;
+  if (grid_x >= 8) grid_x = (grid_x + 7) / 8 * 8;  // whole XCD groups for the XCD-aware numbering
   dim3 grid(grid_x, 1, groups);
   if (vec)
     gemm_kernel<BM, BN, WGM, true, MODE><<<grid, THREADS, 0, st>>>(a, tiles_n, total);

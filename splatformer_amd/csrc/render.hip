@@ -299,6 +299,14 @@ __global__ void render_prep_project_kernel(int n, int num_bases, const float* __
                                            float* __restrict__ depths, int* __restrict__ radii,
                                            float* __restrict__ conics, int* __restrict__ num_tiles_hit) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  // batched views: blockIdx.y = view, cameras [V,4,4], every output offset by view * n records
+  const int view = blockIdx.y;
+  if (view > 0) {
+    const long long o = (long long)view * n;
+    c2w += 16 * view;
+    rgbs += 3 * o; opac += o; xys += 2 * o; depths += o; radii += o; conics += 3 * o; num_tiles_hit += o;
+    viewmat_out = nullptr;
+  }
   // camera: R = c2w[:3,:3] diag(1,-1,-1); viewmat = [R^T | -R^T t]
   float R[3][3], t[3];
 #pragma unroll
@@ -549,10 +557,11 @@ __global__ void project_bwd_kernel(int n, const float* __restrict__ means, const
 }
 
 // ---- intersections ----------------------------------------------------------
+// n_per_view > 0: records are V views x n_per_view Gaussians; view v's tiles are numbered v*tiles_x*tiles_y + ...
 __global__ void isect_emit_kernel(int n, const float* __restrict__ xys, const float* __restrict__ depths,
                                   const int* __restrict__ radii, const int* __restrict__ cum_tiles_hit,
                                   int tiles_x, int tiles_y, int bw, int64_t* __restrict__ isect_ids,
-                                  int32_t* __restrict__ gaussian_ids) {
+                                  int32_t* __restrict__ gaussian_ids, int n_per_view) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   if (radii[i] <= 0) return;
@@ -560,9 +569,10 @@ __global__ void isect_emit_kernel(int n, const float* __restrict__ xys, const fl
   get_tile_bbox(xys[2 * i], xys[2 * i + 1], (float)radii[i], tiles_x, tiles_y, bw, x0, y0, x1, y1);
   int cur = (i == 0) ? 0 : cum_tiles_hit[i - 1];
   const int64_t depth_id = (int64_t)__float_as_int(depths[i]);
+  const int64_t tile_base = n_per_view > 0 ? (int64_t)(i / n_per_view) * tiles_x * tiles_y : 0;
   for (int ty = y0; ty < y1; ++ty)
     for (int tx = x0; tx < x1; ++tx) {
-      const int64_t tile_id = (int64_t)ty * tiles_x + tx;
+      const int64_t tile_id = tile_base + (int64_t)ty * tiles_x + tx;
       isect_ids[cur] = (tile_id << 32) | (depth_id & 0xffffffffll);
       gaussian_ids[cur] = i;
       ++cur;
@@ -592,13 +602,20 @@ rasterize_fwd_kernel(int tiles_x, int tiles_y, int bw, int img_h, int img_w,
                      const float* __restrict__ xys, const float* __restrict__ conics,
                      const float* __restrict__ colors, const float* __restrict__ opacity,
                      const float* __restrict__ background, float* __restrict__ final_Ts,
-                     int* __restrict__ final_idx, float* __restrict__ out_img, float* __restrict__ out_alpha) {
+                     int* __restrict__ final_idx, float* __restrict__ out_img, float* __restrict__ out_alpha,
+                     int clamp_max1) {
   __shared__ int id_batch[MAX_BLOCK];
   __shared__ float4 xyo_batch[MAX_BLOCK];   // x, y, opacity, pad
   __shared__ float4 conic_batch[MAX_BLOCK]; // a, b, c, pad
   __shared__ float4 rgb_batch[MAX_BLOCK];
 
-  const int tile_id = blockIdx.y * tiles_x + blockIdx.x;
+  // batched views: blockIdx.z = view (tiles numbered per view, per-view image planes)
+  const int tile_id = blockIdx.z * tiles_x * tiles_y + blockIdx.y * tiles_x + blockIdx.x;
+  if (blockIdx.z > 0) {
+    const long long po = (long long)blockIdx.z * img_h * img_w;
+    final_Ts += po; final_idx += po; out_img += 3 * po;
+    if (out_alpha) out_alpha += po;
+  }
   const int tr = threadIdx.x;  // flat thread rank, row-major over (ty, tx)
   const int ty = tr / bw, tx = tr - (tr / bw) * bw;
   const int block_size = bw * bw;
@@ -653,9 +670,13 @@ rasterize_fwd_kernel(int tiles_x, int tiles_y, int bw, int img_h, int img_w,
     const int pix = pi * img_w + pj;
     final_Ts[pix] = T;
     final_idx[pix] = cur_idx;
-    out_img[3 * pix + 0] = r0 + T * background[0];
-    out_img[3 * pix + 1] = r1 + T * background[1];
-    out_img[3 * pix + 2] = r2 + T * background[2];
+    float o0 = r0 + T * background[0], o1 = r1 + T * background[1], o2 = r2 + T * background[2];
+    if (clamp_max1) {  // gs_utils.py:111 torch.clamp(rgb, max=1), fused for the eval path
+      o0 = fminf(o0, 1.f); o1 = fminf(o1, 1.f); o2 = fminf(o2, 1.f);
+    }
+    out_img[3 * pix + 0] = o0;
+    out_img[3 * pix + 1] = o1;
+    out_img[3 * pix + 2] = o2;
     if (out_alpha) out_alpha[pix] = 1.f - T;
   }
 }
@@ -883,7 +904,7 @@ int sfx_isect_emit(int n, const float* xys, const float* depths, const int* radi
   if (n == 0) return SFX_OK;
   SFX_REQUIRE(xys && depths && radii && cum_tiles_hit && isect_ids && gaussian_ids, "sfx_isect_emit: null buffer");
   isect_emit_kernel<<<sfx::ceil_div(n, 256), 256, 0, sfx::as_stream(stream)>>>(
-      n, xys, depths, radii, cum_tiles_hit, tiles_x, tiles_y, block_width, isect_ids, gaussian_ids);
+      n, xys, depths, radii, cum_tiles_hit, tiles_x, tiles_y, block_width, isect_ids, gaussian_ids, 0);
   return sfx::check_launch("sfx_isect_emit");
 }
 
@@ -911,7 +932,7 @@ int sfx_rasterize_fwd(int tiles_x, int tiles_y, int block_width, int img_h, int 
   dim3 grid(tiles_x, tiles_y);
   rasterize_fwd_kernel<<<grid, block_width * block_width, 0, sfx::as_stream(stream)>>>(
       tiles_x, tiles_y, block_width, img_h, img_w, gids_sorted, tile_bins, xys, conics, colors, opacity, background,
-      final_Ts, final_idx, out_img, out_alpha);
+      final_Ts, final_idx, out_img, out_alpha, 0);
   return sfx::check_launch("sfx_rasterize_fwd");
 }
 
@@ -931,6 +952,66 @@ int sfx_rasterize_bwd(int tiles_x, int tiles_y, int block_width, int img_h, int 
       tiles_x, tiles_y, block_width, img_h, img_w, gids_sorted, tile_bins, xys, conics, colors, opacity, background,
       final_Ts, final_idx, v_out, v_out_alpha, v_xy, v_xy_abs, v_conic, v_rgb, v_opacity);
   return sfx::check_launch("sfx_rasterize_bwd");
+}
+
+// ---- batched views (eval path of rasterize_gaussians_to_multiimgs) --------------------------------------
+// All V cameras share the intrinsics / image size (the reference's cameras dict); per-view records are laid
+// out view-major ([V, n, ...]); intersections of all views are sorted once (tile ids offset by view * T).
+int sfx_render_prep_project_views(int n, int views, int num_bases, const float* means, long long ld_means,
+                                  const float* log_scales, long long ld_scales, const float* quats_raw,
+                                  long long ld_quats, const float* opac_logit, long long ld_opac,
+                                  const float* features_dc, long long ld_dc, const float* features_rest,
+                                  long long ld_rest, const float* camera_to_worlds, float fx, float fy, float cx,
+                                  float cy, int img_h, int img_w, int block_width, float* rgbs, float* opacities,
+                                  float* xys, float* depths, int* radii, float* conics, int* num_tiles_hit,
+                                  void* stream) {
+  SFX_REQUIRE(n >= 0 && views >= 1 && views <= 65535, "sfx_render_prep_project_views: bad sizes");
+  SFX_REQUIRE((long long)n * views < (1ll << 31), "sfx_render_prep_project_views: views * n must fit int32");
+  SFX_REQUIRE(num_bases == 1 || num_bases == 4 || num_bases == 9 || num_bases == 16 || num_bases == 25,
+              "sfx_render_prep_project_views: num_bases must be a square in {1,4,9,16,25}");
+  SFX_REQUIRE(block_width > 1 && block_width <= 16, "sfx_render_prep_project_views: block_width must be in (1,16]");
+  SFX_REQUIRE(img_h > 0 && img_w > 0, "sfx_render_prep_project_views: empty image");
+  SFX_REQUIRE(camera_to_worlds, "sfx_render_prep_project_views: null cameras");
+  if (n == 0) return SFX_OK;
+  SFX_REQUIRE(means && log_scales && quats_raw && opac_logit && features_dc && (num_bases == 1 || features_rest) &&
+                  rgbs && opacities && xys && depths && radii && conics && num_tiles_hit,
+              "sfx_render_prep_project_views: null buffer");
+  dim3 grid(sfx::ceil_div(n, 256), views);
+  render_prep_project_kernel<<<grid, 256, 0, sfx::as_stream(stream)>>>(
+      n, num_bases, means, log_scales, quats_raw, opac_logit, features_dc, features_rest,
+      PrepStrides{ld_means, ld_scales, ld_quats, ld_opac, ld_dc, ld_rest}, camera_to_worlds, fx, fy, cx, cy, img_h,
+      img_w, block_width, nullptr, rgbs, opacities, xys, depths, radii, conics, num_tiles_hit);
+  return sfx::check_launch("sfx_render_prep_project_views");
+}
+
+int sfx_isect_emit_views(int n_total, int n_per_view, const float* xys, const float* depths, const int* radii,
+                         const int* cum_tiles_hit, int tiles_x, int tiles_y, int block_width, int64_t* isect_ids,
+                         int32_t* gaussian_ids, void* stream) {
+  SFX_REQUIRE(n_total >= 0 && n_per_view > 0 && n_total % n_per_view == 0, "sfx_isect_emit_views: bad sizes");
+  SFX_REQUIRE(block_width > 1 && block_width <= 16, "sfx_isect_emit_views: block_width must be in (1,16]");
+  if (n_total == 0) return SFX_OK;
+  SFX_REQUIRE(xys && depths && radii && cum_tiles_hit && isect_ids && gaussian_ids,
+              "sfx_isect_emit_views: null buffer");
+  isect_emit_kernel<<<sfx::ceil_div(n_total, 256), 256, 0, sfx::as_stream(stream)>>>(
+      n_total, xys, depths, radii, cum_tiles_hit, tiles_x, tiles_y, block_width, isect_ids, gaussian_ids, n_per_view);
+  return sfx::check_launch("sfx_isect_emit_views");
+}
+
+int sfx_rasterize_fwd_views(int views, int tiles_x, int tiles_y, int block_width, int img_h, int img_w,
+                            const int32_t* gids_sorted, const int* tile_bins, const float* xys, const float* conics,
+                            const float* colors, const float* opacity, const float* background, int clamp_max1,
+                            float* final_Ts, int* final_idx, float* out_img, float* out_alpha, void* stream) {
+  SFX_REQUIRE(views >= 1 && views <= 65535, "sfx_rasterize_fwd_views: bad view count");
+  SFX_REQUIRE(block_width > 1 && block_width <= 16, "sfx_rasterize_fwd_views: block_width must be in (1,16]");
+  SFX_REQUIRE(tiles_x == (img_w + block_width - 1) / block_width && tiles_y == (img_h + block_width - 1) / block_width,
+              "sfx_rasterize_fwd_views: tile bounds do not match the image size");
+  SFX_REQUIRE(tile_bins && xys && conics && colors && opacity && background && final_Ts && final_idx && out_img,
+              "sfx_rasterize_fwd_views: null buffer");
+  dim3 grid(tiles_x, tiles_y, views);
+  rasterize_fwd_kernel<<<grid, block_width * block_width, 0, sfx::as_stream(stream)>>>(
+      tiles_x, tiles_y, block_width, img_h, img_w, gids_sorted, tile_bins, xys, conics, colors, opacity, background,
+      final_Ts, final_idx, out_img, out_alpha, clamp_max1);
+  return sfx::check_launch("sfx_rasterize_fwd_views");
 }
 
 }  // extern "C"

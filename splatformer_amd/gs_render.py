@@ -20,7 +20,7 @@ import torch
 from torch import Tensor
 
 from . import _lib
-from ._lib import call, ptr, stream
+from ._lib import F, I, L, P, call, ptr, stream
 from .gsplat_compat import (_RasterizeGaussians, bin_and_sort_gaussians, compute_cumulative_intersects,
                             project_gaussians, rasterize_gaussians, spherical_harmonics)
 
@@ -40,8 +40,23 @@ def _scalar(x) -> float:
     return float(x.item()) if isinstance(x, Tensor) else float(x)
 
 
+_lib.register("sfx_render_prep_project_views", [I, I, I, P, L, P, L, P, L, P, L, P, L, P, L, P, F, F, F, F, I, I, I,
+                                                 P, P, P, P, P, P, P, P])
+_lib.register("sfx_isect_emit_views", [I, I, P, P, P, P, I, I, I, P, P, P])
+_lib.register("sfx_rasterize_fwd_views", [I, I, I, I, I, I, P, P, P, P, P, P, P, I, P, P, P, P, P])
+
+
 def rasterize_gaussians_to_multiimgs(gs_params: Dict[str, Tensor], cameras: Dict) -> Tuple[List[Tensor], List[Tensor]]:
-    """gs_utils.py:20-27: render every camera_to_world of `cameras` sequentially."""
+    """gs_utils.py:20-27: render every camera_to_world of `cameras`.
+
+    Eval (no autograd): all views in one batched pass -- one fused prep/project launch for V cameras, one
+    scan, one stable radix sort of every view's (view, tile, depth) keys, one rasterizer launch over
+    V x tiles -- per-view results identical to rendering the views one by one.  Training: per view through
+    the autograd glue, as the reference."""
+    gp = {k: v.float() if v.dtype == torch.half else v for k, v in gs_params.items()}
+    c2ws = cameras["camera_to_worlds"]
+    if len(c2ws) > 1 and not _needs_grad(gp) and "opacities_sigmoid" not in gp and "opacities" in gp:
+        return _render_fused_views(gp, c2ws, cameras)
     rgbs, alphas = [], []
     for camera_to_world in cameras["camera_to_worlds"]:
         rgb, alpha = rasterize_gaussians_to_singleimg(gs_params, camera_to_world, **cameras)
@@ -107,6 +122,65 @@ def _render_fused(gs, c2w, cx, cy, fx, fy, W, H, background):
     rgb, alpha = _RasterizeGaussians.apply(xys, depths, radii, conics, tiles, rgbs, opac, H, W, BLOCK_WIDTH, bg, True)
     rgb = torch.clamp(rgb, max=1.0)
     return rgb, alpha.unsqueeze(-1)
+
+
+def _render_fused_views(gs, c2ws, cameras):
+    means = gs["means"]
+    _lib.require_gpu(means)
+    dev = means.device
+    n = means.shape[0]
+    V = int(c2ws.shape[0])
+    H, W = int(_scalar(cameras["height"])), int(_scalar(cameras["width"]))
+    fx, fy, cx, cy = (_scalar(cameras[k]) for k in ("fx", "fy", "cx", "cy"))
+    bg = cameras["background_color"].to(device=dev, dtype=torch.float32).contiguous()
+    rest = gs.get("features_rest")
+    nb = 1 + (rest.shape[1] if rest is not None else 0)
+    keep = []
+    pm, lm, t = _rowptr(means, 3); keep.append(t)
+    ps, ls, t = _rowptr(gs["scales"], 3); keep.append(t)
+    pq, lq, t = _rowptr(gs["quats"], 4); keep.append(t)
+    po, lo, t = _rowptr(gs["opacities"], 1); keep.append(t)
+    pd, ldc, t = _rowptr(gs["features_dc"], 3); keep.append(t)
+    pr, lr = None, 0
+    if rest is not None:
+        pr, lr, t = _rowptr(rest, 3 * (nb - 1)); keep.append(t)
+    cams = c2ws.detach().to(device=dev, dtype=torch.float32).contiguous()
+    f = lambda *s, dt=torch.float32: torch.empty(*s, device=dev, dtype=dt)
+    rgbs, opac, xys, depths = f(V, n, 3), f(V, n), f(V, n, 2), f(V, n)
+    radii, conics, tiles = f(V, n, dt=torch.int32), f(V, n, 3), f(V * n, dt=torch.int32)
+    call("sfx_render_prep_project_views", n, V, nb, pm, lm, ps, ls, pq, lq, po, lo, pd, ldc, pr, lr, ptr(cams), fx, fy,
+         cx, cy, H, W, BLOCK_WIDTH, ptr(rgbs), ptr(opac), ptr(xys), ptr(depths), ptr(radii), ptr(conics), ptr(tiles),
+         stream())
+    total, cum = compute_cumulative_intersects(tiles)
+    # per-view intersection counts (gsplat's empty-image branch is per call: alpha = 1 there)
+    ends = cum.view(V, n)[:, -1].tolist() if n else [0] * V
+    per_view = [ends[0]] + [ends[v] - ends[v - 1] for v in range(1, V)]
+    bw = BLOCK_WIDTH
+    tiles_x, tiles_y = (W + bw - 1) // bw, (H + bw - 1) // bw
+    T = tiles_x * tiles_y
+    out = f(V, H, W, 3)
+    alpha = f(V, H, W)
+    if total > 0:
+        isect = f(total, dt=torch.int64)
+        gids = f(total, dt=torch.int32)
+        call("sfx_isect_emit_views", V * n, n, ptr(xys), ptr(depths), ptr(radii), ptr(cum), tiles_x, tiles_y, bw,
+             ptr(isect), ptr(gids), stream())
+        isect_s, gids_s = torch.empty_like(isect), torch.empty_like(gids)
+        key_bits = 32 + max(1, int(V * T - 1).bit_length())
+        ws = _lib.workspace(_lib.fn("sfx_sort_workspace_bytes")(total), dev)
+        call("sfx_sort_pairs_u64", total, ptr(isect), ptr(gids), ptr(isect_s), ptr(gids_s), 0, key_bits, ptr(ws),
+             ws.numel(), stream())
+        del isect, gids
+        bins = f(V * T, 2, dt=torch.int32)
+        call("sfx_tile_bins", total, ptr(isect_s), V * T, ptr(bins), stream())
+        final_Ts, final_idx = f(V, H, W), f(V, H, W, dt=torch.int32)
+        call("sfx_rasterize_fwd_views", V, tiles_x, tiles_y, bw, H, W, ptr(gids_s), ptr(bins), ptr(xys), ptr(conics),
+             ptr(rgbs), ptr(opac), ptr(bg), 1, ptr(final_Ts), ptr(final_idx), ptr(out), ptr(alpha), stream())
+    for v in range(V):
+        if per_view[v] < 1:
+            out[v] = torch.clamp(bg, max=1.0).expand(H, W, 3)
+            alpha[v] = 1.0
+    return list(out.unbind(0)), list(alpha.unsqueeze(-1).unbind(0))
 
 
 def _render_autograd(gs_params, camera_to_world, cx, cy, fx, fy, W, H, background_color):

@@ -33,6 +33,7 @@ def test_python_signatures_cover_header():
     import splatformer_amd.ptv3_ops  # noqa: F401  (registers the PTv3 entry points)
     import splatformer_amd.train_ops  # noqa: F401  (training entry points)
     import splatformer_amd.metrics  # noqa: F401  (evaluation entry points)
+    import splatformer_amd.gs_render  # noqa: F401  (batched-view render entry points)
     missing = [s for s in declared_symbols() if s not in _lib.SIGNATURES]
     assert not missing, f"no ctypes signature for: {missing}"
 
