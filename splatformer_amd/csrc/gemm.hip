@@ -78,6 +78,10 @@ struct GemmArgs {
   const float* dact_pre;
   long long ld_dact;
   int dact;
+  // Stream-K: the tiles x K-slabs iteration space is split evenly over the workgroups; a tile cut by a range
+  // boundary gets partial sums (atomic add into a zero-filled output; the k-slab-0 owner adds the linear
+  // epilogue terms).  Only for linear epilogues (no activation, no pre-residual copy, no in-place residual).
+  int sk;
 };
 
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
@@ -322,7 +326,7 @@ __global__ void __launch_bounds__(THREADS, 2) gemm_kernel(GemmArgs p, int tiles_
 
   // epilogue: branch-free buffer stores (row -1 / out-of-range column -> dropped); the runtime epilogue
   // options are tested once per 16-element column strip, never per element.
-  auto epilogue = [&](const Tile& ti) {
+  auto epilogue = [&](const Tile& ti, bool partial, bool owner0) {
     resolve_rows(ti);
     if constexpr (MODE == MODE_PAIR) {  // partial sums of one neighbour offset: accumulate into the output rows
 #pragma unroll
@@ -348,8 +352,14 @@ __global__ void __launch_bounds__(THREADS, 2) gemm_kernel(GemmArgs p, int tiles_
         const bool nok = n < p.N;
         const bool do_act = n < p.act_ncols;
         float v[16];
+        if (partial) {  // Stream-K piece: linear epilogue split -- only the k-slab-0 owner adds bias/shift
+          const float c0 = owner0 ? ebias[b] * escale[b] + eshift[b] : 0.f;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) v[r] = (acc[a][b][r] + ebias[b]) * escale[b] + eshift[b];
+          for (int r = 0; r < 16; ++r) v[r] = acc[a][b][r] * escale[b] + c0;
+        } else {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) v[r] = (acc[a][b][r] + ebias[b]) * escale[b] + eshift[b];
+        }
         if (p.Ypre && p.pre_before_act) {
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
@@ -394,7 +404,7 @@ __global__ void __launch_bounds__(THREADS, 2) gemm_kernel(GemmArgs p, int tiles_
             bstore1(rP, (nok && m >= 0) ? ((unsigned)m * ldp32 + (unsigned)n) * 4u : OOB, v[r]);
           }
         }
-        if (p.R) {
+        if (p.R && owner0) {
           float rv[16];
           const __amdgpu_buffer_rsrc_t rI = rsrc(p.ridx ? (const void*)p.ridx : (const void*)p.W);
           int rr[16];
@@ -412,10 +422,19 @@ __global__ void __launch_bounds__(THREADS, 2) gemm_kernel(GemmArgs p, int tiles_
 #pragma unroll
           for (int r = 0; r < 16; ++r) v[r] += rv[r];
         }
+        if (partial) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int m = mrow[a][r];
-          bstore1(rY, (nok && m >= 0) ? ((unsigned)m * ldy32 + (unsigned)n) * 4u : OOB, v[r]);
+          for (int r = 0; r < 16; ++r) {
+            const int m = mrow[a][r];
+            __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(
+                v[r], rY, (nok && m >= 0) ? ((unsigned)m * ldy32 + (unsigned)n) * 4u : OOB, 0, 0);
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int m = mrow[a][r];
+            bstore1(rY, (nok && m >= 0) ? ((unsigned)m * ldy32 + (unsigned)n) * 4u : OOB, v[r]);
+          }
         }
       }
     }
@@ -447,23 +466,46 @@ __global__ void __launch_bounds__(THREADS, 2) gemm_kernel(GemmArgs p, int tiles_
   // a contiguous range of logical ids -- consecutive tiles (same A row-block, tn fastest) then run on one
   // XCD and share its L2 instead of being fetched once per XCD.
   const int nwg = (int)gridDim.x;
-  int t = (nwg % 8 == 0) ? (int)(blockIdx.x % 8) * (nwg / 8) + (int)(blockIdx.x / 8) : (int)blockIdx.x;
-  if (t >= total_tiles) return;
+  const int lid = (nwg % 8 == 0) ? (int)(blockIdx.x % 8) * (nwg / 8) + (int)(blockIdx.x / 8) : (int)blockIdx.x;
+  // current segment: tile t, K-slabs [kb, ke).  Persistent: whole tiles lid, lid + nwg, ...;  Stream-K: the
+  // contiguous iteration range [it_begin, it_end) of tiles x slabs.
+  int t, kb = 0, ke = nk;
+  long long it_end = 0;
+  if (p.sk) {
+    const long long total_it = (long long)total_tiles * nk;
+    const long long it0 = total_it * lid / nwg;
+    it_end = total_it * (lid + 1) / nwg;
+    if (it0 >= it_end) return;
+    t = (int)(it0 / nk);
+    kb = (int)(it0 - (long long)t * nk);
+    ke = (int)min((long long)nk, kb + (it_end - it0));
+  } else {
+    t = lid;
+    if (t >= total_tiles) return;
+  }
   constexpr bool per_tile_rows = MODE == MODE_GATHER1 || MODE == MODE_PAIR;
   Tile ti = tile_info(t);
-  load_rows(ti, 0, grow);
-  load_tiles(ti, 0);
+  load_rows(ti, kb, grow);
+  load_tiles(ti, kb);
   store_tiles(0);
   __syncthreads();
   int buf = 0;
   while (true) {
-    const int nt = t + (int)gridDim.x;
-    const bool has_next = nt < total_tiles;
+    int nt, nke = nk;
+    bool has_next;
+    if (p.sk) {
+      nt = t + 1;
+      has_next = (long long)nt * nk < it_end;
+      if (has_next) nke = (int)min((long long)nk, it_end - (long long)nt * nk);
+    } else {
+      nt = t + nwg;
+      has_next = nt < total_tiles;
+    }
     const Tile tn = has_next ? tile_info(nt) : ti;
     int grow_next[A_ITERS];
     if constexpr (per_tile_rows) load_rows(tn, 0, grow_next);  // next tile's gather rows, a whole tile ahead
     zero_acc();
-    for (int kt = 0; kt + 1 < nk; ++kt) {
+    for (int kt = kb; kt + 1 < ke; ++kt) {
       if constexpr (MODE == MODE_GATHERS) load_rows(ti, kt + 1, grow);
       load_tiles(ti, kt + 1);
       __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of the MFMAs it overlaps
@@ -472,8 +514,8 @@ __global__ void __launch_bounds__(THREADS, 2) gemm_kernel(GemmArgs p, int tiles_
       __syncthreads();
       buf ^= 1;
     }
-    // last slab of tile t: its epilogue operands, then the first slab of tile t+1 in flight while the
-    // last MFMAs and the epilogue run
+    // last slab of the segment: its epilogue operands, then the first slab of the next segment in flight
+    // while the last MFMAs and the epilogue run
     pre_epilogue(ti);
     if (has_next) {
       if constexpr (per_tile_rows) {
@@ -486,13 +528,15 @@ __global__ void __launch_bounds__(THREADS, 2) gemm_kernel(GemmArgs p, int tiles_
     }
     __builtin_amdgcn_sched_barrier(0);
     compute(buf);
-    epilogue(ti);
+    epilogue(ti, kb != 0 || ke != nk, kb == 0);
     if (!has_next) break;
     store_tiles(buf ^ 1);
     __syncthreads();
     buf ^= 1;
     t = nt;
     ti = tn;
+    kb = 0;
+    ke = nke;
   }
 }
 
@@ -530,9 +574,19 @@ void launch(GemmArgs a, int groups, bool vec, hipStream_t st) {
   // persistent grid: 2 workgroups per CU (LDS/VGPR bound), balanced so every workgroup gets the same
   // number of tiles (+-1)
   const int slots = 2 * num_cus() / groups > 0 ? 2 * num_cus() / groups : 1;
-  const int per = (total + slots - 1) / slots;
-  int grid_x = total > 0 ? (total + per - 1) / per : 1;
-  if (grid_x >= 8) grid_x = (grid_x + 7) / 8 * 8;  // whole XCD groups for the XCD-aware numbering
+  int grid_x;
+  if (a.sk) {
+    const long long iters = (long long)total * sfx::ceil_div(a.K, BK);
+    grid_x = (int)(iters < slots ? iters : slots);
+    if (grid_x >= 8) grid_x = grid_x / 8 * 8;
+    if (grid_x < 1) grid_x = 1;
+    if (!a.pair_mode)  // partial tiles accumulate atomically: zero the N output columns first
+      (void)hipMemset2DAsync(a.Y, (size_t)a.ldy * 4, 0, (size_t)a.N * 4, (size_t)a.M, st);
+  } else {
+    const int per = (total + slots - 1) / slots;
+    grid_x = total > 0 ? (total + per - 1) / per : 1;
+    if (grid_x >= 8) grid_x = (grid_x + 7) / 8 * 8;  // whole XCD groups for the XCD-aware numbering
+  }
   dim3 grid(grid_x, 1, groups);
   if (vec)
     gemm_kernel<BM, BN, WGM, true, MODE><<<grid, THREADS, 0, st>>>(a, tiles_n, total);
@@ -550,31 +604,54 @@ struct TileCfg {
 constexpr TileCfg kCfgs[] = {{128, 128, 1.0f}, {128, 96, 0.95f}, {128, 64, 0.8f}, {64, 128, 0.95f}, {64, 64, 0.8f}};  // eff fitted to tools/gemm_calls.py sweeps
 constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
 
-int pick_cfg(GemmArgs a, int groups) {
-  static int forced = -2;
-  if (forced == -2) {  // tuning hook: SFX_GEMM_CFG=<index into kCfgs>
+// -> configuration index; sets a.sk when the Stream-K split of the same tile shape is cheaper.
+int pick_cfg(GemmArgs& a, int groups) {
+  static int forced = -2, forced_sk = -2;
+  if (forced == -2) {  // tuning hooks: SFX_GEMM_CFG=<index into kCfgs>, SFX_GEMM_SK=0|1
     const char* e = getenv("SFX_GEMM_CFG");
     forced = (e && *e) ? atoi(e) : -1;
     if (forced >= kNumCfgs) forced = -1;
+    const char* k = getenv("SFX_GEMM_SK");
+    forced_sk = (k && *k) ? atoi(k) : -1;
   }
-  if (forced >= 0) return forced;
-  const long long slots = 2ll * num_cus();
+  const long long slots = 2ll * num_cus() / groups;
+  const int nk = (int)sfx::ceil_div(a.K, BK);
+  // Stream-K needs a linear epilogue that can be split into atomically added pieces
+  // (measured: the memset + atomic partial epilogues only pay off on long K; pair mode needs no memset)
+  const bool sk_ok = groups == 1 && nk >= (a.pair_mode ? 8 : 16) && a.act == ACT_NONE && !a.Ypre && !a.out_rows &&
+                     !(a.R && a.R == a.Y) && a.M > 0 && forced_sk != 0;
+  const double sk_overhead = a.pair_mode ? 2.5 : 4.0;  // slab-equivalents: partial epilogues (+ memset)
   int best = 0;
+  bool best_sk = false;
   double best_cost = 1e300;
   for (int c = 0; c < kNumCfgs; ++c) {
+    if (forced >= 0 && c != forced) continue;
+    const double area = (double)kCfgs[c].bm * kCfgs[c].bn / kCfgs[c].eff;
     const long long tiles = (long long)tiles_m_of(a, kCfgs[c].bm) * sfx::ceil_div(a.N, kCfgs[c].bn) * groups;
     const long long rounds = (tiles + slots - 1) / slots;
-    const double cost = (double)rounds * kCfgs[c].bm * kCfgs[c].bn / kCfgs[c].eff;
+    // cost in slab-area units: K slabs + ~1 slab-equivalent of epilogue per tile
+    double cost = (double)rounds * (nk + 1) * area;
+    bool sk = false;
+    if (sk_ok && c <= 2) {  // Stream-K on the 128-row shapes: ~1.5 extra slab-equivalents (2 partial epilogues)
+      const double sk_cost = ((double)((tiles * nk + slots - 1) / slots) + sk_overhead) * area;
+      if (sk_cost < cost || forced_sk == 1) {
+        cost = sk_cost;
+        sk = true;
+      }
+    }
     if (cost < best_cost) {
       best_cost = cost;
       best = c;
+      best_sk = sk;
     }
   }
+  a.sk = best_sk ? 1 : 0;
+  tiles_m_of(a, kCfgs[best].bm);  // pair mode: slice_tile_off for the chosen shape
   return best;
 }
 
 template <int MODE>
-void dispatch_mode(const GemmArgs& a, int groups, bool vec, hipStream_t st) {
+void dispatch_mode(GemmArgs a, int groups, bool vec, hipStream_t st) {
   switch (pick_cfg(a, groups)) {
     case 0: launch<128, 128, 2, MODE>(a, groups, vec, st); break;
     case 1: launch<128, 96, 4, MODE>(a, groups, vec, st); break;
