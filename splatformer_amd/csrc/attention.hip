@@ -32,11 +32,13 @@ template <int D>
 __global__ void __launch_bounds__(256, 2)
 window_attn_kernel(const float* __restrict__ qkv, const int* __restrict__ order, const int* __restrict__ win,
                    int Kwin, int C, float scale, float* __restrict__ out) {
-  constexpr int DP = D + 4;
+  constexpr int DP = D + 4;   // Q/K rows: conflict-free ds_read_b128 for D = 16, 24, 32
+  constexpr int DPV = 40;     // V rows padded to 32 (+8): the P.V MFMA reads V^T[dd = lane][key] with no
+                              // masking for dd >= D, and the two half-waves (keys 4 apart) hit disjoint banks
   constexpr int HALF = D / 2;  // k-values per lane half in S = K Q^T
   __shared__ __attribute__((aligned(16))) float Qs[KMAX * DP];
   __shared__ __attribute__((aligned(16))) float Ks[KMAX * DP];
-  __shared__ __attribute__((aligned(16))) float Vs[KMAX * DP];
+  __shared__ __attribute__((aligned(16))) float Vs[KMAX * DPV];
   __shared__ int rows[KMAX];
 
   const int w = blockIdx.x, head = blockIdx.y;
@@ -45,6 +47,11 @@ window_attn_kernel(const float* __restrict__ qkv, const int* __restrict__ order,
   const long long ld = 3ll * C;
 
   if (tid < KMAX) rows[tid] = tid < Kwin ? order[key_start + tid] : -1;
+  if (D < 32)  // zero the V padding columns D..31 once
+    for (int e = tid; e < KMAX * (32 - D) / 4; e += 256) {
+      const int row = e / ((32 - D) / 4), c4 = e - row * ((32 - D) / 4);
+      *reinterpret_cast<float4*>(&Vs[row * DPV + D + 4 * c4]) = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
   __syncthreads();
   // gather q/k/v rows of this head: KMAX rows x 3 mats x D/4 float4
   constexpr int CH = D / 4;
@@ -61,7 +68,7 @@ window_attn_kernel(const float* __restrict__ qkv, const int* __restrict__ order,
     } else if (mat == 1) {
       *reinterpret_cast<float4*>(&Ks[row * DP + 4 * ch]) = v;
     } else {
-      *reinterpret_cast<float4*>(&Vs[row * DP + 4 * ch]) = v;
+      *reinterpret_cast<float4*>(&Vs[row * DPV + 4 * ch]) = v;
     }
   }
   __syncthreads();
@@ -85,44 +92,49 @@ window_attn_kernel(const float* __restrict__ qkv, const int* __restrict__ order,
       s[kb] = __builtin_amdgcn_mfma_f32_32x32x2f32(kv.w, qv.w, s[kb], 0, 0, 0);
     }
   }
-  // softmax over keys (register axis + the other half-wave)
+  // softmax over keys (register axis + the other half-wave); keys >= Kwin only exist in short windows
+  if (Kwin < KMAX) {
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (key >= Kwin) s[kb][r] = -INFINITY;
+      }
+  }
   float mx = -INFINITY;
 #pragma unroll
   for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int key = kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-      if (key >= Kwin) s[kb][r] = -INFINITY;
-      mx = fmaxf(mx, s[kb][r]);
-    }
+    for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[kb][r]);
   mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
   float sum = 0.f;
 #pragma unroll
   for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const float e = expf(s[kb][r] - mx);
+      const float e = __expf(s[kb][r] - mx);
       s[kb][r] = e;
       sum += e;
     }
   sum += __shfl_xor(sum, 32, 64);
+  const float rinv = 1.f / sum;
 #pragma unroll
   for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) s[kb][r] = s[kb][r] / sum;
+    for (int r = 0; r < 16; ++r) s[kb][r] *= rinv;
 
   // O^T[dd][query] = sum_key V[key][dd] P^T[key][query]
   floatx16 o;
 #pragma unroll
   for (int r = 0; r < 16; ++r) o[r] = 0.f;
-  const bool dd_ok = l32 < D;
+  const float* vcol = &Vs[4 * h * DPV + l32];
 #pragma unroll
   for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
     for (int st = 0; st < 16; ++st) {
-      const int key = kb * 32 + (st & 3) + 8 * (st >> 2) + 4 * h;
-      const float a = dd_ok ? Vs[key * DP + l32] : 0.f;
-      o = __builtin_amdgcn_mfma_f32_32x32x2f32(a, s[kb][st], o, 0, 0, 0);
+      const int key0 = kb * 32 + (st & 3) + 8 * (st >> 2);  // + 4h folded into vcol
+      o = __builtin_amdgcn_mfma_f32_32x32x2f32(vcol[key0 * DPV], s[kb][st], o, 0, 0, 0);
     }
 
   // scatter: query 32*wid + l32 (lane column), dd rows (r&3) + 8(r>>2) + 4h
