@@ -93,6 +93,88 @@ __global__ void __launch_bounds__(256) cpe_residual_ln_kernel(int M, int C, cons
   }
 }
 
+
+// ---- vectorised variants: a row is held by G lanes (float4 each, NV float4 per lane), G | 64, so one wave
+// covers 64/G rows with 16-byte loads/stores.  C = 4 * G * NV in {64, 96, 128, 256, 512}.
+template <int G>
+__device__ __forceinline__ float group_sum(float v) {
+#pragma unroll
+  for (int o = G / 2; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <int G, int NV>
+__device__ __forceinline__ void ln_row4(float4 (&v)[NV], const float* __restrict__ g, const float* __restrict__ b,
+                                        float eps, int sub, float4 (&o)[NV]) {
+  constexpr int C = 4 * G * NV;
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+  const float mean = group_sum<G>(s) / (float)C;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const float a = v[i].x - mean, bb = v[i].y - mean, c = v[i].z - mean, d = v[i].w - mean;
+    q += (a * a + bb * bb) + (c * c + d * d);
+  }
+  const float rstd = 1.f / sqrtf(group_sum<G>(q) / (float)C + eps);
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = 4 * (sub + G * i);
+    const float4 gg = *reinterpret_cast<const float4*>(g + c);
+    const float4 bv = *reinterpret_cast<const float4*>(b + c);
+    o[i] = make_float4((v[i].x - mean) * rstd * gg.x + bv.x, (v[i].y - mean) * rstd * gg.y + bv.y,
+                       (v[i].z - mean) * rstd * gg.z + bv.z, (v[i].w - mean) * rstd * gg.w + bv.w);
+  }
+}
+
+template <int G, int NV>
+__global__ void __launch_bounds__(256) layernorm4_kernel(int M, const float* __restrict__ X, long long ldx,
+                                                         const float* __restrict__ g, const float* __restrict__ b,
+                                                         float eps, float* __restrict__ Y, long long ldy) {
+  const int row = blockIdx.x * (256 / G) + threadIdx.x / G;
+  const int sub = threadIdx.x % G;
+  if (row >= M) return;
+  float4 v[NV], o[NV];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) v[i] = *reinterpret_cast<const float4*>(X + (long long)row * ldx + 4 * (sub + G * i));
+  ln_row4<G, NV>(v, g, b, eps, sub, o);
+#pragma unroll
+  for (int i = 0; i < NV; ++i) *reinterpret_cast<float4*>(Y + (long long)row * ldy + 4 * (sub + G * i)) = o[i];
+}
+
+template <int G, int NV>
+__global__ void __launch_bounds__(256) cpe_residual_ln4_kernel(int M, const float* __restrict__ T,
+                                                               const float* __restrict__ X,
+                                                               const float* __restrict__ g_cpe,
+                                                               const float* __restrict__ b_cpe,
+                                                               const float* __restrict__ g1,
+                                                               const float* __restrict__ b1, float eps,
+                                                               float* __restrict__ Xout, float* __restrict__ H) {
+  constexpr int C = 4 * G * NV;
+  const int row = blockIdx.x * (256 / G) + threadIdx.x / G;
+  const int sub = threadIdx.x % G;
+  if (row >= M) return;
+  const long long base = (long long)row * C;
+  float4 v[NV], o[NV], x[NV];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    v[i] = *reinterpret_cast<const float4*>(T + base + 4 * (sub + G * i));
+    x[i] = *reinterpret_cast<const float4*>(X + base + 4 * (sub + G * i));
+  }
+  ln_row4<G, NV>(v, g_cpe, b_cpe, eps, sub, o);
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    v[i] = make_float4(x[i].x + o[i].x, x[i].y + o[i].y, x[i].z + o[i].z, x[i].w + o[i].w);
+    *reinterpret_cast<float4*>(Xout + base + 4 * (sub + G * i)) = v[i];
+  }
+  ln_row4<G, NV>(v, g1, b1, eps, sub, o);
+#pragma unroll
+  for (int i = 0; i < NV; ++i) *reinterpret_cast<float4*>(H + base + 4 * (sub + G * i)) = o[i];
+}
+
+inline bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
 }  // namespace
 
 extern "C" {
@@ -102,7 +184,16 @@ int sfx_layernorm(int M, int C, const float* X, long long ldx, const float* gamm
   SFX_REQUIRE(M >= 0 && C > 0 && C <= 64 * MAXV, "sfx_layernorm: C must be in [1, 512]");
   if (M == 0) return SFX_OK;
   SFX_REQUIRE(X && gamma && beta && Y, "sfx_layernorm: null buffer");
-  layernorm_kernel<<<sfx::ceil_div(M, 4), 256, 0, sfx::as_stream(stream)>>>(M, C, X, ldx, gamma, beta, eps, Y, ldy);
+  hipStream_t st = sfx::as_stream(stream);
+  const bool v4 = ldx % 4 == 0 && ldy % 4 == 0 && al16(X) && al16(Y) && al16(gamma) && al16(beta);
+#define SFX_LN4(G, NV) layernorm4_kernel<G, NV><<<sfx::ceil_div(M, 256 / G), 256, 0, st>>>(M, X, ldx, gamma, beta, eps, Y, ldy)
+  if (v4 && C == 64) SFX_LN4(16, 1);
+  else if (v4 && C == 96) SFX_LN4(8, 3);
+  else if (v4 && C == 128) SFX_LN4(32, 1);
+  else if (v4 && C == 256) SFX_LN4(64, 1);
+  else if (v4 && C == 512) SFX_LN4(64, 2);
+  else layernorm_kernel<<<sfx::ceil_div(M, 4), 256, 0, st>>>(M, C, X, ldx, gamma, beta, eps, Y, ldy);
+#undef SFX_LN4
   return sfx::check_launch("sfx_layernorm");
 }
 
@@ -111,8 +202,20 @@ int sfx_cpe_residual_ln(int M, int C, const float* T, const float* X, const floa
   SFX_REQUIRE(M >= 0 && C > 0 && C <= 64 * MAXV, "sfx_cpe_residual_ln: C must be in [1, 512]");
   if (M == 0) return SFX_OK;
   SFX_REQUIRE(T && X && gamma_cpe && beta_cpe && gamma1 && beta1 && X_out && H, "sfx_cpe_residual_ln: null buffer");
-  cpe_residual_ln_kernel<<<sfx::ceil_div(M, 4), 256, 0, sfx::as_stream(stream)>>>(M, C, T, X, gamma_cpe, beta_cpe,
-                                                                                   gamma1, beta1, eps, X_out, H);
+  hipStream_t st = sfx::as_stream(stream);
+  const bool v4 = al16(T) && al16(X) && al16(X_out) && al16(H) && al16(gamma_cpe) && al16(beta_cpe) && al16(gamma1) &&
+                  al16(beta1);
+#define SFX_CPE4(G, NV)                                                                                    \
+  cpe_residual_ln4_kernel<G, NV><<<sfx::ceil_div(M, 256 / G), 256, 0, st>>>(M, T, X, gamma_cpe, beta_cpe, gamma1, \
+                                                                            beta1, eps, X_out, H)
+  if (v4 && C == 64) SFX_CPE4(16, 1);
+  else if (v4 && C == 96) SFX_CPE4(8, 3);
+  else if (v4 && C == 128) SFX_CPE4(32, 1);
+  else if (v4 && C == 256) SFX_CPE4(64, 1);
+  else if (v4 && C == 512) SFX_CPE4(64, 2);
+  else cpe_residual_ln_kernel<<<sfx::ceil_div(M, 4), 256, 0, st>>>(M, C, T, X, gamma_cpe, beta_cpe, gamma1, beta1, eps,
+                                                                   X_out, H);
+#undef SFX_CPE4
   return sfx::check_launch("sfx_cpe_residual_ln");
 }
 
