@@ -102,13 +102,32 @@ class Block(nn.Module):
         self.drop_path = PointSequential(nn.Identity())  # DropPath has no parameters; rate in drop_prob
         self.drop_prob = 0.0
 
+    def cpe_fused(self):
+        """cpe = Linear(SubMConv3d(x)) folded into one sparse conv (exact in real arithmetic):
+        W'_k = W_lin W_k, b' = W_lin b_conv + b_lin -- the per-point linear GEMM disappears.  Computed with
+        the library GEMM, cached until one of the four tensors changes."""
+        conv, lin = self.cpe[0], self.cpe[1]
+        ts = (conv.weight, conv.bias, lin.weight, lin.bias)
+        key = tuple((t.data_ptr(), t._version) for t in ts)
+        cache = self.__dict__.get("_sfx_cpe")
+        if cache is not None and cache[0] == key:
+            return cache[1], cache[2]
+        from .train_ops import transpose
+        with torch.no_grad():
+            C = self.channels
+            wc = conv.weight.detach().reshape(C, -1)                   # [Cout, 27*Cin]
+            wf = ops.linear(lin.weight.detach(), transpose(wc))        # W_lin @ Wc   [C, 27*Cin]
+            bf = ops.linear(conv.bias.detach()[None].contiguous(), lin.weight.detach(), lin.bias.detach())[0]
+        self.__dict__["_sfx_cpe"] = (key, wf.contiguous(), bf.contiguous())
+        return wf, bf
+
     def run(self, point: Point, conv_in: Optional[Tensor] = None, out: Optional[Tensor] = None) -> Point:
         """Block.forward (calflops.py:45-82): x += LN(Lin(SubMConv(x))); x += attn(LN1 x); x += MLP(LN2 x)."""
         x = point.feat
         C = self.channels
-        conv, lin, ln_c = self.cpe[0], self.cpe[1], self.cpe[2]
-        t = ops.subm_conv(x if conv_in is None else conv_in, point.nbr, conv.weight, conv.bias)
-        t = ops.linear(t, lin.weight, lin.bias)
+        ln_c = self.cpe[2]
+        wf, bf = self.cpe_fused()
+        t = ops.subm_conv(x if conv_in is None else conv_in, point.nbr, wf, bf)
         ln1 = self.norm1[0]
         x1, h = ops.cpe_residual_ln(t, x, ln_c.weight, ln_c.bias, ln1.weight, ln1.bias, ln1.eps)
         qkv = ops.linear(h, self.attn.qkv.weight, self.attn.qkv.bias)

@@ -69,11 +69,10 @@ def block_forward(blk: Block, name: str, point: Point, masks: MaskFn, conv_in: O
                   out: Optional[Tensor] = None) -> dict:
     x = point.feat
     n, C = x.shape
-    conv, lin, ln_c = blk.cpe[0], blk.cpe[1], blk.cpe[2]
+    ln_c = blk.cpe[2]
     ln1, ln2, mlp = blk.norm1[0], blk.norm2[0], blk.mlp[0]
-    t = ops.subm_conv(x if conv_in is None else conv_in, point.nbr, conv.weight, conv.bias)
-    u = ops.linear(t, lin.weight, lin.bias)
-    del t
+    wf, bf = blk.cpe_fused()  # Linear folded into the conv (frozen in training: filter_grads(['attn.qkv']))
+    u = ops.subm_conv(x if conv_in is None else conv_in, point.nbr, wf, bf)
     x1, h = ops.cpe_residual_ln(u, x, ln_c.weight, ln_c.bias, ln1.weight, ln1.bias, ln1.eps)
     qkv = ops.linear(h, blk.attn.qkv.weight, blk.attn.qkv.bias)
     K, win, nw = point_windows(point, blk.attn.patch_size_max)
@@ -108,7 +107,7 @@ def block_backward(rec: dict, dy: Tensor, need_input: bool):
         _trace(f"{nm}.fwd.{k}", rec[k])
     _trace(f"{nm}.dy", dy)
     C = blk.channels
-    conv, lin, ln_c = blk.cpe[0], blk.cpe[1], blk.cpe[2]
+    ln_c = blk.cpe[2]
     ln1, ln2, mlp = blk.norm1[0], blk.norm2[0], blk.mlp[0]
     dm = tops.linear_bwd_data(dy, wt(mlp.fc2.weight), rowscale=rec["mm"], dact=tops.DACT_GELU, dact_pre=rec["z"])
     dh2 = tops.linear_bwd_data(dm, wt(mlp.fc1.weight))
@@ -135,9 +134,8 @@ def block_backward(rec: dict, dy: Tensor, need_input: bool):
     del dqkv
     dx1, du = tops.cpe_ln_bwd(rec["u"], rec["x1"], ln_c.weight, ln1.weight, dx2, dh, ln1.eps)
     del dh, dx2
-    dt = tops.linear_bwd_data(du, wt(lin.weight))
-    del du
-    wct = wt(conv.weight)  # [Cout, 27*Cin] -> [27*Cin, Cout]
+    dt = du
+    wct = wt(blk.cpe_fused()[0])  # fused [Cout, 27*Cin] -> [27*Cin, Cout]
     if rec["sep_conv_in"]:
         dci = torch.zeros_like(dx1)
         tops.subm_conv_bwd_data(dt, rec["smap"], wct, dci)
