@@ -163,10 +163,13 @@ window_attn_kernel(const float* __restrict__ qkv, const int* __restrict__ order,
 // float atomics into dqkv, which the caller zero-fills.  Padding queries (positions < query_start of the
 // last window) carry dO = 0 and contribute nothing, exactly as their discarded outputs in the reference.
 template <int D>
-__global__ void __launch_bounds__(256, 1)
+__global__ void __launch_bounds__(256, 2)
 window_attn_bwd_kernel(const float* __restrict__ qkv, const int* __restrict__ order, const int* __restrict__ win,
                        int Kwin, int C, float scale, const float* __restrict__ dout, float* __restrict__ dqkv) {
-  constexpr int DP = D + 4;
+  // One row stride for all four operands: 36 floats = 32 (+4) columns, zero beyond D.  ds_read_b128 row
+  // reads (S, dP) are conflict-free at stride 36 and the MFMA A-operand column reads (V^T, K^T, dO^T, Q^T
+  // with dd = lane) need no masking for dd >= D.  4 x 18 KB LDS -> 2 workgroups per CU.
+  constexpr int DP = 36;
   constexpr int HALF = D / 2;
   __shared__ __attribute__((aligned(16))) float Qs[KMAX * DP];
   __shared__ __attribute__((aligned(16))) float Ks[KMAX * DP];
@@ -182,17 +185,19 @@ window_attn_bwd_kernel(const float* __restrict__ qkv, const int* __restrict__ or
 
   if (tid < KMAX) rows[tid] = tid < Kwin ? order[key_start + tid] : -1;
   __syncthreads();
-  constexpr int CH = D / 4;
+  // gather q/k/v/dO rows of this head (zero rows past Kwin, zero dO for padding queries, zero columns >= D)
+  constexpr int CH = 8;  // float4 per padded row (32 columns)
   for (int e = tid; e < KMAX * 4 * CH; e += 256) {
     const int row = e / (4 * CH);
     const int rem = e - row * 4 * CH;
     const int mat = rem / CH, ch = rem - mat * CH;
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
     const int src = rows[row];
-    if (mat < 3) {
-      if (src >= 0) v = *reinterpret_cast<const float4*>(qkv + (long long)src * ld + mat * C + head * D + 4 * ch);
-    } else if (src >= 0 && key_start + row >= query_start) {
-      v = *reinterpret_cast<const float4*>(dout + (long long)src * C + head * D + 4 * ch);
+    if (4 * ch < D && src >= 0) {
+      if (mat < 3)
+        v = *reinterpret_cast<const float4*>(qkv + (long long)src * ld + mat * C + head * D + 4 * ch);
+      else if (key_start + row >= query_start)
+        v = *reinterpret_cast<const float4*>(dout + (long long)src * C + head * D + 4 * ch);
     }
     float* dst = mat == 0 ? Qs : mat == 1 ? Ks : mat == 2 ? Vs : dOs;
     if (mat == 0) {
@@ -203,49 +208,48 @@ window_attn_bwd_kernel(const float* __restrict__ qkv, const int* __restrict__ or
   __syncthreads();
 
   // ---------------- phase A: this wave's 32 queries on the lane columns ----------------
-  floatx16 s[4], dp[4];
+  const int qi = 32 * wid + l32;
+  floatx16 s[4];
 #pragma unroll
   for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) s[kb][r] = dp[kb][r] = 0.f;
+    for (int r = 0; r < 16; ++r) s[kb][r] = 0.f;
   {
-    const float* qrow = &Qs[(32 * wid + l32) * DP + h * HALF];
-    const float* grow = &dOs[(32 * wid + l32) * DP + h * HALF];
+    const float* qrow = &Qs[qi * DP + h * HALF];
 #pragma unroll
     for (int c = 0; c < HALF / 4; ++c) {
       const float4 qv = *reinterpret_cast<const float4*>(qrow + 4 * c);
-      const float4 gv = *reinterpret_cast<const float4*>(grow + 4 * c);
 #pragma unroll
       for (int kb = 0; kb < 4; ++kb) {
         const float4 kv = *reinterpret_cast<const float4*>(&Ks[(kb * 32 + l32) * DP + h * HALF + 4 * c]);
-        const float4 vv = *reinterpret_cast<const float4*>(&Vs[(kb * 32 + l32) * DP + h * HALF + 4 * c]);
         s[kb] = __builtin_amdgcn_mfma_f32_32x32x2f32(kv.x, qv.x, s[kb], 0, 0, 0);
         s[kb] = __builtin_amdgcn_mfma_f32_32x32x2f32(kv.y, qv.y, s[kb], 0, 0, 0);
         s[kb] = __builtin_amdgcn_mfma_f32_32x32x2f32(kv.z, qv.z, s[kb], 0, 0, 0);
         s[kb] = __builtin_amdgcn_mfma_f32_32x32x2f32(kv.w, qv.w, s[kb], 0, 0, 0);
-        dp[kb] = __builtin_amdgcn_mfma_f32_32x32x2f32(vv.x, gv.x, dp[kb], 0, 0, 0);
-        dp[kb] = __builtin_amdgcn_mfma_f32_32x32x2f32(vv.y, gv.y, dp[kb], 0, 0, 0);
-        dp[kb] = __builtin_amdgcn_mfma_f32_32x32x2f32(vv.z, gv.z, dp[kb], 0, 0, 0);
-        dp[kb] = __builtin_amdgcn_mfma_f32_32x32x2f32(vv.w, gv.w, dp[kb], 0, 0, 0);
       }
     }
+  }
+  if (Kwin < KMAX) {
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (key >= Kwin) s[kb][r] = -INFINITY;
+      }
   }
   float mx = -INFINITY;
 #pragma unroll
   for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int key = kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-      if (key >= Kwin) s[kb][r] = -INFINITY;
-      mx = fmaxf(mx, s[kb][r]);
-    }
+    for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[kb][r]);
   mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
   float sum = 0.f;
 #pragma unroll
   for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const float e = expf(s[kb][r] - mx);
+      const float e = __expf(s[kb][r] - mx);
       s[kb][r] = e;
       sum += e;
     }
@@ -254,44 +258,47 @@ window_attn_bwd_kernel(const float* __restrict__ qkv, const int* __restrict__ or
 #pragma unroll
   for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) s[kb][r] = s[kb][r] / sum;  // same rounding as the forward
-  // O^T[dd][q] (forward recompute) and Delta_q = sum_dd O[q][dd] dO[q][dd]
-  floatx16 o;
+    for (int r = 0; r < 16; ++r) s[kb][r] *= rinv;  // P^T (same normalisation as the forward)
+  // O^T[dd][q] (forward recompute) -> Delta_q = sum_dd O[q][dd] dO[q][dd]
+  floatx16 acc;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) o[r] = 0.f;
-  const bool dd_ok = l32 < D;
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  const float* vcol = &Vs[4 * h * DP + l32];
+  const float* kcol = &Ks[4 * h * DP + l32];
 #pragma unroll
   for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
-    for (int st = 0; st < 16; ++st) {
-      const int key = kb * 32 + (st & 3) + 8 * (st >> 2) + 4 * h;
-      const float a = dd_ok ? Vs[key * DP + l32] : 0.f;
-      o = __builtin_amdgcn_mfma_f32_32x32x2f32(a, s[kb][st], o, 0, 0, 0);
-    }
-  const int qi = 32 * wid + l32;
+    for (int st = 0; st < 16; ++st)
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(vcol[(kb * 32 + (st & 3) + 8 * (st >> 2)) * DP], s[kb][st], acc, 0, 0,
+                                                 0);
   float delta = 0.f;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int dd = (r & 3) + 8 * (r >> 2) + 4 * h;
-    if (dd < D) delta += o[r] * dOs[qi * DP + dd];
-  }
+  for (int r = 0; r < 16; ++r) delta += acc[r] * dOs[qi * DP + (r & 3) + 8 * (r >> 2) + 4 * h];
   delta += __shfl_xor(delta, 32, 64);
-  // dS^T = P^T (dP^T - Delta); dQ^T[dd][q] = sum_key K^T[dd][key] dS^T[key][q]
+  // per key block: dP^T = V dO^T, dS^T = P^T (dP^T - Delta), dQ^T += K^T dS^T
 #pragma unroll
-  for (int kb = 0; kb < 4; ++kb)
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;  // now dQ^T
+  const float* grow = &dOs[qi * DP + h * HALF];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) s[kb][r] = s[kb][r] * (dp[kb][r] - delta);
-  floatx16 dq;
+  for (int kb = 0; kb < 4; ++kb) {
+    floatx16 dp;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) dq[r] = 0.f;
+    for (int r = 0; r < 16; ++r) dp[r] = 0.f;
 #pragma unroll
-  for (int kb = 0; kb < 4; ++kb)
+    for (int c = 0; c < HALF / 4; ++c) {
+      const float4 gv = *reinterpret_cast<const float4*>(grow + 4 * c);
+      const float4 vv = *reinterpret_cast<const float4*>(&Vs[(kb * 32 + l32) * DP + h * HALF + 4 * c]);
+      dp = __builtin_amdgcn_mfma_f32_32x32x2f32(vv.x, gv.x, dp, 0, 0, 0);
+      dp = __builtin_amdgcn_mfma_f32_32x32x2f32(vv.y, gv.y, dp, 0, 0, 0);
+      dp = __builtin_amdgcn_mfma_f32_32x32x2f32(vv.z, gv.z, dp, 0, 0, 0);
+      dp = __builtin_amdgcn_mfma_f32_32x32x2f32(vv.w, gv.w, dp, 0, 0, 0);
+    }
 #pragma unroll
     for (int st = 0; st < 16; ++st) {
-      const int key = kb * 32 + (st & 3) + 8 * (st >> 2) + 4 * h;
-      const float a = dd_ok ? Ks[key * DP + l32] : 0.f;
-      dq = __builtin_amdgcn_mfma_f32_32x32x2f32(a, s[kb][st], dq, 0, 0, 0);
+      const float ds = s[kb][st] * (dp[st] - delta);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(kcol[(kb * 32 + (st & 3) + 8 * (st >> 2)) * DP], ds, acc, 0, 0, 0);
     }
+  }
   const int qpos = key_start + qi;
   if (qi < Kwin && qpos >= query_start) {
     float* dst = dqkv + (long long)rows[qi] * ld + head * D;
@@ -300,7 +307,7 @@ window_attn_bwd_kernel(const float* __restrict__ qkv, const int* __restrict__ or
       const int dd = 8 * g + 4 * h;
       if (dd + 3 < D)
         *reinterpret_cast<float4*>(dst + dd) =
-            make_float4(dq[4 * g + 0] * scale, dq[4 * g + 1] * scale, dq[4 * g + 2] * scale, dq[4 * g + 3] * scale);
+            make_float4(acc[4 * g + 0] * scale, acc[4 * g + 1] * scale, acc[4 * g + 2] * scale, acc[4 * g + 3] * scale);
     }
   }
   if (h == 0) {
@@ -316,19 +323,21 @@ window_attn_bwd_kernel(const float* __restrict__ qkv, const int* __restrict__ or
 #pragma unroll
   for (int r = 0; r < 16; ++r) dk[r] = dv[r] = 0.f;
   const bool key_ok = kk < Kwin;
+  const float* krow = &Ks[kk * DP + h * HALF];
+  const float* vrow = &Vs[kk * DP + h * HALF];
+  const float* gcol = &dOs[4 * h * DP + l32];
+  const float* qcol = &Qs[4 * h * DP + l32];
 #pragma unroll 1
   for (int qb = 0; qb < 4; ++qb) {
     floatx16 sb, pb;
 #pragma unroll
     for (int r = 0; r < 16; ++r) sb[r] = pb[r] = 0.f;
     const float* qrow = &Qs[(qb * 32 + l32) * DP + h * HALF];
-    const float* grow = &dOs[(qb * 32 + l32) * DP + h * HALF];
-    const float* krow = &Ks[kk * DP + h * HALF];
-    const float* vrow = &Vs[kk * DP + h * HALF];
+    const float* grw = &dOs[(qb * 32 + l32) * DP + h * HALF];
 #pragma unroll
     for (int c = 0; c < HALF / 4; ++c) {
       const float4 qv = *reinterpret_cast<const float4*>(qrow + 4 * c);
-      const float4 gv = *reinterpret_cast<const float4*>(grow + 4 * c);
+      const float4 gv = *reinterpret_cast<const float4*>(grw + 4 * c);
       const float4 kv = *reinterpret_cast<const float4*>(krow + 4 * c);
       const float4 vv = *reinterpret_cast<const float4*>(vrow + 4 * c);
       sb = __builtin_amdgcn_mfma_f32_32x32x2f32(qv.x, kv.x, sb, 0, 0, 0);
@@ -341,32 +350,44 @@ window_attn_bwd_kernel(const float* __restrict__ qkv, const int* __restrict__ or
       pb = __builtin_amdgcn_mfma_f32_32x32x2f32(gv.w, vv.w, pb, 0, 0, 0);
     }
     // sb[r] = S[q][kk], pb[r] = dP[q][kk] for q = qb*32 + (r&3) + 8(r>>2) + 4h
-    float P[16], dS[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int q = qb * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-      const float e = key_ok ? expf(sb[r] - st_max[q]) : 0.f;
-      P[r] = e * st_rinv[q];
-      dS[r] = P[r] * (pb[r] - st_delta[q]);
-    }
 #pragma unroll
     for (int st = 0; st < 16; ++st) {
       const int q = qb * 32 + (st & 3) + 8 * (st >> 2) + 4 * h;
-      const float g = dd_ok ? dOs[q * DP + l32] : 0.f;
-      const float qs = dd_ok ? Qs[q * DP + l32] : 0.f;
-      dv = __builtin_amdgcn_mfma_f32_32x32x2f32(g, P[st], dv, 0, 0, 0);
-      dk = __builtin_amdgcn_mfma_f32_32x32x2f32(qs, dS[st], dk, 0, 0, 0);
+      const float P = key_ok ? __expf(sb[st] - st_max[q]) * st_rinv[q] : 0.f;
+      const float dS = P * (pb[st] - st_delta[q]);
+      const int qo = (qb * 32 + (st & 3) + 8 * (st >> 2)) * DP;  // + 4h folded into gcol / qcol
+      dv = __builtin_amdgcn_mfma_f32_32x32x2f32(gcol[qo], P, dv, 0, 0, 0);
+      dk = __builtin_amdgcn_mfma_f32_32x32x2f32(qcol[qo], dS, dk, 0, 0, 0);
     }
   }
-  if (key_ok) {
-    float* dst = dqkv + (long long)rows[kk] * ld + head * D;
+  // dK / dV leave through LDS so that each store instruction writes whole row segments (a lane-per-key
+  // layout would touch 64 rows per instruction).  Keys in the overlap of the ragged last window with its
+  // predecessor receive contributions from both windows and are added atomically; every other key is owned
+  // by this window alone and stored plainly.
+  __syncthreads();  // all waves done reading Q/K/V/dO
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int dd = (r & 3) + 8 * (r >> 2) + 4 * h;
-      if (dd < D) {
-        atomicAdd(dst + C + dd, dk[r]);
-        atomicAdd(dst + 2 * C + dd, dv[r]);
-      }
+  for (int r = 0; r < 16; ++r) {
+    const int dd = (r & 3) + 8 * (r >> 2) + 4 * h;
+    Qs[kk * DP + dd] = dk[r];
+    Vs[kk * DP + dd] = dv[r];
+  }
+  __syncthreads();
+  const int next_ks = (w + 1 < (int)gridDim.x) ? win[2 * (w + 1)] : 0x7fffffff;
+  constexpr int DC = D / 4;
+  for (int e = tid; e < Kwin * 2 * DC; e += 256) {
+    const int row = e / (2 * DC);
+    const int rem = e - row * 2 * DC;
+    const int mat = rem / DC, ch = rem - mat * DC;
+    const float4 v = *reinterpret_cast<const float4*>(&(mat == 0 ? Qs : Vs)[row * DP + 4 * ch]);
+    float* dst = dqkv + (long long)rows[row] * ld + (mat + 1) * C + head * D + 4 * ch;
+    const int pos = key_start + row;
+    if (pos < query_start || pos >= next_ks) {
+      atomicAdd(dst + 0, v.x);
+      atomicAdd(dst + 1, v.y);
+      atomicAdd(dst + 2, v.z);
+      atomicAdd(dst + 3, v.w);
+    } else {
+      *reinterpret_cast<float4*>(dst) = v;
     }
   }
 }
