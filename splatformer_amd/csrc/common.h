@@ -47,6 +47,31 @@ __device__ __forceinline__ float wave_max(float v) {
   for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
   return v;
 }
+// Sum over the 64 lanes, result uniform (every lane): DPP butterflies inside each 16-lane row
+// (quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror, row_mirror) + the four row sums read back as scalars.
+// No LDS traffic, unlike __shfl_xor (ds_bpermute).
+__device__ __forceinline__ float dpp_add(float v, int ctrl_sel) {
+  int t;
+  switch (ctrl_sel) {
+    case 0: t = __builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false); break;   // quad [1,0,3,2]
+    case 1: t = __builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, false); break;   // quad [2,3,0,1]
+    case 2: t = __builtin_amdgcn_mov_dpp(__float_as_int(v), 0x141, 0xF, 0xF, false); break;  // row_half_mirror
+    default: t = __builtin_amdgcn_mov_dpp(__float_as_int(v), 0x140, 0xF, 0xF, false); break; // row_mirror
+  }
+  return v + __int_as_float(t);
+}
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+  v = dpp_add(v, 0);
+  v = dpp_add(v, 1);
+  v = dpp_add(v, 2);
+  v = dpp_add(v, 3);
+  const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+  const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
+  const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+  const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
+  return (r0 + r1) + (r2 + r3);
+}
+
 __device__ __forceinline__ int wave_max_i(int v) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v = max(v, __shfl_xor(v, o, 64));

@@ -778,18 +778,18 @@ rasterize_bwd_kernel(int tiles_x, int tiles_y, int bw, int img_h, int img_w,
         g_ay = fabsf(g_xy1);
         g_o = vis * v_alpha;
       }
-      g_rgb0 = sfx::wave_sum(g_rgb0);
-      g_rgb1 = sfx::wave_sum(g_rgb1);
-      g_rgb2 = sfx::wave_sum(g_rgb2);
-      g_c0 = sfx::wave_sum(g_c0);
-      g_c1 = sfx::wave_sum(g_c1);
-      g_c2 = sfx::wave_sum(g_c2);
-      g_xy0 = sfx::wave_sum(g_xy0);
-      g_xy1 = sfx::wave_sum(g_xy1);
-      g_o = sfx::wave_sum(g_o);
+      g_rgb0 = sfx::wave_sum_dpp(g_rgb0);
+      g_rgb1 = sfx::wave_sum_dpp(g_rgb1);
+      g_rgb2 = sfx::wave_sum_dpp(g_rgb2);
+      g_c0 = sfx::wave_sum_dpp(g_c0);
+      g_c1 = sfx::wave_sum_dpp(g_c1);
+      g_c2 = sfx::wave_sum_dpp(g_c2);
+      g_xy0 = sfx::wave_sum_dpp(g_xy0);
+      g_xy1 = sfx::wave_sum_dpp(g_xy1);
+      g_o = sfx::wave_sum_dpp(g_o);
       if (v_xy_abs) {
-        g_ax = sfx::wave_sum(g_ax);
-        g_ay = sfx::wave_sum(g_ay);
+        g_ax = sfx::wave_sum_dpp(g_ax);
+        g_ay = sfx::wave_sum_dpp(g_ay);
       }
       if (lane == 0) {
         const int g = id_batch[t];
