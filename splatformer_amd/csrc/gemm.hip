@@ -681,7 +681,8 @@ constexpr int WG_TILE = 64;
 
 __global__ void __launch_bounds__(THREADS) wgrad_kernel(int M, int N, int K, const float* __restrict__ dY,
                                                         long long ldy, const float* __restrict__ X, long long ldx,
-                                                        float* __restrict__ dW, long long ldw, int chunk) {
+                                                        float* __restrict__ dW, long long ldw, int chunk,
+                                                        float* __restrict__ db) {
   __shared__ __attribute__((aligned(16))) float sA[WG_TILE * LDS_STRIDE];
   __shared__ __attribute__((aligned(16))) float sB[WG_TILE * LDS_STRIDE];
   const int tiles_k = (K + WG_TILE - 1) / WG_TILE;
@@ -697,6 +698,10 @@ __global__ void __launch_bounds__(THREADS) wgrad_kernel(int M, int N, int K, con
   floatx16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  // bias gradient (db = column sums of dY) rides along in the k-tile-0 workgroups: thread tid < 64 owns
+  // column n0 + tid of the staged dY slab
+  const bool do_db = db != nullptr && k0 == 0;
+  float dbs = 0.f;
   for (int m0 = m_begin; m0 < m_end; m0 += BK) {
     const int m = m0 + lrow;
     const bool mok = m < m_end;
@@ -721,6 +726,13 @@ __global__ void __launch_bounds__(THREADS) wgrad_kernel(int M, int N, int K, con
       sB[(c + 3) * LDS_STRIDE + lrow] = xb[i].w;
     }
     __syncthreads();
+    if (do_db && tid < WG_TILE) {
+#pragma unroll
+      for (int j = 0; j < BK; j += 4) {
+        const float4 v = *reinterpret_cast<const float4*>(&sA[tid * LDS_STRIDE + j]);
+        dbs += (v.x + v.y) + (v.z + v.w);
+      }
+    }
     const float* a_lds = &sA[(wm * 32 + l32) * LDS_STRIDE + h * 16];
     const float* b_lds = &sB[(wn * 32 + l32) * LDS_STRIDE + h * 16];
 #pragma unroll
@@ -733,6 +745,7 @@ __global__ void __launch_bounds__(THREADS) wgrad_kernel(int M, int N, int K, con
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af.w, bf.w, acc, 0, 0, 0);
     }
   }
+  if (do_db && tid < WG_TILE && n0 + tid < N) atomicAdd(&db[n0 + tid], dbs);
   const __amdgpu_buffer_rsrc_t rW = rsrc(dW);
   const int k = k0 + wn * 32 + l32;
   const unsigned ldw32 = (unsigned)ldw;
@@ -742,23 +755,6 @@ __global__ void __launch_bounds__(THREADS) wgrad_kernel(int M, int N, int K, con
     __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(acc[r], rW, (n < N && k < K) ? ((unsigned)n * ldw32 + (unsigned)k) * 4u
                                                                                  : OOB, 0, 0);
   }
-}
-
-// column sums: db[N] += sum_m dY[m, n]  (one wave per 64-column strip x row chunk, atomics across chunks)
-__global__ void __launch_bounds__(256) colsum_kernel(int M, int N, const float* __restrict__ dY, long long ldy,
-                                                     float* __restrict__ db, int rows_per_block) {
-  const int n = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int part = threadIdx.x >> 6;
-  const int m0 = blockIdx.y * rows_per_block;
-  const int m1 = min(M, m0 + rows_per_block);
-  __shared__ float red[4][64];
-  float s = 0.f;
-  if (n < N)
-    for (int m = m0 + part; m < m1; m += 4) s += dY[(long long)m * ldy + n];
-  red[part][threadIdx.x & 63] = s;
-  __syncthreads();
-  if (part == 0 && n < N) atomicAdd(&db[n], red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] +
-                                                red[3][threadIdx.x]);
 }
 
 // dst[c][r] = src[r][c]
@@ -934,13 +930,8 @@ int sfx_linear_wgrad(int M, int N, int K, const float* dY, long long ldy, const 
   if (splits < 1) splits = 1;
   const int chunk = (int)sfx::ceil_div(slabs, splits) * BK;
   splits = (int)sfx::ceil_div(M, chunk);
-  wgrad_kernel<<<dim3(tiles, splits), THREADS, 0, st>>>(M, N, K, dY, ldy, X, ldx, dW, ldw, chunk);
-  int rc = sfx::check_launch("sfx_linear_wgrad");
-  if (rc || !db) return rc;
-  const int rows_per_block = 1024;
-  colsum_kernel<<<dim3(sfx::ceil_div(N, 64), sfx::ceil_div(M, rows_per_block)), 256, 0, st>>>(M, N, dY, ldy, db,
-                                                                                              rows_per_block);
-  return sfx::check_launch("sfx_linear_wgrad(bias)");
+  wgrad_kernel<<<dim3(tiles, splits), THREADS, 0, st>>>(M, N, K, dY, ldy, X, ldx, dW, ldw, chunk, db);
+  return sfx::check_launch("sfx_linear_wgrad");
 }
 
 int sfx_transpose(int rows, int cols, const float* src, long long lds, float* dst, long long ldd, void* stream) {

@@ -157,13 +157,18 @@ __global__ void __launch_bounds__(256) colsum2_kernel(int mode, int M, int C, co
   }
 }
 
+// one wave per output column: lanes take the partial rows lane, lane+64, ... (fixed order), then a fixed
+// butterfly -- deterministic, and 2C waves of parallelism instead of 2C threads
 __global__ void __launch_bounds__(256) colsum2_final_kernel(int C, int blocks, const double* __restrict__ part,
                                                             double* __restrict__ out) {
-  const int j = blockIdx.x * 256 + threadIdx.x;
+  const int j = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
   if (j >= 2 * C) return;
   double s = 0.0;
-  for (int b = 0; b < blocks; ++b) s += part[(long long)b * 2 * C + j];
-  out[j] = s;
+  for (int b = lane; b < blocks; b += 64) s += part[(long long)b * 2 * C + j];
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
+  if (lane == 0) out[j] = s;
 }
 
 // mean, biased var -> rstd; scale = gamma*rstd, shift = beta - mean*scale; running stats (unbiased var)
@@ -362,7 +367,7 @@ static int colsum2(int mode, int M, int C, const float* X, long long ldx, const 
   const int blocks = (int)sfx::ceil_div(M, COL_BLOCK_ROWS);
   colsum2_kernel<<<dim3(sfx::ceil_div(C, 64), blocks), 256, 0, st>>>(mode, M, C, X, ldx, mean, rstd, gamma, beta, act,
                                                                       dY, ldgy, static_cast<double*>(ws));
-  colsum2_final_kernel<<<sfx::ceil_div(2 * C, 256), 256, 0, st>>>(C, blocks, static_cast<double*>(ws), sums);
+  colsum2_final_kernel<<<sfx::ceil_div(2 * C, 4), 256, 0, st>>>(C, blocks, static_cast<double*>(ws), sums);
   return sfx::check_launch(what);
 }
 
