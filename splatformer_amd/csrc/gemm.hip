@@ -31,9 +31,12 @@ namespace {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 
 constexpr int BK = 32;
 constexpr int LDS_STRIDE = BK + 4;
+constexpr int SROW = BK + 8;  // split path: bf16 row stride (80 B: conflict-free ds_read_b128)
 constexpr int THREADS = 256;
 constexpr unsigned OOB = 0x7ffffff0u;        // byte offset past every descriptor extent
 constexpr int RSRC_FLAGS = 0x00020000;       // gfx950 raw buffer, 32-bit data
@@ -82,6 +85,7 @@ struct GemmArgs {
   // boundary gets partial sums (atomic add into a zero-filled output; the k-slab-0 owner adds the linear
   // epilogue terms).  Only for linear epilogues (no activation, no pre-residual copy, no in-place residual).
   int sk;
+  int split;  // 3-term bf16 split operands (see gemm_kernel); chosen in pick_cfg
 };
 
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
@@ -122,6 +126,29 @@ __device__ __forceinline__ void bstore1(__amdgpu_buffer_rsrc_t r, unsigned off, 
   __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, off, 0, 0);
 }
 
+// fp32 -> three bf16 terms by round-to-nearest (v_cvt_pk_bf16_f32): x = t0 + t1 + t2 + r with
+// |t1| <= 2^-8 |x|, |t2| <= 2^-16 |x|, |r| <= 2^-24 |x| (each residual x - t0, (x - t0) - t1 is exact in fp32).
+// bf16 keeps fp32's exponent range, so no scaling and no overflow cases.  Out: 4 elements x 3 terms, packed.
+__device__ __forceinline__ float bf_lo(unsigned u) { return __builtin_bit_cast(float, u << 16); }
+__device__ __forceinline__ float bf_hi(unsigned u) { return __builtin_bit_cast(float, u & 0xffff0000u); }
+__device__ __forceinline__ unsigned pk_bf16(float a, float b) {
+  const bf16x2 v = __builtin_convertvector((float __attribute__((ext_vector_type(2)))){a, b}, bf16x2);
+  return __builtin_bit_cast(unsigned, v);
+}
+__device__ __forceinline__ void split3(float4 v, uint2 (&t)[3]) {
+  unsigned u0 = pk_bf16(v.x, v.y), u1 = pk_bf16(v.z, v.w);
+  t[0] = make_uint2(u0, u1);
+  float r0 = v.x - bf_lo(u0), r1 = v.y - bf_hi(u0), r2 = v.z - bf_lo(u1), r3 = v.w - bf_hi(u1);
+  u0 = pk_bf16(r0, r1);
+  u1 = pk_bf16(r2, r3);
+  t[1] = make_uint2(u0, u1);
+  r0 -= bf_lo(u0);
+  r1 -= bf_hi(u0);
+  r2 -= bf_lo(u1);
+  r3 -= bf_hi(u1);
+  t[2] = make_uint2(pk_bf16(r0, r1), pk_bf16(r2, r3));
+}
+
 // Persistent tile loop: each workgroup walks output tiles blockIdx.x, +gridDim.x, ... and prefetches
 // the first K-slab of its NEXT tile while it computes the last slab and runs the epilogue of the
 // current one, so the global-load latency of a tile start and the epilogue stores overlap (short-K
@@ -129,7 +156,12 @@ __device__ __forceinline__ void bstore1(__amdgpu_buffer_rsrc_t r, unsigned off, 
 // MODE: how the A rows of a tile are found (compile-time so the load path has no runtime branches)
 enum Mode { MODE_DENSE = 0, MODE_GATHER1 = 1, MODE_GATHERS = 2, MODE_PAIR = 3 };
 
-template <int BM, int BN, int WGM, bool VEC, int MODE>
+// SPLIT: the fp32 operands are split into three bf16 terms on the LDS store and every 32x32x16 block
+// product is formed from the six leading term products (t0t0, t0t1, t1t0, t0t2, t1t1, t2t0; the dropped
+// ones are <= 2^-24 relative) on v_mfma_f32_32x32x16_bf16 with fp32 accumulation: fp32 accuracy at
+// 6 x 32 cycles per 32x32x16 block against 8 x 64 for v_mfma_f32_32x32x2_f32.  The split image is 1.5x
+// the fp32 one, so LDS is single-buffered (register prefetch of the next slab, two barriers per slab).
+template <int BM, int BN, int WGM, bool VEC, int MODE, bool SPLIT>
 __global__ void __launch_bounds__(THREADS, 2) gemm_kernel(GemmArgs p, int tiles_n, int total_tiles) {
   constexpr int WGN = 4 / WGM;                 // waves along N
   constexpr int WM = BM / WGM, WN = BN / WGN;  // wave sub-tile
@@ -138,8 +170,15 @@ __global__ void __launch_bounds__(THREADS, 2) gemm_kernel(GemmArgs p, int tiles_
                 "tile shape must split into 32x32 MFMA blocks and whole staging passes");
   constexpr int A_ITERS = BM * BK / 4 / THREADS;
   constexpr int W_ITERS = BN * BK / 4 / THREADS;
-  __shared__ __attribute__((aligned(16))) float sA[2][BM * LDS_STRIDE];
-  __shared__ __attribute__((aligned(16))) float sW[2][BN * LDS_STRIDE];
+  // fp32: double-buffered [row][k] images; SPLIT: one buffer of three bf16 term images per operand
+  constexpr int A_FLOATS = SPLIT ? 3 * BM * SROW / 2 : 2 * BM * LDS_STRIDE;
+  constexpr int W_FLOATS = SPLIT ? 3 * BN * SROW / 2 : 2 * BN * LDS_STRIDE;
+  __shared__ __attribute__((aligned(16))) float sAraw[A_FLOATS];
+  __shared__ __attribute__((aligned(16))) float sWraw[W_FLOATS];
+  float (*sA)[BM * LDS_STRIDE] = reinterpret_cast<float (*)[BM * LDS_STRIDE]>(sAraw);
+  float (*sW)[BN * LDS_STRIDE] = reinterpret_cast<float (*)[BN * LDS_STRIDE]>(sWraw);
+  unsigned short* sAs = reinterpret_cast<unsigned short*>(sAraw);  // [3][BM][SROW]
+  unsigned short* sWs = reinterpret_cast<unsigned short*>(sWraw);  // [3][BN][SROW]
 
   const int g = blockIdx.z;
   const float* A = p.A + g * p.gA;
@@ -260,6 +299,25 @@ __global__ void __launch_bounds__(THREADS, 2) gemm_kernel(GemmArgs p, int tiles_
     }
   };
   auto store_tiles = [&](int buf) {
+    if constexpr (SPLIT) {
+#pragma unroll
+      for (int i = 0; i < A_ITERS; ++i) {
+        uint2 t[3];
+        split3(ra[i], t);
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+          *reinterpret_cast<uint2*>(&sAs[(q * BM + lrow + 32 * i) * SROW + lcol]) = t[q];
+      }
+#pragma unroll
+      for (int i = 0; i < W_ITERS; ++i) {
+        uint2 t[3];
+        split3(rw[i], t);
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+          *reinterpret_cast<uint2*>(&sWs[(q * BN + lrow + 32 * i) * SROW + lcol]) = t[q];
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < A_ITERS; ++i)
       *reinterpret_cast<float4*>(&sA[buf][(lrow + 32 * i) * LDS_STRIDE + lcol]) = ra[i];
@@ -441,6 +499,33 @@ __global__ void __launch_bounds__(THREADS, 2) gemm_kernel(GemmArgs p, int tiles_
   };
 
   auto compute = [&](int buf) {
+    if constexpr (SPLIT) {
+#pragma unroll
+      for (int s = 0; s < BK / 16; ++s) {
+        bf16x8 af[MB][3], wf[NB][3];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+#pragma unroll
+          for (int a = 0; a < MB; ++a)
+            af[a][q] = __builtin_bit_cast(
+                bf16x8, *reinterpret_cast<const uint4*>(&sAs[(q * BM + wm * WM + a * 32 + l32) * SROW + s * 16 + h * 8]));
+#pragma unroll
+          for (int b = 0; b < NB; ++b)
+            wf[b][q] = __builtin_bit_cast(
+                bf16x8, *reinterpret_cast<const uint4*>(&sWs[(q * BN + wn * WN + b * 32 + l32) * SROW + s * 16 + h * 8]));
+        }
+        // smallest terms first; the (a, b) blocks interleave so consecutive MFMAs are independent
+        constexpr int QA[6] = {2, 1, 0, 1, 0, 0}, QW[6] = {0, 1, 2, 0, 1, 0};
+#pragma unroll
+        for (int j = 0; j < 6; ++j)
+#pragma unroll
+          for (int a = 0; a < MB; ++a)
+#pragma unroll
+            for (int b = 0; b < NB; ++b)
+              acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][QA[j]], wf[b][QW[j]], acc[a][b], 0, 0, 0);
+      }
+      return;
+    }
     const float* a_lds = &sA[buf][(wm * WM + l32) * LDS_STRIDE + h * 16];
     const float* w_lds = &sW[buf][(wn * WN + l32) * LDS_STRIDE + h * 16];
 #pragma unroll
@@ -510,9 +595,10 @@ __global__ void __launch_bounds__(THREADS, 2) gemm_kernel(GemmArgs p, int tiles_
       load_tiles(ti, kt + 1);
       __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of the MFMAs it overlaps
       compute(buf);
+      if constexpr (SPLIT) __syncthreads();  // single LDS buffer: every wave is done reading it
       store_tiles(buf ^ 1);
       __syncthreads();
-      buf ^= 1;
+      if constexpr (!SPLIT) buf ^= 1;
     }
     // last slab of the segment: its epilogue operands, then the first slab of the next segment in flight
     // while the last MFMAs and the epilogue run
@@ -530,9 +616,10 @@ __global__ void __launch_bounds__(THREADS, 2) gemm_kernel(GemmArgs p, int tiles_
     compute(buf);
     epilogue(ti, kb != 0 || ke != nk, kb == 0);
     if (!has_next) break;
+    if constexpr (SPLIT) __syncthreads();
     store_tiles(buf ^ 1);
     __syncthreads();
-    buf ^= 1;
+    if constexpr (!SPLIT) buf ^= 1;
     t = nt;
     ti = tn;
     kb = 0;
@@ -568,6 +655,7 @@ int tiles_m_of(GemmArgs& a, int BM) {
 
 template <int BM, int BN, int WGM, int MODE>
 void launch(GemmArgs a, int groups, bool vec, hipStream_t st) {
+  const bool split = a.split != 0;
   const int tiles_m = tiles_m_of(a, BM);
   const int tiles_n = (int)sfx::ceil_div(a.N, BN);
   const int total = tiles_m * tiles_n;
@@ -588,10 +676,14 @@ void launch(GemmArgs a, int groups, bool vec, hipStream_t st) {
     if (grid_x >= 8) grid_x = (grid_x + 7) / 8 * 8;  // whole XCD groups for the XCD-aware numbering
   }
   dim3 grid(grid_x, 1, groups);
-  if (vec)
-    gemm_kernel<BM, BN, WGM, true, MODE><<<grid, THREADS, 0, st>>>(a, tiles_n, total);
+  if (vec && split)
+    gemm_kernel<BM, BN, WGM, true, MODE, true><<<grid, THREADS, 0, st>>>(a, tiles_n, total);
+  else if (vec)
+    gemm_kernel<BM, BN, WGM, true, MODE, false><<<grid, THREADS, 0, st>>>(a, tiles_n, total);
+  else if (split)
+    gemm_kernel<BM, BN, WGM, false, MODE, true><<<grid, THREADS, 0, st>>>(a, tiles_n, total);
   else
-    gemm_kernel<BM, BN, WGM, false, MODE><<<grid, THREADS, 0, st>>>(a, tiles_n, total);
+    gemm_kernel<BM, BN, WGM, false, MODE, false><<<grid, THREADS, 0, st>>>(a, tiles_n, total);
 }
 
 // Tile shapes.  The choice minimises (rounds of 2-per-CU slots) x (tile area / relative MFMA efficiency):
@@ -603,6 +695,18 @@ struct TileCfg {
 };
 constexpr TileCfg kCfgs[] = {{128, 128, 1.0f}, {128, 96, 0.95f}, {128, 64, 0.8f}, {64, 128, 0.95f}, {64, 64, 0.8f}};  // eff fitted to tools/gemm_calls.py sweeps
 constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
+
+// Operand precision: the 3-term bf16 split (fp32-accurate, see gemm_kernel) from K >= split_min_k
+// (SFX_GEMM_SPLIT_MINK; default 64), exact fp32 MFMA below it or with SFX_GEMM_PREC=fp32.
+bool use_split(int K) {
+  static int min_k = -2;
+  if (min_k == -2) {
+    const char* e = getenv("SFX_GEMM_PREC");
+    const char* m = getenv("SFX_GEMM_SPLIT_MINK");
+    min_k = (e && e[0] == 'f') ? -1 : ((m && *m) ? atoi(m) : 64);
+  }
+  return min_k >= 0 && K >= min_k;
+}
 
 // -> configuration index; sets a.sk when the Stream-K split of the same tile shape is cheaper.
 int pick_cfg(GemmArgs& a, int groups) {
@@ -646,6 +750,7 @@ int pick_cfg(GemmArgs& a, int groups) {
     }
   }
   a.sk = best_sk ? 1 : 0;
+  a.split = use_split(a.K) ? 1 : 0;
   tiles_m_of(a, kCfgs[best].bm);  // pair mode: slice_tile_off for the chosen shape
   return best;
 }
