@@ -36,7 +36,6 @@ typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 
 constexpr int BK = 32;
 constexpr int LDS_STRIDE = BK + 4;
-constexpr int SROW = BK + 8;  // split path: bf16 row stride (80 B: conflict-free ds_read_b128)
 constexpr int THREADS = 256;
 constexpr unsigned OOB = 0x7ffffff0u;        // byte offset past every descriptor extent
 constexpr int RSRC_FLAGS = 0x00020000;       // gfx950 raw buffer, 32-bit data
@@ -112,6 +111,15 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p) {
   return __builtin_amdgcn_make_buffer_rsrc(u, (short)0, (int)OOB, RSRC_FLAGS);
 }
 
+// descriptor with an explicit extent (bytes): accesses at or past it are dropped / read 0
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_ext(const void* p, unsigned bytes) {
+  const unsigned long long a = reinterpret_cast<unsigned long long>(p);
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+  void* u = reinterpret_cast<void*>(((unsigned long long)hi << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(u, (short)0, (int)__builtin_amdgcn_readfirstlane(bytes), RSRC_FLAGS);
+}
+
 __device__ __forceinline__ float4 bload4(__amdgpu_buffer_rsrc_t r, unsigned off) {
   const floatx4 v = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
   return make_float4(v.x, v.y, v.z, v.w);
@@ -161,24 +169,36 @@ enum Mode { MODE_DENSE = 0, MODE_GATHER1 = 1, MODE_GATHERS = 2, MODE_PAIR = 3 };
 // ones are <= 2^-24 relative) on v_mfma_f32_32x32x16_bf16 with fp32 accumulation: fp32 accuracy at
 // 6 x 32 cycles per 32x32x16 block against 8 x 64 for v_mfma_f32_32x32x2_f32.  The split image is 1.5x
 // the fp32 one, so LDS is single-buffered (register prefetch of the next slab, two barriers per slab).
-template <int BM, int BN, int WGM, bool VEC, int MODE, bool SPLIT>
-__global__ void __launch_bounds__(THREADS, 2) gemm_kernel(GemmArgs p, int tiles_n, int total_tiles) {
-  constexpr int WGN = 4 / WGM;                 // waves along N
+//
+// NW = waves per workgroup: 4 (2 workgroups per CU) or 8 (one 512-thread workgroup per CU, the large
+// split tiles: 256x128 / 128x256 at 64x64 per wave, LDS double-buffered).
+// Split LDS image: per buffer and term a [rows][32] bf16 array with 64-byte rows and no padding; the
+// 16-byte chunk c of row r sits at chunk c ^ ((r >> 2) & 3), which makes the fragment reads (16 rows x one
+// chunk per quarter-wave) and the staging writes (4 rows x 64 B per half-wave) bank-conflict free.
+template <int BM, int BN, int WGM, int NW, bool VEC, int MODE, bool SPLIT>
+__global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs p, int tiles_n, int total_tiles) {
+  constexpr int NT = NW * 64;                  // threads
+  constexpr int WGN = NW / WGM;                // waves along N
   constexpr int WM = BM / WGM, WN = BN / WGN;  // wave sub-tile
-  constexpr int MB = WM / 32, NB = WN / 32; // 32x32 MFMA blocks per wave
-  static_assert(WM % 32 == 0 && WN % 32 == 0 && (BM * BK / 4) % THREADS == 0 && (BN * BK / 4) % THREADS == 0,
+  constexpr int MB = WM / 32, NB = WN / 32;    // 32x32 MFMA blocks per wave
+  constexpr int RPP = NT / 8;                  // staging rows per pass (8 threads x 4 floats per row)
+  static_assert(WM % 32 == 0 && WN % 32 == 0 && (BM * BK / 4) % NT == 0 && (BN * BK / 4) % NT == 0,
                 "tile shape must split into 32x32 MFMA blocks and whole staging passes");
-  constexpr int A_ITERS = BM * BK / 4 / THREADS;
-  constexpr int W_ITERS = BN * BK / 4 / THREADS;
-  // fp32: double-buffered [row][k] images; SPLIT: one buffer of three bf16 term images per operand
-  constexpr int A_FLOATS = SPLIT ? 3 * BM * SROW / 2 : 2 * BM * LDS_STRIDE;
-  constexpr int W_FLOATS = SPLIT ? 3 * BN * SROW / 2 : 2 * BN * LDS_STRIDE;
+  static_assert(SPLIT || NW == 4, "fp32 tiles run 4 waves");
+  constexpr int A_ITERS = BM * BK / 4 / NT;
+  constexpr int W_ITERS = BN * BK / 4 / NT;
+  constexpr int NBUF = SPLIT ? (NW == 8 ? 2 : 1) : 2;
+  // fp32: double-buffered [row][k] images (row stride 36); SPLIT: NBUF x 3 swizzled bf16 term images
+  constexpr int A_FLOATS = SPLIT ? NBUF * 3 * BM * BK / 2 : 2 * BM * LDS_STRIDE;
+  constexpr int W_FLOATS = SPLIT ? NBUF * 3 * BN * BK / 2 : 2 * BN * LDS_STRIDE;
   __shared__ __attribute__((aligned(16))) float sAraw[A_FLOATS];
   __shared__ __attribute__((aligned(16))) float sWraw[W_FLOATS];
   float (*sA)[BM * LDS_STRIDE] = reinterpret_cast<float (*)[BM * LDS_STRIDE]>(sAraw);
   float (*sW)[BN * LDS_STRIDE] = reinterpret_cast<float (*)[BN * LDS_STRIDE]>(sWraw);
-  unsigned short* sAs = reinterpret_cast<unsigned short*>(sAraw);  // [3][BM][SROW]
-  unsigned short* sWs = reinterpret_cast<unsigned short*>(sWraw);  // [3][BN][SROW]
+  char* sAs = reinterpret_cast<char*>(sAraw);  // [NBUF][3][BM][64 B]
+  char* sWs = reinterpret_cast<char*>(sWraw);  // [NBUF][3][BN][64 B]
+  // byte offset of the 4-element group at k = c4 * 4 (c4 = 0..7) of row r in a swizzled term image
+  auto swz = [](int r, int c4) -> int { return r * 64 + ((((c4 >> 1) ^ (r >> 2)) & 3) << 4) + ((c4 & 1) << 3); };
 
   const int g = blockIdx.z;
   const float* A = p.A + g * p.gA;
@@ -197,7 +217,7 @@ __global__ void __launch_bounds__(THREADS, 2) gemm_kernel(GemmArgs p, int tiles_
   // byte offsets fit 31 bits (host checks every operand against the 2 GiB buffer range)
   const unsigned lda32 = (unsigned)p.lda, ldw32 = (unsigned)p.ldw, ldy32 = (unsigned)p.ldy;
   const unsigned ldr32 = (unsigned)p.ldr, ldp32 = (unsigned)p.ldypre;
-  const int lrow = tid >> 3, lcol = (tid & 7) * 4;  // staging coordinates: rows lrow + 32 i, cols lcol..+3
+  const int lrow = tid >> 3, lcol = (tid & 7) * 4;  // staging coordinates: rows lrow + RPP i, cols lcol..+3
 
   // per-tile geometry (all wave-uniform)
   struct Tile {
@@ -243,7 +263,7 @@ __global__ void __launch_bounds__(THREADS, 2) gemm_kernel(GemmArgs p, int tiles_
       const int seg = MODE == MODE_GATHERS ? (kt * BK + lcol) / p.Kseg : 0;
 #pragma unroll
       for (int i = 0; i < A_ITERS; ++i) {
-        const int m = ti.m0 + lrow + 32 * i;
+        const int m = ti.m0 + lrow + RPP * i;
         rows[i] = bload1i(rG, (m < ti.M && seg < p.S) ? ((unsigned)m * (unsigned)ti.gstride + (unsigned)seg) * 4u
                                                       : OOB);
       }
@@ -262,7 +282,7 @@ __global__ void __launch_bounds__(THREADS, 2) gemm_kernel(GemmArgs p, int tiles_
     }
 #pragma unroll
     for (int i = 0; i < A_ITERS; ++i) {
-      const int m = ti.m0 + lrow + 32 * i;
+      const int m = ti.m0 + lrow + RPP * i;
       const bool mok = m < ti.M;
       unsigned off;
       if constexpr (MODE != MODE_DENSE) {
@@ -284,7 +304,7 @@ __global__ void __launch_bounds__(THREADS, 2) gemm_kernel(GemmArgs p, int tiles_
     }
 #pragma unroll
     for (int i = 0; i < W_ITERS; ++i) {
-      const int n = ti.n0 + lrow + 32 * i;
+      const int n = ti.n0 + lrow + RPP * i;
       const unsigned off = (n < p.N && kin) ? ((unsigned)n * ldw32 + (unsigned)k) * 4u : OOB;
       if (VEC) {
         rw[i] = bload4(rW, off);
@@ -300,30 +320,31 @@ __global__ void __launch_bounds__(THREADS, 2) gemm_kernel(GemmArgs p, int tiles_
   };
   auto store_tiles = [&](int buf) {
     if constexpr (SPLIT) {
+      const int b = NBUF == 2 ? buf : 0;
 #pragma unroll
       for (int i = 0; i < A_ITERS; ++i) {
         uint2 t[3];
         split3(ra[i], t);
+        const int o = swz(lrow + RPP * i, lcol >> 2);
 #pragma unroll
-        for (int q = 0; q < 3; ++q)
-          *reinterpret_cast<uint2*>(&sAs[(q * BM + lrow + 32 * i) * SROW + lcol]) = t[q];
+        for (int q = 0; q < 3; ++q) *reinterpret_cast<uint2*>(sAs + ((b * 3 + q) * BM) * 64 + o) = t[q];
       }
 #pragma unroll
       for (int i = 0; i < W_ITERS; ++i) {
         uint2 t[3];
         split3(rw[i], t);
+        const int o = swz(lrow + RPP * i, lcol >> 2);
 #pragma unroll
-        for (int q = 0; q < 3; ++q)
-          *reinterpret_cast<uint2*>(&sWs[(q * BN + lrow + 32 * i) * SROW + lcol]) = t[q];
+        for (int q = 0; q < 3; ++q) *reinterpret_cast<uint2*>(sWs + ((b * 3 + q) * BN) * 64 + o) = t[q];
       }
       return;
     }
 #pragma unroll
     for (int i = 0; i < A_ITERS; ++i)
-      *reinterpret_cast<float4*>(&sA[buf][(lrow + 32 * i) * LDS_STRIDE + lcol]) = ra[i];
+      *reinterpret_cast<float4*>(&sA[buf][(lrow + RPP * i) * LDS_STRIDE + lcol]) = ra[i];
 #pragma unroll
     for (int i = 0; i < W_ITERS; ++i)
-      *reinterpret_cast<float4*>(&sW[buf][(lrow + 32 * i) * LDS_STRIDE + lcol]) = rw[i];
+      *reinterpret_cast<float4*>(&sW[buf][(lrow + RPP * i) * LDS_STRIDE + lcol]) = rw[i];
   };
 
   floatx16 acc[MB][NB];
@@ -384,7 +405,104 @@ __global__ void __launch_bounds__(THREADS, 2) gemm_kernel(GemmArgs p, int tiles_
 
   // epilogue: branch-free buffer stores (row -1 / out-of-range column -> dropped); the runtime epilogue
   // options are tested once per 16-element column strip, never per element.
+  // Direct-row epilogue (no output-row remap, the common case): every operand row r of a 32-row block is
+  // base + rowc(r) * ld with a wave-uniform rowc(r) * ld, so an address costs one add; rows past M fall
+  // outside the descriptor extent (M * ld * 4 bytes) and columns past N get a base past every extent, so
+  // the hardware drops / zero-fills them with no per-element selects.  One FMA applies bias/scale/shift.
+  constexpr unsigned OOBX = 0x80000000u;
+  auto rowc = [](int r) -> unsigned { return (unsigned)((r & 3) + 8 * (r >> 2)); };
+  auto direct_epilogue = [&](const Tile& ti, bool partial, bool owner0) {
+    const unsigned Mu = (unsigned)ti.M;
+    const __amdgpu_buffer_rsrc_t rYd = rsrc_ext(Y, Mu * ldy32 * 4u);
+    const __amdgpu_buffer_rsrc_t rPd = rsrc_ext(p.Ypre ? p.Ypre : Y, Mu * ldp32 * 4u);
+    const __amdgpu_buffer_rsrc_t rRd = rsrc_ext(p.R ? p.R : Y, p.ridx ? OOB : Mu * ldr32 * 4u);
+    const __amdgpu_buffer_rsrc_t rSd = rsrc_ext(p.rowscale ? p.rowscale : p.W, Mu * 4u);
+    const unsigned ldd32 = (unsigned)p.ld_dact;
+    const __amdgpu_buffer_rsrc_t rDd = rsrc_ext(p.dact_pre ? p.dact_pre : p.W, Mu * ldd32 * 4u);
+    const __amdgpu_buffer_rsrc_t rI = rsrc(p.ridx ? (const void*)p.ridx : (const void*)p.W);
+#pragma unroll
+    for (int a = 0; a < MB; ++a) {
+      const unsigned mb = (unsigned)(ti.m0 + wm * WM + a * 32 + 4 * h);  // row of r = 0 (this lane half)
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        const int n = ti.n0 + wn * WN + b * 32 + l32;
+        const bool nok = n < p.N;
+        const bool do_act = n < p.act_ncols;
+        const unsigned by = nok ? (mb * ldy32 + (unsigned)n) * 4u : OOBX;
+        const float c1 = p.scale ? escale[b] : 1.f;
+        const float cb = ebias[b] * c1 + eshift[b];
+        const float c0 = (partial && !owner0) ? 0.f : cb;
+        float v[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] = __builtin_fmaf(acc[a][b][r], c1, c0);
+        if (p.Ypre && p.pre_before_act) {
+          const unsigned bp = nok ? (mb * ldp32 + (unsigned)n) * 4u : OOBX;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) bstore1(rPd, bp + rowc(r) * ldp32 * 4u, v[r]);
+        }
+        if (p.act == ACT_GELU) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) v[r] = do_act ? gelu_erf(v[r]) : v[r];
+        } else if (p.act == ACT_RELU) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) v[r] = do_act ? fmaxf(v[r], 0.f) : v[r];
+        } else if (p.act == ACT_TANH) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) v[r] = do_act ? tanhf(v[r]) : v[r];
+        }
+        if (p.rowscale) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) v[r] *= bload1(rSd, (mb + rowc(r)) * 4u);
+        }
+        if (p.dact) {
+          const unsigned bd = nok ? (mb * ldd32 + (unsigned)n) * 4u : OOBX;
+          float pre[16];
+#pragma unroll
+          for (int r = 0; r < 16; ++r) pre[r] = bload1(rDd, bd + rowc(r) * ldd32 * 4u);
+#pragma unroll
+          for (int r = 0; r < 16; ++r) v[r] = do_act ? v[r] * dact_grad(p.dact, pre[r]) : v[r];
+        }
+        if (p.Ypre && !p.pre_before_act) {
+          const unsigned bp = nok ? (mb * ldp32 + (unsigned)n) * 4u : OOBX;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) bstore1(rPd, bp + rowc(r) * ldp32 * 4u, v[r]);
+        }
+        if (p.R && owner0) {
+          float rv[16];
+          if (p.ridx) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const unsigned m = mb + rowc(r);
+              const int ri = bload1i(rI, m < Mu ? m * 4u : OOB);
+              rv[r] = bload1(rRd, (nok && m < Mu) ? ((unsigned)ri * ldr32 + (unsigned)n) * 4u : OOB);
+            }
+          } else {
+            const unsigned br = nok ? (mb * ldr32 + (unsigned)n) * 4u : OOBX;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) rv[r] = bload1(rRd, br + rowc(r) * ldr32 * 4u);
+          }
+#pragma unroll
+          for (int r = 0; r < 16; ++r) v[r] += rv[r];
+        }
+        if (partial) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(v[r], rYd, by + rowc(r) * ldy32 * 4u, 0, 0);
+        } else {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) bstore1(rYd, by + rowc(r) * ldy32 * 4u, v[r]);
+        }
+      }
+    }
+  };
+
   auto epilogue = [&](const Tile& ti, bool partial, bool owner0) {
+    if constexpr (MODE != MODE_PAIR) {
+      if (!ti.out_rows) {
+        direct_epilogue(ti, partial, owner0);
+        return;
+      }
+    }
     resolve_rows(ti);
     if constexpr (MODE == MODE_PAIR) {  // partial sums of one neighbour offset: accumulate into the output rows
 #pragma unroll
@@ -498,32 +616,41 @@ __global__ void __launch_bounds__(THREADS, 2) gemm_kernel(GemmArgs p, int tiles_
     }
   };
 
-  auto compute = [&](int buf) {
-    if constexpr (SPLIT) {
+  // SPLIT: k16 steps [s0, s1) of the slab
+  auto compute_split = [&](int buf, int s0, int s1) {
+    const int bb = NBUF == 2 ? buf : 0;
 #pragma unroll
-      for (int s = 0; s < BK / 16; ++s) {
-        bf16x8 af[MB][3], wf[NB][3];
+    for (int s = s0; s < s1; ++s) {
+      bf16x8 af[MB][3], wf[NB][3];
 #pragma unroll
-        for (int q = 0; q < 3; ++q) {
+      for (int q = 0; q < 3; ++q) {
 #pragma unroll
-          for (int a = 0; a < MB; ++a)
-            af[a][q] = __builtin_bit_cast(
-                bf16x8, *reinterpret_cast<const uint4*>(&sAs[(q * BM + wm * WM + a * 32 + l32) * SROW + s * 16 + h * 8]));
+        for (int a = 0; a < MB; ++a) {
+          const int r = wm * WM + a * 32 + l32;
+          af[a][q] = __builtin_bit_cast(
+              bf16x8, *reinterpret_cast<const uint4*>(sAs + ((bb * 3 + q) * BM) * 64 + swz(r, 4 * s + 2 * h)));
+        }
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+          const int r = wn * WN + b * 32 + l32;
+          wf[b][q] = __builtin_bit_cast(
+              bf16x8, *reinterpret_cast<const uint4*>(sWs + ((bb * 3 + q) * BN) * 64 + swz(r, 4 * s + 2 * h)));
+        }
+      }
+      // smallest terms first; the (a, b) blocks interleave so consecutive MFMAs are independent
+      constexpr int QA[6] = {2, 1, 0, 1, 0, 0}, QW[6] = {0, 1, 2, 0, 1, 0};
+#pragma unroll
+      for (int j = 0; j < 6; ++j)
+#pragma unroll
+        for (int a = 0; a < MB; ++a)
 #pragma unroll
           for (int b = 0; b < NB; ++b)
-            wf[b][q] = __builtin_bit_cast(
-                bf16x8, *reinterpret_cast<const uint4*>(&sWs[(q * BN + wn * WN + b * 32 + l32) * SROW + s * 16 + h * 8]));
-        }
-        // smallest terms first; the (a, b) blocks interleave so consecutive MFMAs are independent
-        constexpr int QA[6] = {2, 1, 0, 1, 0, 0}, QW[6] = {0, 1, 2, 0, 1, 0};
-#pragma unroll
-        for (int j = 0; j < 6; ++j)
-#pragma unroll
-          for (int a = 0; a < MB; ++a)
-#pragma unroll
-            for (int b = 0; b < NB; ++b)
-              acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][QA[j]], wf[b][QW[j]], acc[a][b], 0, 0, 0);
-      }
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][QA[j]], wf[b][QW[j]], acc[a][b], 0, 0, 0);
+    }
+  };
+  auto compute = [&](int buf) {
+    if constexpr (SPLIT) {
+      compute_split(buf, 0, BK / 16);
       return;
     }
     const float* a_lds = &sA[buf][(wm * WM + l32) * LDS_STRIDE + h * 16];
@@ -595,10 +722,10 @@ __global__ void __launch_bounds__(THREADS, 2) gemm_kernel(GemmArgs p, int tiles_
       load_tiles(ti, kt + 1);
       __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of the MFMAs it overlaps
       compute(buf);
-      if constexpr (SPLIT) __syncthreads();  // single LDS buffer: every wave is done reading it
+      if constexpr (NBUF == 1) __syncthreads();  // single LDS buffer: every wave is done reading it
       store_tiles(buf ^ 1);
       __syncthreads();
-      if constexpr (!SPLIT) buf ^= 1;
+      if constexpr (NBUF == 2) buf ^= 1;
     }
     // last slab of the segment: its epilogue operands, then the first slab of the next segment in flight
     // while the last MFMAs and the epilogue run
@@ -616,10 +743,10 @@ __global__ void __launch_bounds__(THREADS, 2) gemm_kernel(GemmArgs p, int tiles_
     compute(buf);
     epilogue(ti, kb != 0 || ke != nk, kb == 0);
     if (!has_next) break;
-    if constexpr (SPLIT) __syncthreads();
+    if constexpr (NBUF == 1) __syncthreads();
     store_tiles(buf ^ 1);
     __syncthreads();
-    if constexpr (!SPLIT) buf ^= 1;
+    if constexpr (NBUF == 2) buf ^= 1;
     t = nt;
     ti = tn;
     kb = 0;
@@ -653,15 +780,16 @@ int tiles_m_of(GemmArgs& a, int BM) {
   return t;
 }
 
-template <int BM, int BN, int WGM, int MODE>
+template <int BM, int BN, int WGM, int NW, int MODE>
 void launch(GemmArgs a, int groups, bool vec, hipStream_t st) {
   const bool split = a.split != 0;
   const int tiles_m = tiles_m_of(a, BM);
   const int tiles_n = (int)sfx::ceil_div(a.N, BN);
   const int total = tiles_m * tiles_n;
-  // persistent grid: 2 workgroups per CU (LDS/VGPR bound), balanced so every workgroup gets the same
-  // number of tiles (+-1)
-  const int slots = 2 * num_cus() / groups > 0 ? 2 * num_cus() / groups : 1;
+  // persistent grid: 2 four-wave or 1 eight-wave workgroup per CU (LDS/VGPR bound), balanced so every
+  // workgroup gets the same number of tiles (+-1)
+  const int per_cu = NW == 4 ? 2 : 1;
+  const int slots = per_cu * num_cus() / groups > 0 ? per_cu * num_cus() / groups : 1;
   int grid_x;
   if (a.sk) {
     const long long iters = (long long)total * sfx::ceil_div(a.K, BK);
@@ -676,24 +804,28 @@ void launch(GemmArgs a, int groups, bool vec, hipStream_t st) {
     if (grid_x >= 8) grid_x = (grid_x + 7) / 8 * 8;  // whole XCD groups for the XCD-aware numbering
   }
   dim3 grid(grid_x, 1, groups);
-  if (vec && split)
-    gemm_kernel<BM, BN, WGM, true, MODE, true><<<grid, THREADS, 0, st>>>(a, tiles_n, total);
-  else if (vec)
-    gemm_kernel<BM, BN, WGM, true, MODE, false><<<grid, THREADS, 0, st>>>(a, tiles_n, total);
-  else if (split)
-    gemm_kernel<BM, BN, WGM, false, MODE, true><<<grid, THREADS, 0, st>>>(a, tiles_n, total);
-  else
-    gemm_kernel<BM, BN, WGM, false, MODE, false><<<grid, THREADS, 0, st>>>(a, tiles_n, total);
+  if constexpr (NW == 8) {  // split-only tiles (vec operands)
+    gemm_kernel<BM, BN, WGM, 8, true, MODE, true><<<grid, 512, 0, st>>>(a, tiles_n, total);
+  } else {
+    if (vec && split)
+      gemm_kernel<BM, BN, WGM, 4, true, MODE, true><<<grid, 256, 0, st>>>(a, tiles_n, total);
+    else if (vec)
+      gemm_kernel<BM, BN, WGM, 4, true, MODE, false><<<grid, 256, 0, st>>>(a, tiles_n, total);
+    else
+      gemm_kernel<BM, BN, WGM, 4, false, MODE, false><<<grid, 256, 0, st>>>(a, tiles_n, total);
+  }
 }
 
-// Tile shapes.  The choice minimises (rounds of 2-per-CU slots) x (tile area / relative MFMA efficiency):
-// with K = 64..2048 and M = 15k..100k every layer is a few rounds of tiles, so wave quantisation and
-// N-padding (N = 96, 288 on the C=96 stages) decide more than peak per-tile efficiency.
+// Tile shapes.  The choice minimises (rounds of per-CU slots) x (tile area / relative efficiency): with
+// K = 64..2048 and M = 15k..100k every layer is a few rounds of tiles, so wave quantisation and N-padding
+// (N = 96, 288 on the C=96 stages) decide more than peak per-tile efficiency.  The eight-wave tiles exist
+// only with split operands.
 struct TileCfg {
-  int bm, bn;
+  int bm, bn, nw;
   float eff;
 };
-constexpr TileCfg kCfgs[] = {{128, 128, 1.0f}, {128, 96, 0.95f}, {128, 64, 0.8f}, {64, 128, 0.95f}, {64, 64, 0.8f}};  // eff fitted to tools/gemm_calls.py sweeps
+constexpr TileCfg kCfgs[] = {{128, 128, 4, 1.0f}, {128, 96, 4, 0.95f}, {128, 64, 4, 0.8f}, {64, 128, 4, 0.95f},
+                             {64, 64, 4, 0.8f},   {256, 128, 8, 1.05f}, {128, 256, 8, 1.05f}};  // eff: tools/gemm_calls.py sweeps
 constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
 
 // Operand precision: the 3-term bf16 split (fp32-accurate, see gemm_kernel) from K >= split_min_k
@@ -709,7 +841,7 @@ bool use_split(int K) {
 }
 
 // -> configuration index; sets a.sk when the Stream-K split of the same tile shape is cheaper.
-int pick_cfg(GemmArgs& a, int groups) {
+int pick_cfg(GemmArgs& a, int groups, bool vec) {
   static int forced = -2, forced_sk = -2;
   if (forced == -2) {  // tuning hooks: SFX_GEMM_CFG=<index into kCfgs>, SFX_GEMM_SK=0|1
     const char* e = getenv("SFX_GEMM_CFG");
@@ -718,8 +850,8 @@ int pick_cfg(GemmArgs& a, int groups) {
     const char* k = getenv("SFX_GEMM_SK");
     forced_sk = (k && *k) ? atoi(k) : -1;
   }
-  const long long slots = 2ll * num_cus() / groups;
   const int nk = (int)sfx::ceil_div(a.K, BK);
+  const bool split = vec && use_split(a.K);
   // Stream-K needs a linear epilogue that can be split into atomically added pieces
   // (measured: the memset + atomic partial epilogues only pay off on long K; pair mode needs no memset)
   const bool sk_ok = groups == 1 && nk >= (a.pair_mode ? 8 : 16) && a.act == ACT_NONE && !a.Ypre && !a.out_rows &&
@@ -730,13 +862,16 @@ int pick_cfg(GemmArgs& a, int groups) {
   double best_cost = 1e300;
   for (int c = 0; c < kNumCfgs; ++c) {
     if (forced >= 0 && c != forced) continue;
-    const double area = (double)kCfgs[c].bm * kCfgs[c].bn / kCfgs[c].eff;
+    if (kCfgs[c].nw == 8 && !split) continue;
+    const long long slots = (kCfgs[c].nw == 4 ? 2ll : 1ll) * num_cus() / groups;
+    // tile area per unit of CU throughput (an eight-wave tile has the whole CU, a four-wave one half)
+    const double area = (double)kCfgs[c].bm * kCfgs[c].bn / kCfgs[c].eff / (kCfgs[c].nw / 4);
     const long long tiles = (long long)tiles_m_of(a, kCfgs[c].bm) * sfx::ceil_div(a.N, kCfgs[c].bn) * groups;
     const long long rounds = (tiles + slots - 1) / slots;
     // cost in slab-area units: K slabs + ~1 slab-equivalent of epilogue per tile
     double cost = (double)rounds * (nk + 1) * area;
     bool sk = false;
-    if (sk_ok && c <= 2) {  // Stream-K on the 128-row shapes: ~1.5 extra slab-equivalents (2 partial epilogues)
+    if (sk_ok && kCfgs[c].bm >= 128) {  // Stream-K on the 128-row shapes: ~1.5 extra slab-equivalents (2 partial epilogues)
       const double sk_cost = ((double)((tiles * nk + slots - 1) / slots) + sk_overhead) * area;
       if (sk_cost < cost || forced_sk == 1) {
         cost = sk_cost;
@@ -750,19 +885,21 @@ int pick_cfg(GemmArgs& a, int groups) {
     }
   }
   a.sk = best_sk ? 1 : 0;
-  a.split = use_split(a.K) ? 1 : 0;
+  a.split = split ? 1 : 0;
   tiles_m_of(a, kCfgs[best].bm);  // pair mode: slice_tile_off for the chosen shape
   return best;
 }
 
 template <int MODE>
 void dispatch_mode(GemmArgs a, int groups, bool vec, hipStream_t st) {
-  switch (pick_cfg(a, groups)) {
-    case 0: launch<128, 128, 2, MODE>(a, groups, vec, st); break;
-    case 1: launch<128, 96, 4, MODE>(a, groups, vec, st); break;
-    case 2: launch<128, 64, 2, MODE>(a, groups, vec, st); break;
-    case 3: launch<64, 128, 2, MODE>(a, groups, vec, st); break;
-    default: launch<64, 64, 2, MODE>(a, groups, vec, st); break;
+  switch (pick_cfg(a, groups, vec)) {
+    case 0: launch<128, 128, 2, 4, MODE>(a, groups, vec, st); break;
+    case 1: launch<128, 96, 4, 4, MODE>(a, groups, vec, st); break;
+    case 2: launch<128, 64, 2, 4, MODE>(a, groups, vec, st); break;
+    case 3: launch<64, 128, 2, 4, MODE>(a, groups, vec, st); break;
+    case 4: launch<64, 64, 2, 4, MODE>(a, groups, vec, st); break;
+    case 5: launch<256, 128, 4, 8, MODE>(a, groups, vec, st); break;
+    default: launch<128, 256, 2, 8, MODE>(a, groups, vec, st); break;
   }
 }
 
@@ -774,7 +911,7 @@ void dispatch(const GemmArgs& a, int groups, bool vec, hipStream_t st) {
   else if (a.S == 1)
     dispatch_mode<MODE_GATHER1>(a, groups, vec, st);
   else
-    launch<64, 128, 2, MODE_GATHERS>(a, groups, vec, st);  // multi-segment gather: test/reference path only
+    launch<64, 128, 2, 4, MODE_GATHERS>(a, groups, vec, st);  // multi-segment gather: test/reference path only
 }
 
 
