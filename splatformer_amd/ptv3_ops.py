@@ -56,7 +56,8 @@ def linear(x: Tensor, weight: Tensor, bias: Optional[Tensor] = None, *, act: int
            gather_idx: Optional[Tensor] = None, rows: Optional[int] = None,
            out_rows: Optional[Tensor] = None, rowscale: Optional[Tensor] = None,
            pre_before_act: bool = False) -> Tensor:
-    """y = act((x W^T + b) * scale + shift) + residual[residual_idx]  (fp32 MFMA GEMM, csrc/gemm.hip).
+    """y = act((x W^T + b) * scale + shift) + residual[residual_idx]  (csrc/gemm.hip: fp32-accurate MFMA GEMM,
+    3-term bf16 split operands for K >= 64, exact f32 MFMA below; SFX_GEMM_PREC=fp32 forces f32 MFMA).
 
     With `gather_idx` [M, S] (int32, -1 = empty) the A operand is the implicit
     concatenation of S gathered rows of `x` (SubMConv3d as implicit GEMM).

@@ -40,6 +40,23 @@ def test_linear_vs_torch(device, M, N, K, act):
     assert rel_l2(y.cpu(), ref) < 2e-6
 
 
+@pytest.mark.parametrize("scale", [1.0, 1e-30, 1e30])
+def test_linear_split_precision_is_fp32(device, scale):
+    """The 3-term bf16 split GEMM (default for K >= 64) is as accurate as fp32 arithmetic: its error against
+    an fp64 product is at most that of torch's fp32 CPU GEMM (x1.5), at any magnitude bf16 shares with fp32
+    (no scaling, no overflow: operands at 1e+-30)."""
+    g = torch.Generator().manual_seed(7)
+    M, N, K = 2000, 384, 1024
+    x = torch.randn(M, K, generator=g) * scale
+    w = torch.randn(N, K, generator=g) / K ** 0.5
+    ref = x.double() @ w.double().T
+    y = ops.linear(x.to(device), w.to(device), None).cpu()
+    e_hip = rel_l2(y, ref)
+    e_f32 = rel_l2(x @ w.T, ref)
+    assert torch.isfinite(y).all()
+    assert e_hip <= 1.5 * e_f32, (e_hip, e_f32)
+
+
 def test_linear_gather_is_subm_conv(device):
     n, C = 4000, 64
     s = make_scene(n, 1, seed=3, unique_voxels=True)
