@@ -20,6 +20,8 @@
 // its 128 keys in registers (64 per half-wave), so the softmax is a register
 // reduction + one cross-half exchange, and P^T feeds the P.V MFMA directly as
 // the B operand (no LDS round trip for P).
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
@@ -137,6 +139,203 @@ window_attn_kernel(const float* __restrict__ qkv, const int* __restrict__ order,
       o = __builtin_amdgcn_mfma_f32_32x32x2f32(vcol[key0 * DPV], s[kb][st], o, 0, 0, 0);
     }
 
+  // scatter: query 32*wid + l32 (lane column), dd rows (r&3) + 8(r>>2) + 4h
+  const int qi = 32 * wid + l32;
+  const int qpos = key_start + qi;
+  if (qi < Kwin && qpos >= query_start) {
+    float* dst = out + (long long)rows[qi] * C + head * D;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int dd = 8 * g + 4 * h;
+      if (dd + 3 < D) {
+        *reinterpret_cast<float4*>(dst + dd) = make_float4(o[4 * g + 0], o[4 * g + 1], o[4 * g + 2], o[4 * g + 3]);
+      }
+    }
+  }
+}
+
+
+// ---- split-bf16 forward (default) ---------------------------------------------------------------------
+// The same dataflow on v_mfma_f32_32x32x16_bf16: q, k, v and p enter as three bf16 terms each
+// (sfx::split3) and every 32x32x16 block is the six leading term products accumulated in fp32 -- fp32
+// accuracy at 6 x 32 MFMA cycles per 16-deep step instead of 8 x 64 on v_mfma_f32_32x32x2_f32.
+//   S^T = K Q^T: A = K [key][dd], B = Q^T, KD = 16 (D = 16) or 32 (D = 24, 32; columns >= D zero).
+//   O^T = V^T P^T: B = P^T straight from the softmax registers -- registers 8s..8s+7 of key block kb are
+//   the 16-key step s (element j <-> key 32kb + 16s + 8(j>>2) + 4h + (j&3)); A = V^T, staged transposed
+//   with the keys of every 16-key group permuted to that order so a lane's 8 keys are one 16-byte read.
+// LDS: K term image [3][128][KD] (KD = 16: 48-byte rows; KD = 32: 64-byte rows, 16-byte chunks XOR-
+// swizzled by row >> 2), V^T [3][D][136] (272-byte rows; lanes dd >= D feed zero fragments); all fragment
+// reads are conflict-free.  Q never touches LDS: each lane gathers and splits its own query's 8-wide
+// slices.  31-50 KB per workgroup: 3-4 workgroups per CU to hide the row gathers.
+template <int D>
+__global__ void __launch_bounds__(256, D == 16 ? 4 : 3)
+window_attn_split_kernel(const float* __restrict__ qkv, const int* __restrict__ order, const int* __restrict__ win,
+                         int Kwin, int C, float scale, float* __restrict__ out) {
+  typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+  constexpr int KD = D == 16 ? 16 : 32;
+  constexpr int NKS = KD / 16;
+  constexpr int QROW = KD == 16 ? 48 : 64;  // bytes per Q/K term row
+  constexpr int VST = 136;                  // V^T row stride (bf16)
+  constexpr int QK_BYTES = 3 * KMAX * QROW;
+  constexpr int V_BYTES = 3 * D * VST * 2;
+  __shared__ __attribute__((aligned(16))) char lds[QK_BYTES + V_BYTES];
+  __shared__ int rows[KMAX];
+  char* Ks = lds;
+  unsigned short* Vt = reinterpret_cast<unsigned short*>(lds + QK_BYTES);
+  // byte offset of 16-byte chunk c of term row r
+  auto qk_off = [](int r, int c) -> int {
+    return KD == 16 ? r * 48 + c * 16 : r * 64 + (((c ^ (r >> 2)) & 3) << 4);
+  };
+
+  const int w = blockIdx.x, head = blockIdx.y;
+  const int key_start = win[2 * w], query_start = win[2 * w + 1];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, h = lane >> 5, l32 = lane & 31;
+  const long long ld = 3ll * C;
+
+  if (tid < KMAX) rows[tid] = tid < Kwin ? order[key_start + tid] : -1;
+  // zero padding: K columns D..KD-1 (never written by the staging below)
+  if (D < KD)
+    for (int rr = tid; rr < 3 * KMAX; rr += 256)  // term rows, term-major
+      *reinterpret_cast<uint4*>(Ks + qk_off(rr, D / 8)) = make_uint4(0, 0, 0, 0);
+  __syncthreads();
+  // gather + split, one matrix at a time (wave-uniform paths): q, k rows as KMAX x D/4 float4; v as
+  // key pairs x D/4 float4 so the transposed V^T writes are whole dwords (keys 2m, 2m+1 are adjacent
+  // in the permuted order)
+  constexpr int CH = D / 4;
+  typedef unsigned uintx4 __attribute__((ext_vector_type(4)));
+  // this lane's query slices (B operand of S^T = K Q^T): dd = 16 ks + 8h + j, zero past D
+  bf16x8 qf[NKS][3];
+  {
+    const int src = rows[32 * wid + l32];
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      const int d0 = 16 * ks + 8 * h;
+      float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+      if (src >= 0 && d0 < D) {
+        const float* qp = qkv + (long long)src * ld + head * D + d0;
+        a = *reinterpret_cast<const float4*>(qp);
+        if (d0 + 4 < D) b = *reinterpret_cast<const float4*>(qp + 4);
+      }
+      // scale * log2(e) folded into q: the softmax exponentials are plain exp2
+      const float qs = scale * 1.4426950408889634f;
+      a.x *= qs; a.y *= qs; a.z *= qs; a.w *= qs;
+      b.x *= qs; b.y *= qs; b.z *= qs; b.w *= qs;
+      uint2 ta[3], tb[3];
+      sfx::split3(a, ta);
+      sfx::split3(b, tb);
+#pragma unroll
+      for (int q = 0; q < 3; ++q) qf[ks][q] = __builtin_bit_cast(bf16x8, (uintx4){ta[q].x, ta[q].y, tb[q].x, tb[q].y});
+    }
+  }
+  for (int e = tid; e < KMAX * CH; e += 256) {
+    const int row = e / CH, ch = e - row * CH;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    const int src = rows[row];
+    if (src >= 0) v = *reinterpret_cast<const float4*>(qkv + (long long)src * ld + C + head * D + 4 * ch);
+    uint2 t[3];
+    sfx::split3(v, t);
+    const int o = qk_off(row, ch >> 1) + ((ch & 1) << 3);
+#pragma unroll
+    for (int q = 0; q < 3; ++q) *reinterpret_cast<uint2*>(Ks + q * KMAX * QROW + o) = t[q];
+  }
+  for (int e = tid; e < (KMAX / 2) * CH; e += 256) {
+    const int kp = e / CH, ch = e - kp * CH;
+    const int row = 2 * kp;
+    const int s0 = rows[row], s1 = rows[row + 1];
+    float4 v0 = make_float4(0.f, 0.f, 0.f, 0.f), v1 = v0;
+    if (s0 >= 0) v0 = *reinterpret_cast<const float4*>(qkv + (long long)s0 * ld + 2 * C + head * D + 4 * ch);
+    if (s1 >= 0) v1 = *reinterpret_cast<const float4*>(qkv + (long long)s1 * ld + 2 * C + head * D + 4 * ch);
+    uint2 t0[3], t1[3];
+    sfx::split3(v0, t0);
+    sfx::split3(v1, t1);
+    const int kk = row & 15;  // even: keys row, row + 1 land on adjacent positions
+    const int pos = (row & ~15) + 8 * ((kk >> 2) & 1) + (((kk >> 3) << 2) | (kk & 3));
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      unsigned* vt = reinterpret_cast<unsigned*>(Vt + (q * D + 4 * ch) * VST + pos);
+      vt[0] = (t0[q].x & 0xffffu) | (t1[q].x << 16);
+      vt[VST / 2] = (t0[q].x >> 16) | (t1[q].x & 0xffff0000u);
+      vt[VST] = (t0[q].y & 0xffffu) | (t1[q].y << 16);
+      vt[3 * VST / 2] = (t0[q].y >> 16) | (t1[q].y & 0xffff0000u);
+    }
+  }
+  __syncthreads();
+
+  constexpr int QA[6] = {2, 1, 0, 1, 0, 0}, QB[6] = {0, 1, 2, 0, 1, 0};
+  // S^T[key][query] for this wave's 32 queries, 4 key blocks of 32
+  floatx16 s[4];
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s[kb][r] = 0.f;
+#pragma unroll
+  for (int ks = 0; ks < NKS; ++ks) {
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+      bf16x8 kf[3];
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+        kf[q] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(
+                                               Ks + q * KMAX * QROW + qk_off(kb * 32 + l32, 2 * ks + h)));
+#pragma unroll
+      for (int j = 0; j < 6; ++j)
+        s[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[QA[j]], qf[ks][QB[j]], s[kb], 0, 0, 0);
+    }
+  }
+  // softmax over keys (register axis + the other half-wave); keys >= Kwin only exist in short windows
+  if (Kwin < KMAX) {
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (key >= Kwin) s[kb][r] = -INFINITY;
+      }
+  }
+  float mx = -INFINITY;
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[kb][r]);
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  float sum = 0.f;
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float e = __builtin_amdgcn_exp2f(s[kb][r] - mx);
+      s[kb][r] = e;
+      sum += e;
+    }
+  sum += __shfl_xor(sum, 32, 64);
+  const float rinv = 1.f / sum;
+
+  // O^T[dd][query] = sum_key V^T[dd][key] P^T[key][query]
+  floatx16 o;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) o[r] = 0.f;
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      uint2 a[3], b[3];
+      // unnormalised exp values (0, 1]; 1/sum is applied to O
+      sfx::split3(make_float4(s[kb][8 * st + 0], s[kb][8 * st + 1], s[kb][8 * st + 2], s[kb][8 * st + 3]), a);
+      sfx::split3(make_float4(s[kb][8 * st + 4], s[kb][8 * st + 5], s[kb][8 * st + 6], s[kb][8 * st + 7]), b);
+      bf16x8 pf[3], vf[3];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        pf[q] = __builtin_bit_cast(bf16x8, make_uint4(a[q].x, a[q].y, b[q].x, b[q].y));
+        uint4 vv = make_uint4(0, 0, 0, 0);  // dd = l32 >= D: zero rows of V^T
+        if (l32 < D) vv = *reinterpret_cast<const uint4*>(Vt + (q * D + l32) * VST + (2 * kb + st) * 16 + 8 * h);
+        vf[q] = __builtin_bit_cast(bf16x8, vv);
+      }
+#pragma unroll
+      for (int j = 0; j < 6; ++j) o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[QA[j]], pf[QB[j]], o, 0, 0, 0);
+    }
+
+#pragma unroll
+  for (int r = 0; r < 16; ++r) o[r] *= rinv;
   // scatter: query 32*wid + l32 (lane column), dd rows (r&3) + 8(r>>2) + 4h
   const int qi = 32 * wid + l32;
   const int qpos = key_start + qi;
@@ -408,12 +607,26 @@ int sfx_window_attention(int num_windows, int window, int heads, int head_dim, i
   SFX_REQUIRE(qkv && order && win && out, "sfx_window_attention: null buffer");
   dim3 grid(num_windows, heads);
   hipStream_t st = sfx::as_stream(stream);
-  if (head_dim == 16)
-    window_attn_kernel<16><<<grid, 256, 0, st>>>(qkv, order, win, window, channels, scale, out);
-  else if (head_dim == 24)
-    window_attn_kernel<24><<<grid, 256, 0, st>>>(qkv, order, win, window, channels, scale, out);
-  else
-    window_attn_kernel<32><<<grid, 256, 0, st>>>(qkv, order, win, window, channels, scale, out);
+  static int exact = -1;  // SFX_ATTN_PREC=fp32: the v_mfma_f32_32x32x2_f32 kernel
+  if (exact < 0) {
+    const char* e = getenv("SFX_ATTN_PREC");
+    exact = (e && e[0] == 'f') ? 1 : 0;
+  }
+  if (exact) {
+    if (head_dim == 16)
+      window_attn_kernel<16><<<grid, 256, 0, st>>>(qkv, order, win, window, channels, scale, out);
+    else if (head_dim == 24)
+      window_attn_kernel<24><<<grid, 256, 0, st>>>(qkv, order, win, window, channels, scale, out);
+    else
+      window_attn_kernel<32><<<grid, 256, 0, st>>>(qkv, order, win, window, channels, scale, out);
+  } else {
+    if (head_dim == 16)
+      window_attn_split_kernel<16><<<grid, 256, 0, st>>>(qkv, order, win, window, channels, scale, out);
+    else if (head_dim == 24)
+      window_attn_split_kernel<24><<<grid, 256, 0, st>>>(qkv, order, win, window, channels, scale, out);
+    else
+      window_attn_split_kernel<32><<<grid, 256, 0, st>>>(qkv, order, win, window, channels, scale, out);
+  }
   return sfx::check_launch("sfx_window_attention");
 }
 

@@ -34,6 +34,33 @@ inline int check_launch(const char* what) {
 
 inline unsigned ceil_div(long long a, long long b) { return (unsigned)((a + b - 1) / b); }
 
+// fp32 -> three bf16 terms by round-to-nearest (v_cvt_pk_bf16_f32): x = t0 + t1 + t2 + r with
+// |t1| <= 2^-8 |x|, |t2| <= 2^-16 |x|, |r| <= 2^-24 |x| (each residual x - t0, (x - t0) - t1 is exact in fp32);
+// bf16 keeps fp32's exponent range, so no scaling and no overflow cases.  The MFMA paths that run fp32
+// products as the six leading term products (t0t0, t0t1, t1t0, t0t2, t1t1, t2t0) on bf16 MFMA with fp32
+// accumulation (GEMM, window attention) are as accurate as fp32 arithmetic.
+typedef __bf16 sfx_bf16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float bf_lo(unsigned u) { return __builtin_bit_cast(float, u << 16); }
+__device__ __forceinline__ float bf_hi(unsigned u) { return __builtin_bit_cast(float, u & 0xffff0000u); }
+__device__ __forceinline__ unsigned pk_bf16(float a, float b) {
+  const sfx_bf16x2 v = __builtin_convertvector((float __attribute__((ext_vector_type(2)))){a, b}, sfx_bf16x2);
+  return __builtin_bit_cast(unsigned, v);
+}
+// 4 elements -> 3 terms x 4 packed bf16
+__device__ __forceinline__ void split3(float4 v, uint2 (&t)[3]) {
+  unsigned u0 = pk_bf16(v.x, v.y), u1 = pk_bf16(v.z, v.w);
+  t[0] = make_uint2(u0, u1);
+  float r0 = v.x - bf_lo(u0), r1 = v.y - bf_hi(u0), r2 = v.z - bf_lo(u1), r3 = v.w - bf_hi(u1);
+  u0 = pk_bf16(r0, r1);
+  u1 = pk_bf16(r2, r3);
+  t[1] = make_uint2(u0, u1);
+  r0 -= bf_lo(u0);
+  r1 -= bf_hi(u0);
+  r2 -= bf_lo(u1);
+  r3 -= bf_hi(u1);
+  t[2] = make_uint2(pk_bf16(r0, r1), pk_bf16(r2, r3));
+}
+
 // 64-lane wavefront helpers ------------------------------------------------
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 

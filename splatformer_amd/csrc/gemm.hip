@@ -32,7 +32,6 @@ namespace {
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 
 constexpr int BK = 32;
 constexpr int LDS_STRIDE = BK + 4;
@@ -134,28 +133,7 @@ __device__ __forceinline__ void bstore1(__amdgpu_buffer_rsrc_t r, unsigned off, 
   __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, off, 0, 0);
 }
 
-// fp32 -> three bf16 terms by round-to-nearest (v_cvt_pk_bf16_f32): x = t0 + t1 + t2 + r with
-// |t1| <= 2^-8 |x|, |t2| <= 2^-16 |x|, |r| <= 2^-24 |x| (each residual x - t0, (x - t0) - t1 is exact in fp32).
-// bf16 keeps fp32's exponent range, so no scaling and no overflow cases.  Out: 4 elements x 3 terms, packed.
-__device__ __forceinline__ float bf_lo(unsigned u) { return __builtin_bit_cast(float, u << 16); }
-__device__ __forceinline__ float bf_hi(unsigned u) { return __builtin_bit_cast(float, u & 0xffff0000u); }
-__device__ __forceinline__ unsigned pk_bf16(float a, float b) {
-  const bf16x2 v = __builtin_convertvector((float __attribute__((ext_vector_type(2)))){a, b}, bf16x2);
-  return __builtin_bit_cast(unsigned, v);
-}
-__device__ __forceinline__ void split3(float4 v, uint2 (&t)[3]) {
-  unsigned u0 = pk_bf16(v.x, v.y), u1 = pk_bf16(v.z, v.w);
-  t[0] = make_uint2(u0, u1);
-  float r0 = v.x - bf_lo(u0), r1 = v.y - bf_hi(u0), r2 = v.z - bf_lo(u1), r3 = v.w - bf_hi(u1);
-  u0 = pk_bf16(r0, r1);
-  u1 = pk_bf16(r2, r3);
-  t[1] = make_uint2(u0, u1);
-  r0 -= bf_lo(u0);
-  r1 -= bf_hi(u0);
-  r2 -= bf_lo(u1);
-  r3 -= bf_hi(u1);
-  t[2] = make_uint2(pk_bf16(r0, r1), pk_bf16(r2, r3));
-}
+using sfx::split3;  // fp32 -> three bf16 terms (common.h)
 
 // Persistent tile loop: each workgroup walks output tiles blockIdx.x, +gridDim.x, ... and prefetches
 // the first K-slab of its NEXT tile while it computes the last slab and runs the epilogue of the

@@ -12,7 +12,7 @@ n, C, H = (int(a) for a in sys.argv[1:4]) if len(sys.argv) > 3 else (37759, 256,
 reps = int(sys.argv[4]) if len(sys.argv) > 4 else 20
 dev = torch.device("cuda")
 qkv = torch.randn(n, 3 * C, device=dev)
-order = torch.randperm(n, device=dev).int()
+order = (torch.arange(n, device=dev) if os.environ.get("ATTN_ORDER") == "identity" else torch.randperm(n, device=dev)).int()
 K = min(n, 128)
 tab = ops.window_table([n], K)
 win = torch.tensor(tab, dtype=torch.int32, device=dev)

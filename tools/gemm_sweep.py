@@ -15,7 +15,18 @@ SHAPES = [(37759, 256, 256), (37759, 1024, 256), (37759, 256, 1024), (37759, 768
 
 def main():
     dev = torch.device("cuda")
-    tag = os.environ.get("SFX_GEMM_CFG", "auto") + "/" + os.environ.get("SFX_GEMM_PREC", "split")
+    if os.environ.get("SWEEP_CACHE_SPLIT") == "1":  # time the GEMM alone: split each A once
+        cache = {}
+        orig = ops.split_operand
+
+        def cached(x):
+            k = (x.data_ptr(), tuple(x.shape))
+            if k not in cache:
+                cache[k] = orig(x)
+            return cache[k]
+        ops.split_operand = cached
+    tag = os.environ.get("SFX_GEMM_CFG", "auto") + "/" + os.environ.get("SFX_GEMM_PREC", "split") + \
+        ("/cached" if os.environ.get("SWEEP_CACHE_SPLIT") == "1" else "")
     for M, N, K in SHAPES:
         x = torch.randn(M, K, device=dev)
         w = torch.randn(N, K, device=dev) / K ** 0.5
