@@ -33,6 +33,12 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA (no sparsity)
+# The GEMM computes fp32 products as six bf16 term products (3-term split, gemm.hip): its fp32-equivalent
+# ceiling is the dense bf16 peak / 6.
+SPLIT_PEAK_TFLOPS = round(BF16_MFMA_PEAK_TFLOPS / 6, 1)
+# rocprofv3 FETCH_SIZE / WRITE_SIZE passes over this bench (tools/traffic_summary.py), committed per round
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r01_traffic_splitgemm.json")
 HBM_PEAK_GBS = 8000.0
 
 
@@ -130,10 +136,22 @@ def roofline_probe(model, scene, reps=5):
         per.append((ms, kind, shape, fl))
     achieved = tot_fl / (tot_ms * 1e-3) / 1e12
     top = max(per)
+    traffic = None
+    try:  # measured HBM bytes of the same launches (PMC passes, per scene), see TRAFFIC_FILE
+        with open(TRAFFIC_FILE) as f:
+            traffic = json.load(f)["per_scene"]["gemm_kernel"]["hbm_B"]
+    except (OSError, KeyError, ValueError):
+        pass
     return {
-        "bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-        "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
-        "kernel": "gemm_kernel (sfx_linear / sfx_subm_conv, fp32 v_mfma_f32_32x32x2_f32), all launches of one scene",
+        "bound": "mfma", "achieved": round(achieved, 2), "peak": SPLIT_PEAK_TFLOPS, "unit": "TFLOP/s",
+        "frac": round(achieved / SPLIT_PEAK_TFLOPS, 4), "traffic": traffic,
+        "traffic_unit": "HBM bytes per scene (all GEMM launches; 2*FETCH_SIZE + WRITE_SIZE, " +
+                        os.path.relpath(TRAFFIC_FILE, ROOT) + ")",
+        "peak_basis": (f"fp32-equivalent ceiling of the 3-term bf16 split GEMM = dense bf16 MFMA {BF16_MFMA_PEAK_TFLOPS:.0f}"
+                       f" / 6 term products; exact-fp32 MFMA peak is {FP32_MFMA_PEAK_TFLOPS}"),
+        "frac_of_fp32_mfma_peak": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
+        "kernel": ("gemm_kernel (sfx_linear / sfx_subm_conv: fp32 operands split into 3 bf16 terms, "
+                   "6 x v_mfma_f32_32x32x16_bf16 per block, fp32 accumulation), all launches of one scene"),
         "launches": len(per), "gemm_ms_per_scene": round(tot_ms, 3),
         "algorithmic_gflop_per_scene": round(tot_fl / 1e9, 1),
         "top_launch": {"op": top[1], "M_N_K": list(top[2]), "avg_ms": round(top[0], 4),
