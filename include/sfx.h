@@ -120,6 +120,11 @@ int sfx_linear(int M, int N, int K, const float* A, long long lda, const int* ga
                long long group_stride_bias, long long group_stride_Y, const int* out_row_idx, const float* rowscale,
                int pre_before_act, void* stream);
 
+/* Tuning / test hook: force the GEMM tile configuration (index into gemm.hip kCfgs, -1 = cost model) and
+ * Stream-K (0 off, 1 on where legal, -1 = cost model) for every later sfx_linear / sfx_subm_conv call of the
+ * process.  Eight-wave configurations apply only to split (K >= 64) launches. */
+int sfx_gemm_force_config(int cfg, int stream_k);
+
 /* ---- training (configs C/D): backward of the nn.Linear layers -------------------------------------
  * dX[M,K] (=|+=) rowscale[m] * (dY[M,N] W[N,K]) * act'(dact_pre[m,k]) for k < dact_ncols (-1 = all);
  * Wt = W^T stored [K, N] (ldwt); dact: 0 none, 1 GELU(erf) on the pre-activation, 2 ReLU, 3 tanh given

@@ -339,6 +339,15 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs
   // are fetched BEFORE the next tile's prefetch is issued, so the epilogue never waits on the prefetch.
   float ebias[NB], escale[NB], eshift[NB];
   int mrow[MB][16];
+  auto load_mrow = [&](const Tile& ti, __amdgpu_buffer_rsrc_t rO) {
+#pragma unroll
+    for (int a = 0; a < MB; ++a)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int mt = ti.m0 + wm * WM + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        mrow[a][r] = bload1i(rO, mt < ti.M ? (unsigned)mt * 4u : OOB);
+      }
+  };
   auto pre_epilogue = [&](const Tile& ti) {
     // branch-free: absent operands read through an out-of-range offset (-> 0) and are then selected away
     const __amdgpu_buffer_rsrc_t rB = rsrc(bias ? bias : p.W);
@@ -356,20 +365,16 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs
       escale[b] = sv;  // raw loads; the defaults for absent operands are selected in the epilogue, so
       eshift[b] = hv;  // nothing here waits on them
     }
-    const bool remap = ti.out_rows != nullptr;
-    if (remap) {
-#pragma unroll
-      for (int a = 0; a < MB; ++a)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int mt = ti.m0 + wm * WM + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-          mrow[a][r] = bload1i(rO, mt < ti.M ? (unsigned)mt * 4u : OOB);
-        }
-    }
+    // output-row remaps (pair mode's pair_out; an out_rows argument of the other modes) are loaded in the
+    // epilogue, keeping 16 * MB registers free across the MFMAs
+    (void)rO;
   };
   // output row of accumulator row r of block a (-1: outside the tile)
   auto resolve_rows = [&](const Tile& ti) {
     const bool remap = ti.out_rows != nullptr;
+    if constexpr (MODE != MODE_PAIR) {
+      if (remap) load_mrow(ti, rsrc(ti.out_rows));
+    }
 #pragma unroll
     for (int a = 0; a < MB; ++a)
 #pragma unroll
@@ -481,23 +486,31 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs
         return;
       }
     }
-    resolve_rows(ti);
     if constexpr (MODE == MODE_PAIR) {  // partial sums of one neighbour offset: accumulate into the output rows
+      const __amdgpu_buffer_rsrc_t rO = rsrc(ti.out_rows);
 #pragma unroll
-      for (int a = 0; a < MB; ++a)
+      for (int a = 0; a < MB; ++a) {
+        int orow[16];
+        bool ok[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int mt = ti.m0 + wm * WM + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          ok[r] = mt < ti.M;
+          orow[r] = bload1i(rO, ok[r] ? (unsigned)mt * 4u : OOB);
+        }
 #pragma unroll
         for (int b = 0; b < NB; ++b) {
           const int n = ti.n0 + wn * WN + b * 32 + l32;
           const bool nok = n < p.N;
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int m = mrow[a][r];
+          for (int r = 0; r < 16; ++r)
             __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(
-                acc[a][b][r], rY, (nok && m >= 0) ? ((unsigned)m * ldy32 + (unsigned)n) * 4u : OOB, 0, 0);
-          }
+                acc[a][b][r], rY, (nok && ok[r]) ? ((unsigned)orow[r] * ldy32 + (unsigned)n) * 4u : OOB, 0, 0);
         }
+      }
       return;
     }
+    resolve_rows(ti);
 #pragma unroll
     for (int a = 0; a < MB; ++a) {
 #pragma unroll
@@ -818,18 +831,24 @@ bool use_split(int K) {
   return min_k >= 0 && K >= min_k;
 }
 
+// tuning / test hooks: SFX_GEMM_CFG=<index into kCfgs>, SFX_GEMM_SK=0|1, or sfx_gemm_force_config()
+int forced = -2, forced_sk = -2;
+void read_force_env() {
+  if (forced != -2) return;
+  const char* e = getenv("SFX_GEMM_CFG");
+  forced = (e && *e) ? atoi(e) : -1;
+  if (forced >= kNumCfgs) forced = -1;
+  const char* k = getenv("SFX_GEMM_SK");
+  forced_sk = (k && *k) ? atoi(k) : -1;
+}
+
 // -> configuration index; sets a.sk when the Stream-K split of the same tile shape is cheaper.
 int pick_cfg(GemmArgs& a, int groups, bool vec) {
-  static int forced = -2, forced_sk = -2;
-  if (forced == -2) {  // tuning hooks: SFX_GEMM_CFG=<index into kCfgs>, SFX_GEMM_SK=0|1
-    const char* e = getenv("SFX_GEMM_CFG");
-    forced = (e && *e) ? atoi(e) : -1;
-    if (forced >= kNumCfgs) forced = -1;
-    const char* k = getenv("SFX_GEMM_SK");
-    forced_sk = (k && *k) ? atoi(k) : -1;
-  }
+  read_force_env();
   const int nk = (int)sfx::ceil_div(a.K, BK);
   const bool split = vec && use_split(a.K);
+  // eight-wave tiles exist only with split operands
+  const int force = (forced >= 0 && !(kCfgs[forced].nw == 8 && !split)) ? forced : -1;
   // Stream-K needs a linear epilogue that can be split into atomically added pieces
   // (measured: the memset + atomic partial epilogues only pay off on long K; pair mode needs no memset)
   const bool sk_ok = groups == 1 && nk >= (a.pair_mode ? 8 : 16) && a.act == ACT_NONE && !a.Ypre && !a.out_rows &&
@@ -839,7 +858,7 @@ int pick_cfg(GemmArgs& a, int groups, bool vec) {
   bool best_sk = false;
   double best_cost = 1e300;
   for (int c = 0; c < kNumCfgs; ++c) {
-    if (forced >= 0 && c != forced) continue;
+    if (force >= 0 && c != force) continue;
     if (kCfgs[c].nw == 8 && !split) continue;
     const long long slots = (kCfgs[c].nw == 4 ? 2ll : 1ll) * num_cus() / groups;
     // tile area per unit of CU throughput (an eight-wave tile has the whole CU, a four-wave one half)
@@ -1009,6 +1028,14 @@ __global__ void centre_pairs_kernel(int n, const int* __restrict__ nbr, int* __r
 extern "C" {
 
 // See include/sfx.h for the contract.
+int sfx_gemm_force_config(int cfg, int stream_k) {
+  SFX_REQUIRE(cfg >= -1 && cfg < kNumCfgs && stream_k >= -1 && stream_k <= 1, "sfx_gemm_force_config: bad values");
+  read_force_env();  // so the environment defaults are not applied over the hook later
+  forced = cfg;
+  forced_sk = stream_k;
+  return SFX_OK;
+}
+
 int sfx_linear(int M, int N, int K, const float* A, long long lda, const int* gather_idx, int num_segments,
                const float* W, long long ldw, const float* bias, const float* scale, const float* shift, int act,
                int act_ncols, const float* R, long long ldr, const int* residual_idx, float* Y, long long ldy,

@@ -34,8 +34,16 @@ _lib.register("sfx_subm_pairs", [I, P, P, Z, P, P, P, P])
 _lib.register("sfx_subm_conv", [I, I, I, P, L, P, P, P, P, P, P, P, L, P])
 _lib.register("sfx_gs_pack", [I, P, L, P, L, P, L, P, L, P, L, P, L, I, F, P, L, P, P, P])
 _lib.register("sfx_offsets_to_batch", [I, I, P, P, P])
+_lib.register("sfx_gemm_force_config", [I, I])
 
 ACT_NONE, ACT_GELU, ACT_RELU, ACT_TANH = 0, 1, 2, 3
+# gemm.hip kCfgs: 128x128, 128x96, 128x64, 64x128, 64x64 (4 waves, 2 per CU), 256x128, 128x256 (8 waves)
+GEMM_NUM_CONFIGS = 7
+
+
+def gemm_force_config(cfg: int = -1, stream_k: int = -1) -> None:
+    """Tuning / test hook: force the GEMM tile configuration and Stream-K choice (-1 = cost model)."""
+    call("sfx_gemm_force_config", cfg, stream_k)
 ORDER_TYPES = {"z": 0, "z-trans": 1, "hilbert": 2, "hilbert-trans": 3}
 
 

@@ -223,3 +223,38 @@ def test_backbone_feature_l2(device):
     p = model.backbone(dd, perms=perms)
     ref = ptv3_ref.ptv3_forward(sd, cfg, data, perms, prefix="backbone.backbone.")
     assert rel_l2(p.feat.cpu(), ref.feat) < 1e-5
+
+
+@pytest.mark.parametrize("cfg", list(range(ops.GEMM_NUM_CONFIGS)))
+def test_gemm_every_tile_config(device, cfg):
+    """Every tile configuration (incl. the eight-wave ping-pong tiles) and Stream-K on/off, for dense,
+    gathered (one segment) and offset-major pair (SubM conv) launches, against fp64 products."""
+    g = torch.Generator().manual_seed(cfg)
+    n, C = 6000, 96
+    s = make_scene(n, 1, seed=5, unique_voxels=True)
+    grid = torch.floor(s["means"] * 384).int()
+    nbr_ref = ptv3_ref.subm_neighbors(grid, torch.zeros(grid.shape[0], dtype=torch.int64))
+    smap = ops.subm_neighbors(grid.to(device), None)
+    try:
+        for sk in (0, 1):
+            ops.gemm_force_config(cfg, sk)
+            for (M, N, K) in [(3001, 200, 64), (2500, 136, 544), (777, 520, 1024)]:
+                x = torch.randn(M, K, generator=g)
+                w = torch.randn(N, K, generator=g) / K ** 0.5
+                b = torch.randn(N, generator=g)
+                res = torch.randn(M, N, generator=g)
+                ref = x.double() @ w.double().T + b.double() + res.double()
+                y = ops.linear(x.to(device), w.to(device), b.to(device), residual=res.to(device))
+                assert rel_l2(y.cpu(), ref) < 2e-6, (cfg, sk, M, N, K)
+                yg = torch.nn.functional.gelu(x @ w.T + b)
+                y2 = ops.linear(x.to(device), w.to(device), b.to(device), act=ops.ACT_GELU)
+                assert rel_l2(y2.cpu(), yg) < 2e-6, (cfg, sk, M, N, K, "gelu")
+            for cin in (C, 256):
+                xx = torch.randn(grid.shape[0], cin, generator=g)
+                ww = torch.randn(cin, 3, 3, 3, cin, generator=g) * 0.05
+                bb = torch.randn(cin, generator=g)
+                ref2 = ptv3_ref.subm_conv(xx, nbr_ref, ww, bb)
+                y3 = ops.subm_conv(xx.to(device), smap, ww.to(device), bb.to(device))
+                assert rel_l2(y3.cpu(), ref2) < 2e-6, (cfg, sk, cin, "conv")
+    finally:
+        ops.gemm_force_config(-1, -1)
