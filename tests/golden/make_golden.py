@@ -17,8 +17,14 @@ SURVEY.md §8(c).  We then run:
    outputs for a fixed backbone feature pin batchify / grid_coord / heads /
    residual / tanh semantics.
 
-Outputs: tests/golden/render_glue.npz, tests/golden/feature_predictor.npz
-(inputs and outputs only -- data, no reference source).
+3. `dataset/GS.py:SplatfactoDataset` scene loading (load_gs_params_fromnerfstudio,
+   load_images_cameras_fromnerfstudio, load_scene, read_image) on a synthetic
+   nerfstudio/colmap directory written here (NaN rows, inf scales, outliers,
+   more than max_gs_num Gaussians, elevation-named OOD test views, an RGBA
+   image): pins splatformer_amd/scene_io.py.
+
+Outputs: tests/golden/render_glue.npz, tests/golden/feature_predictor.npz,
+tests/golden/scene_io.npz (inputs and outputs only -- data, no reference source).
 """
 from __future__ import annotations
 
@@ -43,6 +49,7 @@ def install_stubs(recorder):
 
     gin.configurable = configurable
     gin.external_configurable = lambda *a, **k: a[0]
+    gin.query_parameter = lambda name: recorder.get("gin", {}).get(name)
     sys.modules["gin"] = gin
     for m in ["cv2", "torch_scatter"]:
         sys.modules[m] = types.ModuleType(m)
@@ -191,7 +198,82 @@ def main():
         fo["out_" + k] = v.numpy()
     np.savez_compressed(os.path.join(OUT, "feature_predictor.npz"), **fo)
     torch.tensor = orig_tensor
-    print("wrote", sorted(out)[:4], "...", len(out), "render arrays;", len(fo), "feature-predictor arrays")
+    so = scene_io_golden(rec)
+    print("wrote", sorted(out)[:4], "...", len(out), "render arrays;", len(fo), "feature-predictor arrays;",
+          len(so), "scene-io arrays")
+
+
+def make_scene_dirs(root, n=1200, seed=3):
+    """Synthetic nerfstudio + colmap folders (our own files) for the scene-loading goldens."""
+    import pickle
+    from PIL import Image
+    g = torch.Generator().manual_seed(seed)
+    ns = os.path.join(root, "scene0", "splatfacto")
+    os.makedirs(os.path.join(ns, "nerfstudio_models"), exist_ok=True)
+    means = torch.randn(n, 3, generator=g) * torch.tensor([2.0, 1.0, 0.5]) + torch.tensor([0.3, -1.0, 2.0])
+    means[7] = torch.tensor([40.0, 0.0, 0.0])            # outliers
+    means[8] = torch.tensor([0.0, -35.0, 0.0])
+    params = {"means": means, "scales": torch.randn(n, 3, generator=g) - 4.0,
+              "quats": torch.randn(n, 4, generator=g), "opacities": torch.randn(n, 1, generator=g),
+              "features_dc": torch.randn(n, 3, generator=g), "features_rest": torch.randn(n, 3, 3, generator=g) * 0.1}
+    params["means"][11, 1] = float("nan")                # NaN rows in three attributes
+    params["features_rest"][12, 2, 0] = float("nan")
+    params["quats"][13, 3] = float("nan")
+    params["scales"][14, 0] = float("-inf")             # inf after the log-scale shift
+    ck = {"_model.gauss_params." + k: v for k, v in params.items()}
+    ck["step"] = 29999
+    torch.save(ck, os.path.join(ns, "nerfstudio_models", "step-000029999.ckpt"))
+    c2w = lambda m: torch.cat([torch.linalg.qr(torch.randn(m, 3, 3, generator=g))[0],
+                               torch.randn(m, 3, 1, generator=g) * 3], 2)
+    meta = {"train_camera_to_worlds": c2w(5), "test_camera_to_worlds": c2w(12),
+            "fx": torch.tensor(711.1), "fy": torch.tensor(711.1), "cx": torch.tensor(400.0),
+            "cy": torch.tensor(400.0), "width": torch.tensor(800), "height": torch.tensor(800)}
+    with open(os.path.join(ns, "camera_for-3d-denoise.pkl"), "wb") as f:
+        pickle.dump(meta, f)
+    cm = os.path.join(root, "colmap", "scene0")
+    os.makedirs(os.path.join(cm, "images"), exist_ok=True)
+    names = [f"frame_{i:03d}.png" for i in range(5)]
+    names += [f"elevation{e}_azimuth{a}.png" for e in (30, 70, 80, 90) for a in (0, 120, 240)]
+    for nm in names:
+        open(os.path.join(cm, "images", nm), "wb").close()
+    rgba = (torch.rand(6, 5, 4, generator=g) * 255).to(torch.uint8).numpy()
+    img = os.path.join(root, "rgba.png")
+    Image.fromarray(rgba, "RGBA").save(img)
+    return ns, cm, params, meta, img
+
+
+def scene_io_golden(rec):
+    import importlib
+    import tempfile
+    GS = importlib.import_module("dataset.GS")
+    so = {}
+    with tempfile.TemporaryDirectory() as root:
+        ns, cm, params, meta, img = make_scene_dirs(root)
+        for k, v in params.items():
+            so["in_" + k] = v.numpy()
+        for k, v in meta.items():
+            so["in_meta_" + k] = v.numpy()
+        so["in_rgba"] = np.array(__import__("PIL.Image", fromlist=["Image"]).open(img))
+        feats = ["means", "scales", "opacities", "quats", "features_dc", "features_rest"]
+        rec["gin"] = {"FeaturePredictor.input_features": feats, "training.pretrain_steps": 0}
+        for nd in (0, 3):
+            ds = GS.SplatfactoDataset.__new__(GS.SplatfactoDataset)
+            ds.remove_outlier_ndevs, ds.max_gs_num, ds.train_or_test = nd, 1000, "test"
+            ds.folders, ds.load_pose_src = [(ns, cm)], "nerfstudio"
+            scene = ds.load_scene(0)
+            p = f"nd{nd}_"
+            for k, v in scene["gs_params"].items():
+                so[p + k] = v.numpy()
+            so[p + "test_c2w"] = scene["meta"]["test_camera_to_worlds"].numpy()
+            so[p + "train_c2w"] = scene["meta"]["train_camera_to_worlds"].numpy()
+            so[p + "test_names"] = np.array([os.path.basename(x) for x in scene["test_imgs_path"]])
+            so[p + "train_names"] = np.array([os.path.basename(x) for x in scene["train_imgs_path"]])
+        ds = GS.SplatfactoDataset.__new__(GS.SplatfactoDataset)
+        bg = torch.tensor([0.25, 0.5, 1.0])
+        so["rgba_bg"] = bg.numpy()
+        so["rgba_out"] = ds.read_image(img, background=bg).numpy()
+    np.savez_compressed(os.path.join(OUT, "scene_io.npz"), **so)
+    return so
 
 
 if __name__ == "__main__":
