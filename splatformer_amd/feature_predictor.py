@@ -92,7 +92,7 @@ class FeaturePredictor(nn.Module):
                 m[-1].weight.data.zero_()
                 m[-1].bias.data.zero_()
         if resume_ckpt is not None:
-            self.load_state_dict(torch.load(resume_ckpt, map_location="cpu", weights_only=True))
+            load_checkpoint(self, resume_ckpt)
         self._pack_cache = None
 
     # ---- packed head weights (rebuilt only when a parameter changes) --------------
@@ -179,3 +179,37 @@ class FeaturePredictor(nn.Module):
             outs.append(o)
         assert len(outs) == 1, "Now only support batch size 1"
         return outs
+
+
+def convert_state_dict(sd: Dict[str, Tensor], target: Dict[str, Tensor]) -> Dict[str, Tensor]:
+    """A checkpoint of the reference FeaturePredictor (train.py:344 saves `model.module.state_dict()` after the
+    SyncBatchNorm conversion of train.py:404) -> this module's state dict.
+
+    * a DDP `module.` prefix is stripped (checkpoints saved without `.module`);
+    * SyncBatchNorm and BatchNorm1d share their keys (weight, bias, running_mean, running_var,
+      num_batches_tracked) -- nothing to convert;
+    * SubMConv3d weights: spconv 2.x stores [Cout, 3, 3, 3, Cin] (this layout); an spconv 1.x checkpoint's
+      [3, 3, 3, Cin, Cout] is permuted to it.  (Which (x, y, z) neighbour each of the 27 kernel taps reads
+      follows Pointcept's spconv call; the tap order itself is parity unpinned)
+    """
+    if sd and all(k.startswith("module.") for k in sd):
+        sd = {k[len("module."):]: v for k, v in sd.items()}
+    out = {}
+    for k, v in sd.items():
+        t = target.get(k)
+        if t is not None and v.dim() == 5 and tuple(v.shape) != tuple(t.shape):
+            if tuple(v.permute(4, 0, 1, 2, 3).shape) == tuple(t.shape):
+                v = v.permute(4, 0, 1, 2, 3).contiguous()
+        out[k] = v
+    return out
+
+
+def load_checkpoint(model: nn.Module, ckpt, strict: bool = True):
+    """Load a reference checkpoint (path or state dict; `torch.load(weights_only=True)`, never unpickling
+    arbitrary objects) into `model` through convert_state_dict.  Cached derived weights (folded CPE convs,
+    packed heads) are keyed on the parameters' versions, so they are rebuilt on the next forward."""
+    sd = torch.load(ckpt, map_location="cpu", weights_only=True) if isinstance(ckpt, (str, bytes)) else ckpt
+    if isinstance(sd, dict) and "state_dict" in sd and isinstance(sd["state_dict"], dict):
+        sd = sd["state_dict"]
+    return model.load_state_dict(convert_state_dict(sd, model.state_dict()), strict=strict)
+
