@@ -280,6 +280,14 @@ int sfx_rasterize_fwd_views(int views, int tiles_x, int tiles_y, int block_width
  * Images are [num_images, elems_per_image] contiguous f32. */
 int sfx_image_stats_u8(int num_images, long long elems_per_image, const float* pred, const float* gt,
                        int clamp_pred, unsigned long long* sums, int* maxes, void* stream);
+/* SSIM per image (utils/metrics.py:93-135: 11x11 Gaussian window sigma 1.5, zero padding, C1 = 0.01^2,
+ * C2 = 0.03^2, mean of the SSIM map over channels and pixels).  img1/img2: [num_images][height][width][channels]
+ * fp32 (HWC, as rendered); window: the 121 fp32 taps of the reference's 2-D window (row-major); out: [num_images].
+ * quantize_u8 = 1 evaluates the uint8 images the evaluation loop scores ((x*255) truncated, img1 clamped to <= 1,
+ * then /255: train.py:104-113, metrics.py:26-29); 0 uses the values as given. */
+size_t sfx_ssim_workspace_bytes(int num_images, int height, int width, int channels);
+int sfx_ssim(int num_images, int height, int width, int channels, const float* img1, const float* img2,
+             const float* window, int quantize_u8, float* out, void* ws, size_t ws_bytes, void* stream);
 
 #ifdef __cplusplus
 }

@@ -59,9 +59,110 @@ __global__ void __launch_bounds__(kThreads) image_stats_kernel(long long elems, 
   }
 }
 
+// ---- SSIM (reference utils/metrics.py:93-135, window 11, sigma 1.5, zero padding 5) ------------------------
+// One workgroup per 16x16 output tile of one channel of one image: the 26x26 halo of both images staged in
+// LDS (zero outside the image = conv2d's padding), each lane forms the five windowed moments of its pixel with
+// the 121-tap window (the reference's 2-D window, outer product of the normalised 1-D Gaussian in fp32), the
+// SSIM map value, and the workgroup sum goes to a per-(image, tile) partial; a second kernel reduces the
+// partials of each image in a fixed order (deterministic) and divides by C*H*W.
+constexpr int SS_T = 16, SS_R = 5, SS_W = 11, SS_S = SS_T + 2 * SS_R;
+
+__global__ void __launch_bounds__(SS_T * SS_T) ssim_tile_kernel(int H, int W, int C, const float* __restrict__ a,
+                                                                const float* __restrict__ b,
+                                                                const float* __restrict__ win, int quant,
+                                                                float* __restrict__ partial) {
+  __shared__ float sa[SS_S][SS_S + 1], sb[SS_S][SS_S + 1], sw[SS_W * SS_W];
+  __shared__ float red[SS_T * SS_T / 64];
+  const int img = blockIdx.z / C, c = blockIdx.z % C;
+  const int x0 = blockIdx.x * SS_T - SS_R, y0 = blockIdx.y * SS_T - SS_R;
+  const long long base = (long long)img * H * W * C;
+  for (int i = threadIdx.x; i < SS_S * SS_S; i += SS_T * SS_T) {
+    const int yy = i / SS_S, xx = i % SS_S;
+    const int y = y0 + yy, x = x0 + xx;
+    const bool in = y >= 0 && y < H && x >= 0 && x < W;
+    const long long o = base + ((long long)y * W + x) * C + c;
+    float va = in ? a[o] : 0.f, vb = in ? b[o] : 0.f;
+    if (quant) {  // the evaluation's uint8 images, /255 (train.py:104-113, metrics.py:26-29)
+      va = (float)quant_u8(va, true) / 255.f;
+      vb = (float)quant_u8(vb, false) / 255.f;
+    }
+    sa[yy][xx] = va;
+    sb[yy][xx] = vb;
+  }
+  if (threadIdx.x < SS_W * SS_W) sw[threadIdx.x] = win[threadIdx.x];
+  __syncthreads();
+  const int tx = threadIdx.x % SS_T, ty = threadIdx.x / SS_T;
+  float m1 = 0.f, m2 = 0.f, s11 = 0.f, s22 = 0.f, s12 = 0.f;
+  for (int i = 0; i < SS_W; ++i)
+#pragma unroll
+    for (int j = 0; j < SS_W; ++j) {
+      const float w = sw[i * SS_W + j], p = sa[ty + i][tx + j], q = sb[ty + i][tx + j];
+      m1 = fmaf(w, p, m1);
+      m2 = fmaf(w, q, m2);
+      s11 = fmaf(w, p * p, s11);
+      s22 = fmaf(w, q * q, s22);
+      s12 = fmaf(w, p * q, s12);
+    }
+  const float C1 = 0.01f * 0.01f, C2 = 0.03f * 0.03f;
+  const float mu11 = m1 * m1, mu22 = m2 * m2, mu12 = m1 * m2;
+  const float v = ((2.f * mu12 + C1) * (2.f * (s12 - mu12) + C2)) /
+                  ((mu11 + mu22 + C1) * ((s11 - mu11) + (s22 - mu22) + C2));
+  const int x = blockIdx.x * SS_T + tx, y = blockIdx.y * SS_T + ty;
+  float t = (x < W && y < H) ? v : 0.f;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) t += __shfl_xor(t, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = t;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float s = 0.f;
+    for (int w = 0; w < SS_T * SS_T / 64; ++w) s += red[w];
+    const int tiles = gridDim.x * gridDim.y;
+    partial[((long long)img * C + c) * tiles + blockIdx.y * gridDim.x + blockIdx.x] = s;
+  }
+}
+
+__global__ void __launch_bounds__(256) ssim_reduce_kernel(int per_image, double denom,
+                                                          const float* __restrict__ partial,
+                                                          float* __restrict__ out) {
+  __shared__ double red[256];
+  double s = 0.0;
+  for (int i = threadIdx.x; i < per_image; i += 256) s += partial[(long long)blockIdx.x * per_image + i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o >= 1; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[blockIdx.x] = (float)(red[0] / denom);
+}
+
 }  // namespace
 
 extern "C" {
+
+size_t sfx_ssim_workspace_bytes(int num_images, int height, int width, int channels) {
+  const long long tiles = (long long)sfx::ceil_div(width, SS_T) * sfx::ceil_div(height, SS_T);
+  return sizeof(float) * (size_t)((long long)num_images * channels * tiles + SS_W * SS_W);
+}
+
+int sfx_ssim(int num_images, int height, int width, int channels, const float* img1, const float* img2,
+             const float* window, int quantize_u8, float* out, void* ws, size_t ws_bytes, void* stream) {
+  sfx::clear_error();
+  SFX_REQUIRE(num_images >= 0 && height > 0 && width > 0 && channels > 0, "sfx_ssim: bad sizes");
+  if (num_images == 0) return SFX_OK;
+  SFX_REQUIRE(img1 && img2 && window && out && ws, "sfx_ssim: null buffer");
+  SFX_REQUIRE(ws_bytes >= sfx_ssim_workspace_bytes(num_images, height, width, channels),
+              "sfx_ssim: workspace too small");
+  SFX_REQUIRE((long long)num_images * channels <= 65535, "sfx_ssim: at most 65535 image-channels per call");
+  hipStream_t st = sfx::as_stream(stream);
+  float* partial = reinterpret_cast<float*>(ws);
+  const int tx = (int)sfx::ceil_div(width, SS_T), ty = (int)sfx::ceil_div(height, SS_T);
+  ssim_tile_kernel<<<dim3(tx, ty, num_images * channels), SS_T * SS_T, 0, st>>>(height, width, channels, img1, img2,
+                                                                               window, quantize_u8, partial);
+  ssim_reduce_kernel<<<num_images, 256, 0, st>>>(channels * tx * ty, (double)channels * height * width, partial,
+                                                 out);
+  return sfx::check_launch("sfx_ssim");
+}
 
 int sfx_image_stats_u8(int num_images, long long elems_per_image, const float* pred, const float* gt,
                        int clamp_pred, unsigned long long* sums, int* maxes, void* stream) {

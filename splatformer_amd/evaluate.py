@@ -3,8 +3,8 @@
 For each scene of this rank's chunk (dataset/GS.py:54-67): refine with the FeaturePredictor (one scene
 per forward, feature_predictor.py:244), render the V test views of the refined Gaussians
 (gs_utils.rasterize_gaussians_to_multiimgs), quantise prediction and target to uint8 and accumulate the
-per-image PSNR sum (train.py:104-131, utils/metrics.py); finally reduce to rank 0 (train.py:170-176).
-SSIM / LPIPS (metrics.py:103-135, VGG weights) are out of this round's scope.
+per-image PSNR and SSIM sums (train.py:104-131, utils/metrics.py); finally reduce to rank 0
+(train.py:170-176).  LPIPS (VGG weights, unavailable offline) is out of scope.
 """
 from __future__ import annotations
 
@@ -14,7 +14,7 @@ import torch
 
 from . import dist
 from .gs_render import rasterize_gaussians_to_multiimgs
-from .metrics import image_stats_u8, psnr_from_stats
+from .metrics import image_stats_u8, psnr_from_stats, ssim
 
 
 @torch.no_grad()
@@ -29,6 +29,7 @@ def evaluate_scenes(model, scenes: Sequence[dict], cameras: Sequence[dict],
     rank, ws = dist.world()
     mine = dist.scene_chunk(len(scenes), rank, ws)
     psnr_sum = torch.zeros((), dtype=torch.float64)
+    ssim_sum = torch.zeros((), dtype=torch.float64)
     num_images = 0
     for i in mine:
         gs = scenes[i] if evaluate_input else model([scenes[i]], [i])[0]
@@ -38,6 +39,7 @@ def evaluate_scenes(model, scenes: Sequence[dict], cameras: Sequence[dict],
         sums, maxes = image_stats_u8(pred, gt, clamp_pred=False)  # rgbs are already clamped (gs_utils.py:111)
         psnr = psnr_from_stats(sums, maxes, pred[0].numel())
         psnr_sum += psnr.sum()
+        ssim_sum += ssim(pred, gt, quantize_u8=True).double().sum().cpu()
         num_images += pred.shape[0]
-    return dist.reduce_metrics({"psnr": psnr_sum}, num_images, len(mine),
+    return dist.reduce_metrics({"psnr": psnr_sum, "ssim": ssim_sum}, num_images, len(mine),
                                device=device if ws > 1 and device.type == "cuda" else None)

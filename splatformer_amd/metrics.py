@@ -1,4 +1,4 @@
-"""Evaluation metrics on device: uint8-quantised PSNR (reference utils/metrics.py + train.py:104-113).
+"""Evaluation metrics on device: uint8-quantised PSNR and SSIM (reference utils/metrics.py + train.py:104-113).
 
 `psnr_u8(pred, gt)` mirrors the reference evaluation contract for synthetic (3-channel) targets:
 - train.py:104-113: `gt = (gt*255).to(uint8)`, `pred = (pred*255).to(uint8)` (truncation), pred having
@@ -16,10 +16,14 @@ from __future__ import annotations
 
 import torch
 
+import math
+
 from . import _lib
-from ._lib import I, L, P, call, ptr, stream
+from ._lib import I, L, P, Z, call, ptr, stream
 
 _lib.register("sfx_image_stats_u8", [I, L, P, P, I, P, P, P])
+_lib.register("sfx_ssim_workspace_bytes", [I, I, I, I], Z)
+_lib.register("sfx_ssim", [I, I, I, I, P, P, P, I, P, P, Z, P])
 
 
 def image_stats_u8(pred: torch.Tensor, gt: torch.Tensor, clamp_pred: bool = True):
@@ -53,4 +57,39 @@ def psnr_u8(pred: torch.Tensor, gt: torch.Tensor, clamp_pred: bool = True) -> to
     """[V,H,W,3] prediction and target in [0,1] -> per-image PSNR [V] (float64, on the host)."""
     sums, maxes = image_stats_u8(pred, gt, clamp_pred)
     return psnr_from_stats(sums, maxes, pred.numel() // max(pred.shape[0], 1))
+
+
+def ssim_window(window_size: int = 11, sigma: float = 1.5) -> torch.Tensor:
+    """The reference's 2-D window (metrics.py:93-101): normalised 1-D Gaussian (fp32), outer product."""
+    g = torch.tensor([math.exp(-(x - window_size // 2) ** 2 / float(2 * sigma ** 2)) for x in range(window_size)],
+                     dtype=torch.float32)
+    g = (g / g.sum()).unsqueeze(1)
+    return g.mm(g.t()).float()
+
+
+_WIN = {}
+
+
+def ssim(img1: torch.Tensor, img2: torch.Tensor, quantize_u8: bool = False) -> torch.Tensor:
+    """[V,H,W,C] images (HWC) -> SSIM per image [V] (float32 on the device), = MetricComputer's
+    `ssim(x.permute(0,3,1,2), ..., window_size=11, size_average=False)` (metrics.py:15, :103-135).
+    quantize_u8: score the uint8 images of the evaluation loop (truncation, img1 clamped to <= 1, /255) --
+    the batch-max rule of metrics.py:26-29 is taken as dividing (it differs only for images whose largest
+    uint8 value is <= 1)."""
+    _lib.require_gpu(img1)
+    if img1.shape != img2.shape or img1.dim() != 4:
+        raise ValueError(f"ssim: expected two equal [V,H,W,C] tensors, got {tuple(img1.shape)}, {tuple(img2.shape)}")
+    V, H, W, C = img1.shape
+    a = img1.float().contiguous()
+    b = img2.float().contiguous()
+    dev = a.device
+    win = _WIN.get(dev)
+    if win is None:
+        win = _WIN[dev] = ssim_window().reshape(-1).to(dev)
+    nbytes = _lib.fn("sfx_ssim_workspace_bytes")(V, H, W, C)
+    ws = torch.empty(max(int(nbytes), 4), dtype=torch.uint8, device=dev)
+    out = torch.empty(V, dtype=torch.float32, device=dev)
+    call("sfx_ssim", V, H, W, C, ptr(a), ptr(b), ptr(win), 1 if quantize_u8 else 0, ptr(out), ptr(ws), ws.numel(),
+         stream())
+    return out
 

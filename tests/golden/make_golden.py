@@ -24,7 +24,10 @@ SURVEY.md §8(c).  We then run:
    image): pins splatformer_amd/scene_io.py.
 
 Outputs: tests/golden/render_glue.npz, tests/golden/feature_predictor.npz,
-tests/golden/scene_io.npz (inputs and outputs only -- data, no reference source).
+tests/golden/scene_io.npz, tests/golden/metrics.npz (inputs and outputs only -- data, no reference source).
+
+4. `utils/metrics.py` psnr / ssim (lpips stubbed: its VGG weights are not available offline) on seeded image
+   batches: pins oracle/metrics_ref.py and the SSIM kernel.
 """
 from __future__ import annotations
 
@@ -51,7 +54,7 @@ def install_stubs(recorder):
     gin.external_configurable = lambda *a, **k: a[0]
     gin.query_parameter = lambda name: recorder.get("gin", {}).get(name)
     sys.modules["gin"] = gin
-    for m in ["cv2", "torch_scatter"]:
+    for m in ["cv2", "torch_scatter", "lpips"]:
         sys.modules[m] = types.ModuleType(m)
     ply = types.ModuleType("plyfile")
     ply.PlyData = object
@@ -199,8 +202,24 @@ def main():
     np.savez_compressed(os.path.join(OUT, "feature_predictor.npz"), **fo)
     torch.tensor = orig_tensor
     so = scene_io_golden(rec)
+    mo = metrics_golden()
     print("wrote", sorted(out)[:4], "...", len(out), "render arrays;", len(fo), "feature-predictor arrays;",
-          len(so), "scene-io arrays")
+          len(so), "scene-io arrays;", len(mo), "metrics arrays")
+
+
+def metrics_golden():
+    import importlib
+    metrics = importlib.import_module("utils.metrics")
+    g = torch.Generator().manual_seed(21)
+    mo = {}
+    for i, (n, h, w) in enumerate([(2, 40, 36), (3, 23, 17)]):
+        a = torch.rand(n, 3, h, w, generator=g)
+        b = (a + 0.1 * torch.randn(n, 3, h, w, generator=g)).clamp(0, 1)
+        mo[f"b{i}_img1"], mo[f"b{i}_img2"] = a.numpy(), b.numpy()
+        mo[f"b{i}_ssim"] = metrics.ssim(a, b, window_size=11, size_average=False).numpy()
+        mo[f"b{i}_psnr"] = metrics.psnr(a, b).numpy()
+    np.savez_compressed(os.path.join(OUT, "metrics.npz"), **mo)
+    return mo
 
 
 def make_scene_dirs(root, n=1200, seed=3):

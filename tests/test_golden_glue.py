@@ -41,3 +41,13 @@ def test_nan_quaternion_patched(gold):
     q = gold["deg1_quats"]
     np.testing.assert_array_equal(q[5], np.array([0, 0, 0, 1], dtype=np.float32))
     assert np.isfinite(q).all()
+
+
+def test_metrics_oracle_matches_reference_golden():
+    """oracle/metrics_ref.py (psnr, ssim) against outputs of the reference's own utils/metrics.py."""
+    from oracle import metrics_ref
+    d = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "metrics.npz"))
+    for i in range(2):
+        a, b = torch.from_numpy(d[f"b{i}_img1"]), torch.from_numpy(d[f"b{i}_img2"])
+        np.testing.assert_array_equal(metrics_ref.ssim(a, b, 11, size_average=False).numpy(), d[f"b{i}_ssim"])
+        np.testing.assert_array_equal(metrics_ref.psnr(a, b).numpy(), d[f"b{i}_psnr"])

@@ -58,5 +58,31 @@ def test_evaluate_scenes_single_rank(device):
     want = torch.cat([gsplat_ref.psnr_u8(renders[s], targets[s]).reshape(-1) for s in range(2)])
     assert got["num_images"] == 6 and got["num_scenes"] == 2
     assert got["psnr"] == pytest.approx(float(want.double().mean()), abs=1e-4)
+    # SSIM of the uint8 images /255 (train.py:104-113 -> metrics.py:26-29, :103-135)
+    from oracle import metrics_ref
+    q = lambda x: (x * 255).to(torch.uint8).float().div(255.0).permute(0, 3, 1, 2)  # noqa: E731
+    want_ssim = torch.cat([metrics_ref.ssim(q(renders[s].clamp(max=1)), q(targets[s]), 11, size_average=False)
+                           for s in range(2)])
+    assert got["ssim"] == pytest.approx(float(want_ssim.double().mean()), abs=2e-6)
     refined = evaluate_scenes(model, scenes, cams, lambda i: targets[i].to(device), device)
     assert refined["num_images"] == 6 and refined["psnr"] == refined["psnr"]  # finite / not NaN
+
+
+def test_ssim_matches_reference_golden(device):
+    """sfx_ssim vs the outputs of the reference's own utils/metrics.py ssim (tests/golden/metrics.npz) and the
+    oracle on a render-sized batch (HWC layout as rendered; tolerance 2e-6 absolute on an SSIM in [-1, 1])."""
+    import os
+    import numpy as np
+    from oracle import metrics_ref
+    from splatformer_amd import metrics
+    d = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "metrics.npz"))
+    for i in range(2):
+        a, b = torch.from_numpy(d[f"b{i}_img1"]), torch.from_numpy(d[f"b{i}_img2"])
+        got = metrics.ssim(a.permute(0, 2, 3, 1).to(device), b.permute(0, 2, 3, 1).to(device)).cpu()
+        assert (got - torch.from_numpy(d[f"b{i}_ssim"])).abs().max() < 2e-6
+    g = torch.Generator().manual_seed(3)
+    x = torch.rand(3, 130, 97, 3, generator=g)
+    y = (x + 0.05 * torch.randn(x.shape, generator=g)).clamp(0, 1)
+    ref = metrics_ref.ssim(x.permute(0, 3, 1, 2), y.permute(0, 3, 1, 2), 11, size_average=False)
+    got = metrics.ssim(x.to(device), y.to(device)).cpu()
+    assert (got - ref).abs().max() < 2e-6
