@@ -28,6 +28,8 @@ tests/golden/scene_io.npz, tests/golden/metrics.npz (inputs and outputs only -- 
 
 4. `utils/metrics.py` psnr / ssim (lpips stubbed: its VGG weights are not available offline) on seeded image
    batches: pins oracle/metrics_ref.py and the SSIM kernel.
+5. `utils/gs_utils.py` export_ply_forviewer (plyfile stubbed to record the vertex array) for SH degree 1 and 0
+   scenes and prepare_viewer (cfg_args, cameras.json): pins splatformer_amd/export.py (tests/golden/export.npz).
 """
 from __future__ import annotations
 
@@ -57,8 +59,22 @@ def install_stubs(recorder):
     for m in ["cv2", "torch_scatter", "lpips"]:
         sys.modules[m] = types.ModuleType(m)
     ply = types.ModuleType("plyfile")
-    ply.PlyData = object
-    ply.PlyElement = object
+
+    class PlyElement:  # records the vertex array export_ply_forviewer builds
+        @staticmethod
+        def describe(elements, name):
+            recorder["ply_elements"] = elements.copy()
+            return (name, elements)
+
+    class PlyData:
+        def __init__(self, els):
+            self.els = els
+
+        def write(self, path):
+            recorder["ply_path"] = path
+
+    ply.PlyData = PlyData
+    ply.PlyElement = PlyElement
     sys.modules["plyfile"] = ply
 
     gs = types.ModuleType("gsplat")
@@ -203,8 +219,35 @@ def main():
     torch.tensor = orig_tensor
     so = scene_io_golden(rec)
     mo = metrics_golden()
+    eo = export_golden(rec, gs_utils)
     print("wrote", sorted(out)[:4], "...", len(out), "render arrays;", len(fo), "feature-predictor arrays;",
-          len(so), "scene-io arrays;", len(mo), "metrics arrays")
+          len(so), "scene-io arrays;", len(mo), "metrics arrays;", len(eo), "export arrays")
+
+
+def export_golden(rec, gs_utils):
+    import tempfile
+    from splatformer_amd.scenes import make_cameras, make_scene
+    eo = {}
+    with tempfile.TemporaryDirectory() as root:
+        for deg in (1, 0):
+            s = make_scene(50, sh_degree=deg, seed=31 + deg)
+            if deg == 0:
+                s["features_rest"] = torch.zeros(50, 0, 3)
+            rec.pop("ply_elements", None)
+            gs_utils.export_ply_forviewer(s, os.path.join(root, "pc", f"deg{deg}.ply"))
+            for k, v in s.items():
+                eo[f"deg{deg}_in_{k}"] = v.numpy()
+            eo[f"deg{deg}_vertices"] = rec["ply_elements"]
+        cams = make_cameras(80, 60, n_views=3)
+        cams_t = {k: (torch.as_tensor(v) if not isinstance(v, torch.Tensor) else v) for k, v in cams.items()}
+        cams_t["camera_to_worlds"] = cams_t["camera_to_worlds"][:, :3, :4].contiguous()  # nerfstudio [V,3,4]
+        gs_utils.prepare_viewer(cams_t, root, 1)
+        eo["cam_c2w"] = cams_t["camera_to_worlds"].numpy()
+        eo["cam_intr"] = np.array([float(cams_t[k]) for k in ("fx", "fy", "width", "height")])
+        eo["cameras_json"] = np.array(open(os.path.join(root, "cameras.json")).read())
+        eo["cfg_args"] = np.array(open(os.path.join(root, "cfg_args")).read())
+    np.savez_compressed(os.path.join(OUT, "export.npz"), **eo)
+    return eo
 
 
 def metrics_golden():
