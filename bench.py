@@ -33,10 +33,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
-BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA (no sparsity)
-# The GEMM computes fp32 products as six bf16 term products (3-term split, gemm.hip): its fp32-equivalent
-# ceiling is the dense bf16 peak / 6.
-SPLIT_PEAK_TFLOPS = round(BF16_MFMA_PEAK_TFLOPS / 6, 1)
+F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense fp16 / bf16 MFMA (no sparsity)
+# The GEMM computes fp32-accurate products as three fp16 term products (fp16x2 split operands, gemm.hip): its
+# fp32-equivalent ceiling is the dense fp16 peak / 3.
+SPLIT_PEAK_TFLOPS = round(F16_MFMA_PEAK_TFLOPS / 3, 1)
 # rocprofv3 FETCH_SIZE / WRITE_SIZE passes over this bench (tools/traffic_summary.py), committed per round
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r01_traffic_splitgemm.json")
 HBM_PEAK_GBS = 8000.0
@@ -80,31 +80,34 @@ class GemmRecorder:
         rec = self
 
         def lin(x, weight, bias=None, **kw):
-            out = rec._lin(x, weight, bias, **kw)
+            res = rec._lin(x, weight, bias, **kw)
+            out = res[0] if isinstance(res, tuple) else res
             M = out.shape[0]
             N, K = weight.shape
             kw2 = dict(kw)
             kw2["out"] = torch.empty_like(out) if kw.get("out") is None else torch.empty_like(kw["out"])
             rec.calls.append(("linear", 2.0 * M * N * K, lambda: rec._lin(x, weight, bias, **kw2), (M, N, K)))
-            return out
+            return res
 
-        def conv(x, smap, weight, bias, out=None):
-            o = rec._conv(x, smap, weight, bias, out=out)
+        def conv(x, smap, weight, bias, out=None, **kw):
+            o = rec._conv(x, smap, weight, bias, out=out, **kw)
             n, cin = x.shape
             cout = weight.shape[0]
             scratch = torch.empty_like(o)
             fl = 2.0 * (n + smap.num_pairs) * cin * cout
-            rec.calls.append(("subm_conv", fl, lambda: rec._conv(x, smap, weight, bias, out=scratch), (n, cout, cin)))
+            rec.calls.append(("subm_conv", fl, lambda: rec._conv(x, smap, weight, bias, out=scratch, **kw),
+                              (n, cout, cin)))
             return o
 
         def grp(x, weight, bias, groups, **kw):
-            out = rec._grp(x, weight, bias, groups, **kw)
+            res = rec._grp(x, weight, bias, groups, **kw)
+            out = res[0] if isinstance(res, tuple) else res
             G, N, K = weight.shape
             scratch = torch.empty_like(out)
             rec.calls.append(("grouped_linear", 2.0 * x.shape[0] * G * N * K,
-                              lambda: rec._grp(x, weight, bias, groups, act=kw.get("act", 0), out=scratch),
+                              lambda: rec._grp(x, weight, bias, groups, **dict(kw, out=scratch)),
                               (x.shape[0], G * N, K)))
-            return out
+            return res
 
         ptv3_ops.linear, ptv3_ops.subm_conv, ptv3_ops.grouped_linear = lin, conv, grp
         return self
@@ -147,11 +150,12 @@ def roofline_probe(model, scene, reps=5):
         "frac": round(achieved / SPLIT_PEAK_TFLOPS, 4), "traffic": traffic,
         "traffic_unit": "HBM bytes per scene (all GEMM launches; 2*FETCH_SIZE + WRITE_SIZE, " +
                         os.path.relpath(TRAFFIC_FILE, ROOT) + ")",
-        "peak_basis": (f"fp32-equivalent ceiling of the 3-term bf16 split GEMM = dense bf16 MFMA {BF16_MFMA_PEAK_TFLOPS:.0f}"
-                       f" / 6 term products; exact-fp32 MFMA peak is {FP32_MFMA_PEAK_TFLOPS}"),
+        "peak_basis": (f"fp32-equivalent ceiling of the fp16x2 split GEMM = dense fp16 MFMA {F16_MFMA_PEAK_TFLOPS:.0f}"
+                       f" / 3 term products; exact-fp32 MFMA peak is {FP32_MFMA_PEAK_TFLOPS}"),
         "frac_of_fp32_mfma_peak": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
-        "kernel": ("gemm_kernel (sfx_linear / sfx_subm_conv: fp32 operands split into 3 bf16 terms, "
-                   "6 x v_mfma_f32_32x32x16_bf16 per block, fp32 accumulation), all launches of one scene"),
+        "kernel": ("gemm_kernel (sfx_linear / sfx_subm_conv: fp32 operands scaled by powers of two and split into "
+                   "2 fp16 terms, 3 x v_mfma_f32_32x32x16_f16 per block, fp32 accumulation; K < 64: exact fp32 "
+                   "MFMA), all launches of one scene (incl. their operand-maxima passes)"),
         "launches": len(per), "gemm_ms_per_scene": round(tot_ms, 3),
         "algorithmic_gflop_per_scene": round(tot_fl / 1e9, 1),
         "top_launch": {"op": top[1], "M_N_K": list(top[2]), "avg_ms": round(top[0], 4),

@@ -118,7 +118,22 @@ int sfx_linear(int M, int N, int K, const float* A, long long lda, const int* ga
                int act_ncols, const float* R, long long ldr, const int* residual_idx, float* Y, long long ldy,
                float* Ypre, long long ldypre, int groups, long long group_stride_A, long long group_stride_W,
                long long group_stride_bias, long long group_stride_Y, const int* out_row_idx, const float* rowscale,
-               int pre_before_act, void* stream);
+               int pre_before_act, const unsigned long long* a_amax, unsigned a_tag,
+               const unsigned long long* w_amax, unsigned w_tag, unsigned long long* y_amax, unsigned y_tag,
+               void* stream);
+
+/* fp16x2 operand maxima ("amax slots").  The GEMMs run K >= 64 products on split operands: fp16x2 by default
+ * (a power-of-two scale per operand from an upper bound of its largest magnitude; SFX_GEMM_PREC=bf16x3 or fp32
+ * select the other forms).  A slot is 64 unsigned long long sub-slots, zero-initialised by the caller once,
+ * holding (tag << 32 | float bits) written with atomicMax; readers use the sub-slots carrying their tag.
+ * a_amax / w_amax (may be NULL: the library then runs its own maxima pass) bound |A'| and |W| of a GEMM;
+ * y_amax (may be NULL) receives max |Y| of a launch's outputs under y_tag (Stream-K is then not used).
+ * sfx_amax_f32 writes max |X| of a [rows x cols] (row stride ld) matrix; sfx_ln_amax_bound writes the bound
+ * sqrt(C-1) * max|gamma| + max|beta| of any LayerNorm output with those affine parameters. */
+int sfx_amax_f32(int rows, int cols, const float* x, long long ld, unsigned long long* slot, unsigned tag,
+                 void* stream);
+int sfx_ln_amax_bound(int C, const float* gamma, const float* beta, unsigned long long* slot, unsigned tag,
+                      void* stream);
 
 /* Tuning / test hook: force the GEMM tile configuration (index into gemm.hip kCfgs, -1 = cost model) and
  * Stream-K (0 off, 1 on where legal, -1 = cost model) for every later sfx_linear / sfx_subm_conv call of the
@@ -241,7 +256,8 @@ int sfx_subm_pairs(int n, const int* nbr, void* ws, size_t ws_bytes, int* pair_i
  * weight [Cout,3,3,3,Cin]; pair_off_host = the 28 pair_off values copied to the host. */
 int sfx_subm_conv(int n, int cin, int cout, const float* x, long long ldx, const int* nbr, const float* weight,
                   const float* bias, const int* pair_in, const int* pair_out, const int* pair_off_host, float* out,
-                  long long ldo, void* stream);
+                  long long ldo, const unsigned long long* x_amax, unsigned x_tag,
+                  const unsigned long long* w_amax, unsigned w_tag, void* stream);
 
 /* FeaturePredictor batchify (feature_predictor.py:134-156): strided attribute rows -> feat rows
  * [means,scales,opacities,quats,dc,rest], grid_coord = floor(means*res), optional atomic grid max. */

@@ -61,6 +61,50 @@ __device__ __forceinline__ void split3(float4 v, uint2 (&t)[3]) {
   t[2] = make_uint2(pk_bf16(r0, r1), pk_bf16(r2, r3));
 }
 
+// fp32 -> two fp16 terms of the scaled value (fp16x2 GEMM operands): x*s = h + l + r with h = fp16(x*s),
+// l = fp16(x*s - h) (the residual x*s - h is exact in fp32), |r| <= 2^-22 |x*s|.  `s` is a power of two that
+// puts the operand's largest magnitude in [2^14, 2^15), so no term overflows; elements far below the maximum
+// lose bits of l only below 2^-24 of the maximum (fp16 subnormals).  h*h + h*l + l*h on fp16 MFMA with fp32
+// accumulation has the error of fp32 arithmetic (dropped l*l <= 2^-22).
+typedef _Float16 sfx_f16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ unsigned pk_f16(float a, float b) {
+  const sfx_f16x2 v = __builtin_convertvector((float __attribute__((ext_vector_type(2)))){a, b}, sfx_f16x2);
+  return __builtin_bit_cast(unsigned, v);
+}
+__device__ __forceinline__ void split2h(float4 v, float s, uint2 (&t)[2]) {
+  const float x0 = v.x * s, x1 = v.y * s, x2 = v.z * s, x3 = v.w * s;
+  const unsigned u0 = pk_f16(x0, x1), u1 = pk_f16(x2, x3);
+  t[0] = make_uint2(u0, u1);
+  const sfx_f16x2 h0 = __builtin_bit_cast(sfx_f16x2, u0), h1 = __builtin_bit_cast(sfx_f16x2, u1);
+  t[1] = make_uint2(pk_f16(x0 - (float)h0.x, x1 - (float)h0.y), pk_f16(x2 - (float)h1.x, x3 - (float)h1.y));
+}
+
+// amax slots (fp16x2 GEMM operand scales): 64 u64 sub-slots holding (tag << 32 | bits of a non-negative float),
+// written with atomicMax (larger tags supersede older contents), read as the max over the sub-slots that carry
+// the expected tag.  Every lane of the calling wave returns the same value.
+constexpr int kAmaxSub = 64;
+__device__ __forceinline__ float read_amax(const unsigned long long* slot, unsigned tag) {
+  const unsigned long long v = slot[__lane_id()];
+  float m = ((unsigned)(v >> 32) == tag) ? __builtin_bit_cast(float, (unsigned)(v & 0xffffffffu)) : 0.f;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(unsigned, m)));
+}
+// workgroup-wide max of `m` (every thread calls it), one atomic into sub-slot blockIdx % 64
+__device__ __forceinline__ void publish_amax(float m, unsigned long long* slot, unsigned tag, float* lds_waves) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  const int nw = (blockDim.x * blockDim.y + 63) / 64, w = (threadIdx.y * blockDim.x + threadIdx.x) >> 6;
+  if ((threadIdx.x & 63) == 0) lds_waves[w] = m;
+  __syncthreads();
+  if (threadIdx.x == 0 && threadIdx.y == 0) {
+    float r = 0.f;
+    for (int i = 0; i < nw; ++i) r = fmaxf(r, lds_waves[i]);
+    atomicMax(slot + (blockIdx.x + blockIdx.y * gridDim.x) % kAmaxSub,
+              ((unsigned long long)tag << 32) | __builtin_bit_cast(unsigned, r));
+  }
+}
+
 // 64-lane wavefront helpers ------------------------------------------------
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 

@@ -24,6 +24,8 @@
 // hardware -- no per-element branches, which hipcc would otherwise turn into
 // one `s_waitcnt vmcnt(0)` per load and serialise the prefetch.
 #include <cstdlib>
+#include <cstring>
+#include <type_traits>
 
 #include "common.h"
 
@@ -83,7 +85,16 @@ struct GemmArgs {
   // boundary gets partial sums (atomic add into a zero-filled output; the k-slab-0 owner adds the linear
   // epilogue terms).  Only for linear epilogues (no activation, no pre-residual copy, no in-place residual).
   int sk;
-  int split;  // 3-term bf16 split operands (see gemm_kernel); chosen in pick_cfg
+  int split;  // operand precision (see gemm_kernel): 0 exact fp32 MFMA, 2 fp16x2, 3 bf16x3; chosen in pick_cfg
+  // fp16x2 operand maxima, as "amax slots": 64 sub-slots of (tag << 32 | float bits) written with atomicMax
+  // by the producer of the tensor (one sub-slot per producing workgroup); a reader takes the max over the
+  // sub-slots carrying the expected tag, so slots are reused without clearing.  Upper bounds are enough
+  // (a looser bound only lowers the scale).
+  const unsigned long long* a_amax;
+  const unsigned long long* w_amax;
+  unsigned a_tag, w_tag;
+  unsigned long long* y_amax;  // optional: max |Y| of this launch's outputs -> slot, tag y_tag
+  unsigned y_tag;
 };
 
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
@@ -133,7 +144,8 @@ __device__ __forceinline__ void bstore1(__amdgpu_buffer_rsrc_t r, unsigned off, 
   __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, off, 0, 0);
 }
 
-using sfx::split3;  // fp32 -> three bf16 terms (common.h)
+using sfx::split3;   // fp32 -> three bf16 terms (common.h)
+using sfx::split2h;  // fp32 -> two fp16 terms of the scaled value (common.h)
 
 // Persistent tile loop: each workgroup walks output tiles blockIdx.x, +gridDim.x, ... and prefetches
 // the first K-slab of its NEXT tile while it computes the last slab and runs the epilogue of the
@@ -153,8 +165,16 @@ enum Mode { MODE_DENSE = 0, MODE_GATHER1 = 1, MODE_GATHERS = 2, MODE_PAIR = 3 };
 // Split LDS image: per buffer and term a [rows][32] bf16 array with 64-byte rows and no padding; the
 // 16-byte chunk c of row r sits at chunk c ^ ((r >> 2) & 3), which makes the fragment reads (16 rows x one
 // chunk per quarter-wave) and the staging writes (4 rows x 64 B per half-wave) bank-conflict free.
-template <int BM, int BN, int WGM, int NW, bool VEC, int MODE, bool SPLIT>
+//
+// SPL = 2 (the default for K >= 64): fp16x2 -- each operand is scaled by a power of two that puts its largest
+// magnitude in [2^14, 2^15) and split into two fp16 terms (split2h); a block is h*h + h*l + l*h on
+// v_mfma_f32_32x32x16_f16 (three products, two LDS term images) and the accumulators are unscaled once before
+// the epilogue.  Error: that of fp32 arithmetic (dropped l*l <= 2^-22 relative, products exact in fp32).
+template <int BM, int BN, int WGM, int NW, bool VEC, int MODE, int SPL>
 __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs p, int tiles_n, int total_tiles) {
+  constexpr bool SPLIT = SPL != 0;
+  constexpr int NTERM = SPL == 2 ? 2 : 3;  // LDS term images per operand
+  static_assert(SPL == 0 || SPL == 2 || SPL == 3, "operand precision");
   constexpr int NT = NW * 64;                  // threads
   constexpr int WGN = NW / WGM;                // waves along N
   constexpr int WM = BM / WGM, WN = BN / WGN;  // wave sub-tile
@@ -167,14 +187,14 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs
   constexpr int W_ITERS = BN * BK / 4 / NT;
   constexpr int NBUF = SPLIT ? (NW == 8 ? 2 : 1) : 2;
   // fp32: double-buffered [row][k] images (row stride 36); SPLIT: NBUF x 3 swizzled bf16 term images
-  constexpr int A_FLOATS = SPLIT ? NBUF * 3 * BM * BK / 2 : 2 * BM * LDS_STRIDE;
-  constexpr int W_FLOATS = SPLIT ? NBUF * 3 * BN * BK / 2 : 2 * BN * LDS_STRIDE;
+  constexpr int A_FLOATS = SPLIT ? NBUF * NTERM * BM * BK / 2 : 2 * BM * LDS_STRIDE;
+  constexpr int W_FLOATS = SPLIT ? NBUF * NTERM * BN * BK / 2 : 2 * BN * LDS_STRIDE;
   __shared__ __attribute__((aligned(16))) float sAraw[A_FLOATS];
   __shared__ __attribute__((aligned(16))) float sWraw[W_FLOATS];
   float (*sA)[BM * LDS_STRIDE] = reinterpret_cast<float (*)[BM * LDS_STRIDE]>(sAraw);
   float (*sW)[BN * LDS_STRIDE] = reinterpret_cast<float (*)[BN * LDS_STRIDE]>(sWraw);
-  char* sAs = reinterpret_cast<char*>(sAraw);  // [NBUF][3][BM][64 B]
-  char* sWs = reinterpret_cast<char*>(sWraw);  // [NBUF][3][BN][64 B]
+  char* sAs = reinterpret_cast<char*>(sAraw);  // [NBUF][NTERM][BM][64 B]
+  char* sWs = reinterpret_cast<char*>(sWraw);  // [NBUF][NTERM][BN][64 B]
   // byte offset of the 4-element group at k = c4 * 4 (c4 = 0..7) of row r in a swizzled term image
   auto swz = [](int r, int c4) -> int { return r * 64 + ((((c4 >> 1) ^ (r >> 2)) & 3) << 4) + ((c4 & 1) << 3); };
 
@@ -192,6 +212,22 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs
   const int h = lane >> 5, l32 = lane & 31;
   const int K = p.K;
   const int nk = (K + BK - 1) / BK;
+  // fp16x2 operand scales (powers of two) and their inverses, from the tagged maxima
+  float scA = 1.f, scW = 1.f, invA = 1.f, invW = 1.f;
+  if constexpr (SPL == 2) {
+    auto scale_of = [](float m, float& s, float& inv) {
+      int e = 0;
+      if (m > 0.f && m <= 3.4028235e38f) {  // finite, non-zero (inf / NaN: unscaled; the result is inf / NaN)
+        (void)frexpf(m, &e);
+        e = 15 - e;
+        e = e > 126 ? 126 : (e < -126 ? -126 : e);
+      }
+      s = ldexpf(1.f, e);
+      inv = ldexpf(1.f, -e);
+    };
+    scale_of(sfx::read_amax(p.a_amax, p.a_tag), scA, invA);
+    scale_of(sfx::read_amax(p.w_amax, p.w_tag), scW, invW);
+  }
   // byte offsets fit 31 bits (host checks every operand against the 2 GiB buffer range)
   const unsigned lda32 = (unsigned)p.lda, ldw32 = (unsigned)p.ldw, ldy32 = (unsigned)p.ldy;
   const unsigned ldr32 = (unsigned)p.ldr, ldp32 = (unsigned)p.ldypre;
@@ -301,19 +337,19 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs
       const int b = NBUF == 2 ? buf : 0;
 #pragma unroll
       for (int i = 0; i < A_ITERS; ++i) {
-        uint2 t[3];
-        split3(ra[i], t);
+        uint2 t[NTERM];
+        if constexpr (SPL == 2) split2h(ra[i], scA, t); else split3(ra[i], t);
         const int o = swz(lrow + RPP * i, lcol >> 2);
 #pragma unroll
-        for (int q = 0; q < 3; ++q) *reinterpret_cast<uint2*>(sAs + ((b * 3 + q) * BM) * 64 + o) = t[q];
+        for (int q = 0; q < NTERM; ++q) *reinterpret_cast<uint2*>(sAs + ((b * NTERM + q) * BM) * 64 + o) = t[q];
       }
 #pragma unroll
       for (int i = 0; i < W_ITERS; ++i) {
-        uint2 t[3];
-        split3(rw[i], t);
+        uint2 t[NTERM];
+        if constexpr (SPL == 2) split2h(rw[i], scW, t); else split3(rw[i], t);
         const int o = swz(lrow + RPP * i, lcol >> 2);
 #pragma unroll
-        for (int q = 0; q < 3; ++q) *reinterpret_cast<uint2*>(sWs + ((b * 3 + q) * BN) * 64 + o) = t[q];
+        for (int q = 0; q < NTERM; ++q) *reinterpret_cast<uint2*>(sWs + ((b * NTERM + q) * BN) * 64 + o) = t[q];
       }
       return;
     }
@@ -339,6 +375,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs
   // are fetched BEFORE the next tile's prefetch is issued, so the epilogue never waits on the prefetch.
   float ebias[NB], escale[NB], eshift[NB];
   int mrow[MB][16];
+  float ymax = 0.f;  // running max |Y| of this workgroup's outputs (p.y_amax)
   auto load_mrow = [&](const Tile& ti, __amdgpu_buffer_rsrc_t rO) {
 #pragma unroll
     for (int a = 0; a < MB; ++a)
@@ -467,6 +504,10 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs
 #pragma unroll
           for (int r = 0; r < 16; ++r) v[r] += rv[r];
         }
+        if (p.y_amax) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) ymax = fmaxf(ymax, fabsf(v[r]));
+        }
         if (partial) {
 #pragma unroll
           for (int r = 0; r < 16; ++r)
@@ -480,6 +521,14 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs
   };
 
   auto epilogue = [&](const Tile& ti, bool partial, bool owner0) {
+    if constexpr (SPL == 2) {  // undo the operand scales (powers of two: exact)
+#pragma unroll
+      for (int a = 0; a < MB; ++a)
+#pragma unroll
+        for (int b = 0; b < NB; ++b)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[a][b][r] = acc[a][b][r] * invA * invW;
+    }
     if constexpr (MODE != MODE_PAIR) {
       if (!ti.out_rows) {
         direct_epilogue(ti, partial, owner0);
@@ -589,6 +638,10 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs
 #pragma unroll
           for (int r = 0; r < 16; ++r) v[r] += rv[r];
         }
+        if (p.y_amax) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) ymax = fmaxf(ymax, mrow[a][r] >= 0 ? fabsf(v[r]) : 0.f);
+        }
         if (partial) {
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
@@ -610,33 +663,46 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs
   // SPLIT: k16 steps [s0, s1) of the slab
   auto compute_split = [&](int buf, int s0, int s1) {
     const int bb = NBUF == 2 ? buf : 0;
+    typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
+    typedef typename std::conditional<SPL == 2, f16x8, bf16x8>::type frag_t;
 #pragma unroll
     for (int s = s0; s < s1; ++s) {
-      bf16x8 af[MB][3], wf[NB][3];
+      frag_t af[MB][NTERM], wf[NB][NTERM];
 #pragma unroll
-      for (int q = 0; q < 3; ++q) {
+      for (int q = 0; q < NTERM; ++q) {
 #pragma unroll
         for (int a = 0; a < MB; ++a) {
           const int r = wm * WM + a * 32 + l32;
           af[a][q] = __builtin_bit_cast(
-              bf16x8, *reinterpret_cast<const uint4*>(sAs + ((bb * 3 + q) * BM) * 64 + swz(r, 4 * s + 2 * h)));
+              frag_t, *reinterpret_cast<const uint4*>(sAs + ((bb * NTERM + q) * BM) * 64 + swz(r, 4 * s + 2 * h)));
         }
 #pragma unroll
         for (int b = 0; b < NB; ++b) {
           const int r = wn * WN + b * 32 + l32;
           wf[b][q] = __builtin_bit_cast(
-              bf16x8, *reinterpret_cast<const uint4*>(sWs + ((bb * 3 + q) * BN) * 64 + swz(r, 4 * s + 2 * h)));
+              frag_t, *reinterpret_cast<const uint4*>(sWs + ((bb * NTERM + q) * BN) * 64 + swz(r, 4 * s + 2 * h)));
         }
       }
       // smallest terms first; the (a, b) blocks interleave so consecutive MFMAs are independent
-      constexpr int QA[6] = {2, 1, 0, 1, 0, 0}, QW[6] = {0, 1, 2, 0, 1, 0};
+      if constexpr (SPL == 2) {
+        constexpr int QA[3] = {1, 0, 0}, QW[3] = {0, 1, 0};
 #pragma unroll
-      for (int j = 0; j < 6; ++j)
+        for (int j = 0; j < 3; ++j)
 #pragma unroll
-        for (int a = 0; a < MB; ++a)
+          for (int a = 0; a < MB; ++a)
 #pragma unroll
-          for (int b = 0; b < NB; ++b)
-            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][QA[j]], wf[b][QW[j]], acc[a][b], 0, 0, 0);
+            for (int b = 0; b < NB; ++b)
+              acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[a][QA[j]], wf[b][QW[j]], acc[a][b], 0, 0, 0);
+      } else {
+        constexpr int QA[6] = {2, 1, 0, 1, 0, 0}, QW[6] = {0, 1, 2, 0, 1, 0};
+#pragma unroll
+        for (int j = 0; j < 6; ++j)
+#pragma unroll
+          for (int a = 0; a < MB; ++a)
+#pragma unroll
+            for (int b = 0; b < NB; ++b)
+              acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][QA[j]], wf[b][QW[j]], acc[a][b], 0, 0, 0);
+      }
     }
   };
   auto compute = [&](int buf) {
@@ -743,6 +809,10 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs
     kb = 0;
     ke = nke;
   }
+  if (p.y_amax) {
+    __shared__ float ywaves[NW];
+    sfx::publish_amax(ymax, p.y_amax, p.y_tag, ywaves);
+  }
 }
 
 int num_cus() {
@@ -796,14 +866,19 @@ void launch(GemmArgs a, int groups, bool vec, hipStream_t st) {
   }
   dim3 grid(grid_x, 1, groups);
   if constexpr (NW == 8) {  // split-only tiles (vec operands)
-    gemm_kernel<BM, BN, WGM, 8, true, MODE, true><<<grid, 512, 0, st>>>(a, tiles_n, total);
-  } else {
-    if (vec && split)
-      gemm_kernel<BM, BN, WGM, 4, true, MODE, true><<<grid, 256, 0, st>>>(a, tiles_n, total);
-    else if (vec)
-      gemm_kernel<BM, BN, WGM, 4, true, MODE, false><<<grid, 256, 0, st>>>(a, tiles_n, total);
+    if (a.split == 2)
+      gemm_kernel<BM, BN, WGM, 8, true, MODE, 2><<<grid, 512, 0, st>>>(a, tiles_n, total);
     else
-      gemm_kernel<BM, BN, WGM, 4, false, MODE, false><<<grid, 256, 0, st>>>(a, tiles_n, total);
+      gemm_kernel<BM, BN, WGM, 8, true, MODE, 3><<<grid, 512, 0, st>>>(a, tiles_n, total);
+  } else {
+    if (vec && a.split == 2)
+      gemm_kernel<BM, BN, WGM, 4, true, MODE, 2><<<grid, 256, 0, st>>>(a, tiles_n, total);
+    else if (vec && split)
+      gemm_kernel<BM, BN, WGM, 4, true, MODE, 3><<<grid, 256, 0, st>>>(a, tiles_n, total);
+    else if (vec)
+      gemm_kernel<BM, BN, WGM, 4, true, MODE, 0><<<grid, 256, 0, st>>>(a, tiles_n, total);
+    else
+      gemm_kernel<BM, BN, WGM, 4, false, MODE, 0><<<grid, 256, 0, st>>>(a, tiles_n, total);
   }
 }
 
@@ -821,14 +896,134 @@ constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
 
 // Operand precision: the 3-term bf16 split (fp32-accurate, see gemm_kernel) from K >= split_min_k
 // (SFX_GEMM_SPLIT_MINK; default 64), exact fp32 MFMA below it or with SFX_GEMM_PREC=fp32.
-bool use_split(int K) {
-  static int min_k = -2;
+// Operand precision of a launch (GemmArgs::split): exact fp32 MFMA below K = 64 (SFX_GEMM_SPLIT_MINK) or with
+// SFX_GEMM_PREC=fp32; otherwise split operands, fp16x2 (default) or bf16x3 (SFX_GEMM_PREC=bf16x3).  Both split
+// forms are as accurate as fp32 arithmetic; fp16x2 needs half the MFMAs and LDS images of bf16x3.
+int split_mode(int K) {
+  static int min_k = -2, mode = 2;
   if (min_k == -2) {
     const char* e = getenv("SFX_GEMM_PREC");
     const char* m = getenv("SFX_GEMM_SPLIT_MINK");
-    min_k = (e && e[0] == 'f') ? -1 : ((m && *m) ? atoi(m) : 64);
+    const bool f32 = e && !strcmp(e, "fp32");
+    mode = (e && !strcmp(e, "bf16x3")) ? 3 : 2;
+    min_k = f32 ? -1 : ((m && *m) ? atoi(m) : 64);
   }
-  return min_k >= 0 && K >= min_k;
+  return (min_k >= 0 && K >= min_k) ? mode : 0;
+}
+
+// ---- fp16x2 operand maxima -------------------------------------------------------------------------------
+// max |x| over a GEMM operand, atomically max-ed into a slot as (tag << 32 | float bits): a launch's larger tag
+// supersedes whatever an earlier launch left, so slots need no clearing.  A' is read as the GEMM reads it
+// (dense rows, or gathered rows of S segments of Kseg columns; `groups` copies at a group stride).
+struct AmaxJob {
+  const float* base;
+  long long ld, group_stride;
+  int rows, cols, groups;  // cols per (gathered) segment
+  const int* gidx;         // [rows][gstride] gather index (first S used) or null
+  int gstride, S;
+};
+
+__global__ void __launch_bounds__(256) amax_kernel(AmaxJob j0, AmaxJob j1, unsigned long long* slot0,
+                                                   unsigned long long* slot1, unsigned tag0, unsigned tag1) {
+  const AmaxJob j = blockIdx.y == 0 ? j0 : j1;
+  // one wave per (group, row, segment): lanes sweep the row's columns, 16 B per lane where aligned
+  const int per_group = j.rows * j.S;
+  const int segs = j.groups * per_group;
+  const int wave = (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6), nwaves = (int)gridDim.x * 4;
+  const int lane = threadIdx.x & 63;
+  const bool vec = (j.cols % 4 == 0) && (j.ld % 4 == 0) && (j.group_stride % 4 == 0) &&
+                   ((reinterpret_cast<uintptr_t>(j.base) & 15) == 0);
+  float m = 0.f;
+  const bool flat = !j.gidx && j.ld == j.cols && (j.groups == 1 || j.group_stride == (long long)j.rows * j.ld);
+  if (flat && vec) {  // one contiguous array (the common case): 4 independent 16-byte loads in flight per lane
+    const long long n4 = (long long)segs * j.cols / 4;
+    const float4* q = reinterpret_cast<const float4*>(j.base);
+    const long long stride = (long long)gridDim.x * 256;
+    long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    for (; i + 7 * stride < n4; i += 8 * stride) {
+      float4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = q[i + u * stride];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        m = fmaxf(m, fmaxf(fmaxf(fabsf(v[u].x), fabsf(v[u].y)), fmaxf(fabsf(v[u].z), fabsf(v[u].w))));
+    }
+    for (; i < n4; i += stride) {
+      const float4 v = q[i];
+      m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    }
+  }
+  for (int sg = flat && vec ? segs : __builtin_amdgcn_readfirstlane(wave); sg < segs; sg += nwaves) {
+    const int g = sg / per_group;
+    const int rs = sg - g * per_group;
+    const int r0 = j.S == 1 ? rs : rs / j.S, seg = rs - r0 * j.S;
+    const long long row = j.gidx ? (long long)j.gidx[(long long)r0 * j.gstride + seg] : r0;
+    if (row < 0) continue;
+    const float* q = j.base + (long long)g * j.group_stride + row * j.ld;
+    if (vec) {
+      for (int c = lane * 4; c < j.cols; c += 256) {
+        const float4 v = *reinterpret_cast<const float4*>(q + c);
+        m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+      }
+    } else {
+      for (int c = lane; c < j.cols; c += 64) m = fmaxf(m, fabsf(q[c]));
+    }
+  }
+  __shared__ float wmax[4];
+  // one atomic per workgroup, spread over the 64 sub-slots (same-address atomics serialise)
+  sfx::publish_amax(m, blockIdx.y == 0 ? slot0 : slot1, blockIdx.y == 0 ? tag0 : tag1, wmax);
+}
+
+// amax slots of the library's own maxima passes: a per-device ring; stream order makes a slot's producer
+// (amax_kernel) and consumer (the GEMM) adjacent, the ring keeps launches queued on other streams apart
+unsigned long long* amax_slot() {
+  constexpr int kSlots = 2048;
+  static unsigned long long* bufs[64] = {};
+  static unsigned next[64] = {};
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (!bufs[dev]) {
+    if (hipMalloc(&bufs[dev], sizeof(unsigned long long) * sfx::kAmaxSub * kSlots) != hipSuccess) return nullptr;
+    (void)hipMemset(bufs[dev], 0, sizeof(unsigned long long) * sfx::kAmaxSub * kSlots);
+  }
+  return bufs[dev] + sfx::kAmaxSub * (next[dev]++ % kSlots);
+}
+
+unsigned next_amax_tag() {
+  static unsigned tag = 0;
+  if (++tag == 0) ++tag;  // 0 never matches (fresh slots hold zeros)
+  return tag;
+}
+
+int amax_blocks(const AmaxJob& j) {  // >= 32 KB of operand per wave, at most 2 workgroups per CU
+  const long long bytes = (long long)j.groups * j.rows * j.S * j.cols * 4;
+  const long long b = (bytes + 4 * 32768 - 1) / (4 * 32768);
+  const long long cap = 2ll * num_cus();
+  return (int)(b < 1 ? 1 : (b > cap ? cap : b));
+}
+
+// queue the maxima passes an fp16x2 launch lacks (A' and / or W); false on slot-allocation failure
+bool prepare_amax(GemmArgs& a, const AmaxJob& ja, const AmaxJob& jw, hipStream_t st) {
+  const bool need_a = !a.a_amax, need_w = !a.w_amax;
+  if (!need_a && !need_w) return true;
+  unsigned long long* sa = need_a ? amax_slot() : nullptr;
+  unsigned long long* sw = need_w ? amax_slot() : nullptr;
+  if ((need_a && !sa) || (need_w && !sw)) return false;
+  const unsigned ta = need_a ? next_amax_tag() : 0, tw = need_w ? next_amax_tag() : 0;
+  const AmaxJob& j0 = need_a ? ja : jw;
+  const int bx = (need_a && need_w) ? (amax_blocks(ja) > amax_blocks(jw) ? amax_blocks(ja) : amax_blocks(jw))
+                                    : amax_blocks(j0);
+  amax_kernel<<<dim3(bx, need_a && need_w ? 2 : 1), 256, 0, st>>>(j0, jw, need_a ? sa : sw, sw, need_a ? ta : tw,
+                                                                  tw);
+  if (need_a) { a.a_amax = sa; a.a_tag = ta; }
+  if (need_w) { a.w_amax = sw; a.w_tag = tw; }
+  return true;
+}
+
+// the operand jobs of a GemmArgs (non-pair launches; pair launches get the maxima from their caller)
+void gemm_amax_jobs(const GemmArgs& a, int groups, AmaxJob& ja, AmaxJob& jw) {
+  ja = AmaxJob{a.A, a.lda, a.gA, a.M, a.gidx ? a.Kseg : a.K, groups, a.gidx, a.gstride, a.gidx ? a.S : 1};
+  jw = AmaxJob{a.W, a.ldw, a.gW, a.N, a.K, groups, nullptr, 0, 1};
 }
 
 // tuning / test hooks: SFX_GEMM_CFG=<index into kCfgs>, SFX_GEMM_SK=0|1, or sfx_gemm_force_config()
@@ -846,12 +1041,13 @@ void read_force_env() {
 int pick_cfg(GemmArgs& a, int groups, bool vec) {
   read_force_env();
   const int nk = (int)sfx::ceil_div(a.K, BK);
-  const bool split = vec && use_split(a.K);
+  const bool split = a.split != 0;
   // eight-wave tiles exist only with split operands
   const int force = (forced >= 0 && !(kCfgs[forced].nw == 8 && !split)) ? forced : -1;
   // Stream-K needs a linear epilogue that can be split into atomically added pieces
   // (measured: the memset + atomic partial epilogues only pay off on long K; pair mode needs no memset)
   const bool sk_ok = groups == 1 && nk >= (a.pair_mode ? 8 : 16) && a.act == ACT_NONE && !a.Ypre && !a.out_rows &&
+                     !a.y_amax &&
                      !(a.R && a.R == a.Y) && a.M > 0 && forced_sk != 0;
   const double sk_overhead = a.pair_mode ? 2.5 : 4.0;  // slab-equivalents: partial epilogues (+ memset)
   int best = 0;
@@ -882,7 +1078,6 @@ int pick_cfg(GemmArgs& a, int groups, bool vec) {
     }
   }
   a.sk = best_sk ? 1 : 0;
-  a.split = split ? 1 : 0;
   tiles_m_of(a, kCfgs[best].bm);  // pair mode: slice_tile_off for the chosen shape
   return best;
 }
@@ -900,7 +1095,18 @@ void dispatch_mode(GemmArgs a, int groups, bool vec, hipStream_t st) {
   }
 }
 
-void dispatch(const GemmArgs& a, int groups, bool vec, hipStream_t st) {
+void dispatch(const GemmArgs& a0, int groups, bool vec, hipStream_t st) {
+  GemmArgs a = a0;
+  a.split = vec ? split_mode(a.K) : 0;
+  if (a.split == 2 && (!a.a_amax || !a.w_amax)) {
+    if (a.pair_mode) {
+      a.split = 3;  // (callers of pair launches pass the maxima; bf16x3 needs none)
+    } else {
+      AmaxJob ja, jw;
+      gemm_amax_jobs(a, groups, ja, jw);
+      if (!prepare_amax(a, ja, jw, st)) a.split = 3;
+    }
+  }
   if (a.pair_mode)
     dispatch_mode<MODE_PAIR>(a, groups, vec, st);
   else if (!a.gidx)
@@ -1036,12 +1242,24 @@ int sfx_gemm_force_config(int cfg, int stream_k) {
   return SFX_OK;
 }
 
+int sfx_amax_f32(int rows, int cols, const float* x, long long ld, unsigned long long* slot, unsigned tag,
+                 void* stream) {
+  SFX_REQUIRE(rows >= 0 && cols >= 0 && ld >= cols, "sfx_amax_f32: bad sizes");
+  SFX_REQUIRE(slot && tag != 0, "sfx_amax_f32: null slot or tag 0");
+  SFX_REQUIRE(rows == 0 || cols == 0 || x, "sfx_amax_f32: null buffer");
+  const AmaxJob j{x, ld, 0, rows, cols, 1, nullptr, 0, 1};
+  amax_kernel<<<dim3(amax_blocks(j), 1), 256, 0, sfx::as_stream(stream)>>>(j, j, slot, slot, tag, tag);
+  return sfx::check_launch("sfx_amax_f32");
+}
+
 int sfx_linear(int M, int N, int K, const float* A, long long lda, const int* gather_idx, int num_segments,
                const float* W, long long ldw, const float* bias, const float* scale, const float* shift, int act,
                int act_ncols, const float* R, long long ldr, const int* residual_idx, float* Y, long long ldy,
                float* Ypre, long long ldypre, int groups, long long group_stride_A, long long group_stride_W,
                long long group_stride_bias, long long group_stride_Y, const int* out_row_idx, const float* rowscale,
-               int pre_before_act, void* stream) {
+               int pre_before_act, const unsigned long long* a_amax, unsigned a_tag,
+               const unsigned long long* w_amax, unsigned w_tag, unsigned long long* y_amax, unsigned y_tag,
+               void* stream) {
   SFX_REQUIRE(M >= 0 && N > 0 && K > 0, "sfx_linear: bad sizes M=%d N=%d K=%d", M, N, K);
   SFX_REQUIRE(act >= 0 && act <= 3, "sfx_linear: bad activation %d", act);
   SFX_REQUIRE(groups >= 1, "sfx_linear: groups < 1");
@@ -1062,6 +1280,7 @@ int sfx_linear(int M, int N, int K, const float* A, long long lda, const int* ga
   a.act_ncols = act_ncols < 0 ? N : act_ncols; a.R = R; a.ldr = ldr; a.ridx = residual_idx; a.Y = Y; a.ldy = ldy;
   a.Ypre = Ypre; a.ldypre = ldypre; a.gA = group_stride_A; a.gW = group_stride_W; a.gB = group_stride_bias;
   a.gY = group_stride_Y; a.out_rows = out_row_idx; a.rowscale = rowscale; a.pre_before_act = pre_before_act;
+  a.a_amax = a_amax; a.a_tag = a_tag; a.w_amax = w_amax; a.w_tag = w_tag; a.y_amax = y_amax; a.y_tag = y_tag;
   const bool vec = (K % 4 == 0) && (lda % 4 == 0) && (ldw % 4 == 0) && aligned16(A) && aligned16(W) &&
                    (group_stride_A % 4 == 0) && (group_stride_W % 4 == 0);
   dispatch(a, groups, vec, sfx::as_stream(stream));
@@ -1074,7 +1293,8 @@ int sfx_linear(int M, int N, int K, const float* A, long long lda, const int* ga
 // pair_off_host: 28 host ints (prefix of pair counts per offset, centre slice empty).
 int sfx_subm_conv(int n, int cin, int cout, const float* x, long long ldx, const int* nbr, const float* weight,
                   const float* bias, const int* pair_in, const int* pair_out, const int* pair_off_host, float* out,
-                  long long ldo, void* stream) {
+                  long long ldo, const unsigned long long* x_amax, unsigned x_tag,
+                  const unsigned long long* w_amax, unsigned w_tag, void* stream) {
   SFX_REQUIRE(n >= 0 && cin > 0 && cout > 0, "sfx_subm_conv: bad sizes");
   if (n == 0) return SFX_OK;
   SFX_REQUIRE(x && nbr && weight && out && pair_off_host, "sfx_subm_conv: null buffer");
@@ -1087,6 +1307,13 @@ int sfx_subm_conv(int n, int cin, int cout, const float* x, long long ldx, const
   GemmArgs a{};
   a.M = n; a.N = cout; a.K = cin; a.A = x; a.lda = ldx; a.gidx = nbr + 13; a.S = 1; a.Kseg = cin; a.gstride = 27;
   a.W = weight + 13ll * cin; a.ldw = 27ll * cin; a.bias = bias; a.act = 0; a.act_ncols = cout; a.Y = out; a.ldy = ldo;
+  // fp16x2: one pair of maxima (all of x, all 27 weight slices) for both launches
+  a.a_amax = x_amax; a.a_tag = x_tag; a.w_amax = w_amax; a.w_tag = w_tag;
+  if (vec && split_mode(cin) == 2 &&
+      !prepare_amax(a, AmaxJob{x, ldx, 0, n, cin, 1, nullptr, 0, 1},
+                    AmaxJob{weight, 27ll * cin, 0, cout, 27 * cin, 1, nullptr, 0, 1}, st)) {
+    a.a_amax = a.w_amax = nullptr;  // (dispatch falls back to bf16x3 for the pair launch)
+  }
   dispatch(a, 1, vec, st);
   int rc = sfx::check_launch("sfx_subm_conv(centre)");
   if (rc) return rc;
@@ -1116,6 +1343,10 @@ int sfx_subm_conv_bwd_data(int n, int cin, int cout, const float* dy, long long 
               "sfx_subm_conv_bwd_data: operand exceeds the 2 GiB buffer-descriptor range");
   hipStream_t st = sfx::as_stream(stream);
   const bool vec = (cout % 4 == 0) && (ldy % 4 == 0) && aligned16(dy) && aligned16(weight_t);
+  GemmArgs am{};
+  if (vec && split_mode(cout) == 2)
+    (void)prepare_amax(am, AmaxJob{dy, ldy, 0, n, cout, 1, nullptr, 0, 1},
+                       AmaxJob{weight_t, (long long)cout, 0, 27 * cin, cout, 1, nullptr, 0, 1}, st);
   int* cg = centre_ws;
   int* cs = centre_ws + n;
   centre_pairs_kernel<<<sfx::ceil_div(n, 256), 256, 0, st>>>(n, nbr, cg, cs);
@@ -1123,6 +1354,7 @@ int sfx_subm_conv_bwd_data(int n, int cin, int cout, const float* dy, long long 
   a.N = cin; a.K = cout; a.A = dy; a.lda = ldy; a.S = 1; a.Kseg = cout; a.gstride = 1;
   a.ldw = cout; a.act = 0; a.act_ncols = cin; a.Y = dx; a.ldy = lddx;
   a.pair_mode = 1; a.slice_w_stride = (long long)cin * cout;
+  a.a_amax = am.a_amax; a.a_tag = am.a_tag; a.w_amax = am.w_amax; a.w_tag = am.w_tag;
   // centre offset (k = 13) as a one-slice pair launch
   GemmArgs c = a;
   c.pair_in = cg; c.pair_out = cs; c.W = weight_t + 13ll * cin * cout; c.num_slices = 1;

@@ -175,9 +175,32 @@ __global__ void __launch_bounds__(256) cpe_residual_ln4_kernel(int M, const floa
 
 inline bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
+// |LN(x)_c| = |z_c gamma_c + beta_c| with |z_c| <= sqrt(C - 1) (biased variance, eps only shrinks z)
+__global__ void __launch_bounds__(64) ln_amax_bound_kernel(int C, const float* __restrict__ g,
+                                                            const float* __restrict__ b,
+                                                            unsigned long long* __restrict__ slot, unsigned tag) {
+  __shared__ float red[1];
+  float mg = 0.f, mb = 0.f;  // one wave: both maxima are complete before the bound is formed
+  for (int c = threadIdx.x; c < C; c += 64) {
+    mg = fmaxf(mg, fabsf(g[c]));
+    mb = fmaxf(mb, fabsf(b[c]));
+  }
+  mg = sfx::wave_max(mg);
+  mb = sfx::wave_max(mb);
+  const float bound = sqrtf((float)(C > 1 ? C - 1 : 1)) * mg * 1.0001f + mb;
+  sfx::publish_amax(bound, slot, tag, red);
+}
+
 }  // namespace
 
 extern "C" {
+
+int sfx_ln_amax_bound(int C, const float* gamma, const float* beta, unsigned long long* slot, unsigned tag,
+                      void* stream) {
+  SFX_REQUIRE(C > 0 && gamma && beta && slot && tag != 0, "sfx_ln_amax_bound: bad arguments");
+  ln_amax_bound_kernel<<<1, 64, 0, sfx::as_stream(stream)>>>(C, gamma, beta, slot, tag);
+  return sfx::check_launch("sfx_ln_amax_bound");
+}
 
 int sfx_layernorm(int M, int C, const float* X, long long ldx, const float* gamma, const float* beta, float eps,
                   float* Y, long long ldy, void* stream) {

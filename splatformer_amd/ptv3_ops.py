@@ -15,7 +15,9 @@ from . import _lib
 from ._lib import I, L, P, F, Z, call, ptr, stream
 
 _lib.register("sfx_linear", [I, I, I, P, L, P, I, P, L, P, P, P, I, I, P, L, P, P, L, P, L, I, L, L, L, L, P, P, I,
-                              P])
+                              P, I, P, I, P, I, P])
+_lib.register("sfx_amax_f32", [I, I, P, L, P, I, P])
+_lib.register("sfx_ln_amax_bound", [I, P, P, P, I, P])
 _lib.register("sfx_layernorm", [I, I, P, L, P, P, F, P, L, P])
 _lib.register("sfx_cpe_residual_ln", [I, I, P, P, P, P, P, P, F, P, P, P])
 _lib.register("sfx_window_attention", [I, I, I, I, I, P, P, P, F, P, P])
@@ -31,7 +33,7 @@ _lib.register("sfx_subm_neighbors", [I, P, P, I, P, P, P, P, P, P])
 _lib.register("sfx_subm_permute", [I, P, P, P, P, P, P])
 _lib.register("sfx_subm_pairs_workspace_bytes", [I], Z)
 _lib.register("sfx_subm_pairs", [I, P, P, Z, P, P, P, P])
-_lib.register("sfx_subm_conv", [I, I, I, P, L, P, P, P, P, P, P, P, L, P])
+_lib.register("sfx_subm_conv", [I, I, I, P, L, P, P, P, P, P, P, P, L, P, I, P, I, P])
 _lib.register("sfx_gs_pack", [I, P, L, P, L, P, L, P, L, P, L, P, L, I, F, P, L, P, P, P])
 _lib.register("sfx_offsets_to_batch", [I, I, P, P, P])
 _lib.register("sfx_gemm_force_config", [I, I])
@@ -45,6 +47,56 @@ def gemm_force_config(cfg: int = -1, stream_k: int = -1) -> None:
     """Tuning / test hook: force the GEMM tile configuration and Stream-K choice (-1 = cost model)."""
     call("sfx_gemm_force_config", cfg, stream_k)
 ORDER_TYPES = {"z": 0, "z-trans": 1, "hilbert": 2, "hilbert-trans": 3}
+
+
+# ---- fp16x2 operand maxima ("amax slots", include/sfx.h) ----------------------------------------------------
+# A slot is (device pointer to 64 u64 sub-slots, tag).  The GEMM scales its fp16x2 operands from upper bounds
+# of their largest magnitudes: the refiner passes the slots its producers fill (GEMM epilogues, LayerNorm
+# weight bounds, cached weight maxima); a GEMM without one runs the library's own maxima pass.
+AMAX_SUB = 64
+_AMAX_RING = 4096
+_amax_state: dict = {}
+
+
+def new_amax(device) -> Tuple[int, int]:
+    """A fresh (slot pointer, tag) from a per-device ring (zero-initialised once; tags only grow)."""
+    st = _amax_state.get(device)
+    if st is None:
+        buf = torch.zeros(_AMAX_RING * AMAX_SUB, dtype=torch.int64, device=device)
+        st = _amax_state[device] = [buf, 0, 0]
+    buf = st[0]
+    st[1] = (st[1] + 1) % _AMAX_RING
+    st[2] = st[2] + 1 if st[2] < 0x7FFFFFFF else 1
+    return buf.data_ptr() + 8 * AMAX_SUB * st[1], st[2]
+
+
+def weight_amax(w: Tensor) -> Tuple[int, int]:
+    """max |W| of a weight matrix (2-D view), cached on the tensor until its storage or version changes."""
+    key = (w.data_ptr(), w._version, tuple(w.shape))
+    c = getattr(w, "_sfx_wamax", None)
+    if c is not None and c[0] == key:
+        return c[1]
+    w2 = w.reshape(w.shape[0], -1)
+    slot = new_amax(w.device)
+    call("sfx_amax_f32", w2.shape[0], w2.shape[1], ptr(w2), w2.stride(0), slot[0], slot[1], stream())
+    w._sfx_wamax = (key, slot)
+    return slot
+
+
+def ln_amax(gamma: Tensor, beta: Tensor) -> Tuple[int, int]:
+    """Bound sqrt(C-1) max|gamma| + max|beta| of a LayerNorm's outputs, cached on gamma."""
+    key = (gamma.data_ptr(), gamma._version, beta.data_ptr(), beta._version)
+    c = getattr(gamma, "_sfx_lnamax", None)
+    if c is not None and c[0] == key:
+        return c[1]
+    slot = new_amax(gamma.device)
+    call("sfx_ln_amax_bound", gamma.shape[0], ptr(gamma), ptr(beta), slot[0], slot[1], stream())
+    gamma._sfx_lnamax = (key, slot)
+    return slot
+
+
+def _slot_args(slot: Optional[Tuple[int, int]]):
+    return (None, 0) if slot is None else slot
 
 
 def _rows(t: Tensor) -> Tuple[int, int]:
@@ -63,9 +115,13 @@ def linear(x: Tensor, weight: Tensor, bias: Optional[Tensor] = None, *, act: int
            residual_idx: Optional[Tensor] = None, out: Optional[Tensor] = None, pre_out: Optional[Tensor] = None,
            gather_idx: Optional[Tensor] = None, rows: Optional[int] = None,
            out_rows: Optional[Tensor] = None, rowscale: Optional[Tensor] = None,
-           pre_before_act: bool = False) -> Tensor:
+           pre_before_act: bool = False, a_amax: Optional[Tuple[int, int]] = None,
+           w_amax: Optional[Tuple[int, int]] = None, y_amax: bool = False):
     """y = act((x W^T + b) * scale + shift) + residual[residual_idx]  (csrc/gemm.hip: fp32-accurate MFMA GEMM,
-    3-term bf16 split operands for K >= 64, exact f32 MFMA below; SFX_GEMM_PREC=fp32 forces f32 MFMA).
+    fp16x2 split operands for K >= 64, exact f32 MFMA below; SFX_GEMM_PREC=bf16x3|fp32 select the others).
+
+    a_amax / w_amax: amax slots bounding |x| / |W| (None: the library measures them); y_amax=True returns
+    (y, slot of max |y|) for the consumer of y.
 
     With `gather_idx` [M, S] (int32, -1 = empty) the A operand is the implicit
     concatenation of S gathered rows of `x` (SubMConv3d as implicit GEMM).
@@ -89,24 +145,29 @@ def linear(x: Tensor, weight: Tensor, bias: Optional[Tensor] = None, *, act: int
     py, ldy = _rows(out)
     pr, ldr = _rows(residual) if residual is not None else (None, 0)
     pp, ldp = _rows(pre_out) if pre_out is not None else (None, 0)
+    ys = new_amax(out.device) if y_amax else None
     call("sfx_linear", M, N, K, pa, lda, ptr(gather_idx), S, pw, ldw, ptr(bias), ptr(scale), ptr(shift), act,
          act_ncols, pr, ldr, ptr(residual_idx), py, ldy, pp, ldp, 1, 0, 0, 0, 0, ptr(out_rows), ptr(rowscale),
-         1 if pre_before_act else 0, stream())
-    return out
+         1 if pre_before_act else 0, *_slot_args(a_amax), *_slot_args(w_amax), *_slot_args(ys), stream())
+    return (out, ys) if y_amax else out
 
 
 def grouped_linear(x: Tensor, weight: Tensor, bias: Tensor, groups: int, *, act: int = ACT_NONE,
-                   out: Optional[Tensor] = None) -> Tensor:
-    """Block-diagonal linear: x [M, G*K] -> [M, G*N] with weight [G, N, K], bias [G, N] (one launch)."""
+                   out: Optional[Tensor] = None, a_amax: Optional[Tuple[int, int]] = None,
+                   w_amax: Optional[Tuple[int, int]] = None, y_amax: bool = False):
+    """Block-diagonal linear: x [M, G*K] -> [M, G*N] with weight [G, N, K], bias [G, N] (one launch);
+    amax slots as in `linear`."""
     G, N, K = weight.shape
     M = x.shape[0]
     if out is None:
         out = torch.empty(M, G * N, device=x.device, dtype=torch.float32)
     pa, lda = _rows(x)
     py, ldy = _rows(out)
+    ys = new_amax(out.device) if y_amax else None
     call("sfx_linear", M, N, K, pa, lda, None, 1, ptr(weight), K, ptr(bias), None, None, act, -1, None, 0, None, py,
-         ldy, None, 0, G, K, N * K, N, N, None, None, 0, stream())
-    return out
+         ldy, None, 0, G, K, N * K, N, N, None, None, 0, *_slot_args(a_amax), *_slot_args(w_amax),
+         *_slot_args(ys), stream())
+    return (out, ys) if y_amax else out
 
 
 def layernorm(x: Tensor, gamma: Tensor, beta: Tensor, eps: float, out: Optional[Tensor] = None) -> Tensor:
@@ -285,8 +346,10 @@ def subm_neighbors(grid_coord: Tensor, batch: Optional[Tensor], with_pairs: bool
 
 
 def subm_conv(x: Tensor, smap: "SubmMap", weight: Tensor, bias: Optional[Tensor],
-              out: Optional[Tensor] = None) -> Tensor:
-    """SubMConv3d(k=3): dense centre GEMM + offset-major pair GEMM with atomic accumulation."""
+              out: Optional[Tensor] = None, x_amax: Optional[Tuple[int, int]] = None,
+              w_amax: Optional[Tuple[int, int]] = None) -> Tensor:
+    """SubMConv3d(k=3): dense centre GEMM + offset-major pair GEMM with atomic accumulation (x_amax / w_amax:
+    amax slots bounding |x| and the whole weight; None: measured by the library)."""
     n, cin = x.shape
     cout = weight.shape[0]
     if out is None:
@@ -294,7 +357,7 @@ def subm_conv(x: Tensor, smap: "SubmMap", weight: Tensor, bias: Optional[Tensor]
     px, ldx = _rows(x)
     po, ldo = _rows(out)
     call("sfx_subm_conv", n, cin, cout, px, ldx, ptr(smap.nbr), ptr(weight), ptr(bias), ptr(smap.pair_in),
-         ptr(smap.pair_out), smap._off_host, po, ldo, stream())
+         ptr(smap.pair_out), smap._off_host, po, ldo, *_slot_args(x_amax), *_slot_args(w_amax), stream())
     return out
 
 
