@@ -213,7 +213,8 @@ int sfx_cpe_residual_ln(int M, int C, const float* T, const float* X, const floa
 /* SerializedAttention (non-flash): windows win[w] = (key_start, query_start) over serialized positions,
  * qkv [N,3C] in point order, order [N] serialized->point; out[order[p]] for every query position p. */
 int sfx_window_attention(int num_windows, int window, int heads, int head_dim, int channels, const float* qkv,
-                         const int* order, const int* win, float scale, float* out, void* stream);
+                         const int* order, const int* win, float scale, float* out,
+                         const unsigned long long* qkv_amax, unsigned qkv_tag, void* stream);
 
 /* Point.serialization: codes[R][n] = batch << 3*depth | enc_t(grid) for order types t0..t3 (0 z, 1 z-trans,
  * 2 hilbert, 3 hilbert-trans) and combined sort keys r << code_bits | code; finalize turns the argsort of

@@ -22,6 +22,8 @@
 // the B operand (no LDS round trip for P).
 #include <cstdlib>
 
+#include <type_traits>
+
 #include "common.h"
 
 namespace {
@@ -167,17 +169,41 @@ window_attn_kernel(const float* __restrict__ qkv, const int* __restrict__ order,
 // swizzled by row >> 2), V^T [3][D][136] (272-byte rows; lanes dd >= D feed zero fragments); all fragment
 // reads are conflict-free.  Q never touches LDS: each lane gathers and splits its own query's 8-wide
 // slices.  31-50 KB per workgroup: 3-4 workgroups per CU to hide the row gathers.
-template <int D>
+//
+// F16 (when the caller passes an amax slot bounding |qkv|): fp16x2 terms instead -- q, k, v scaled by a
+// power of two that puts the bound in [2^14, 2^15), the unnormalised probabilities (0, 1] by 2^14, two fp16
+// terms each (sfx::split2h), three term products per block on v_mfma_f32_32x32x16_f16; S and O are unscaled
+// in registers.  Same fp32-level accuracy, half the MFMAs and two-thirds of the LDS images.
+template <int D, bool F16>
 __global__ void __launch_bounds__(256, D == 16 ? 4 : 3)
 window_attn_split_kernel(const float* __restrict__ qkv, const int* __restrict__ order, const int* __restrict__ win,
-                         int Kwin, int C, float scale, float* __restrict__ out) {
-  typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+                         int Kwin, int C, float scale, float* __restrict__ out,
+                         const unsigned long long* __restrict__ qkv_amax, unsigned qkv_tag) {
+  typedef typename std::conditional<F16, _Float16, __bf16>::type elem_t;
+  typedef elem_t bf16x8 __attribute__((ext_vector_type(8)));  // (fragment type: bf16 or fp16 terms)
+  constexpr int NT = F16 ? 2 : 3;            // terms per operand
   constexpr int KD = D == 16 ? 16 : 32;
   constexpr int NKS = KD / 16;
   constexpr int QROW = KD == 16 ? 48 : 64;  // bytes per Q/K term row
-  constexpr int VST = 136;                  // V^T row stride (bf16)
-  constexpr int QK_BYTES = 3 * KMAX * QROW;
-  constexpr int V_BYTES = 3 * D * VST * 2;
+  constexpr int VST = 136;                  // V^T row stride (16-bit elements)
+  constexpr int QK_BYTES = NT * KMAX * QROW;
+  constexpr int V_BYTES = NT * D * VST * 2;
+  // operand scales (F16): qkv by sq, probabilities by 2^14
+  float sq = 1.f, iq = 1.f;
+  if constexpr (F16) {
+    const float m = sfx::read_amax(qkv_amax, qkv_tag);
+    int e = 0;
+    if (m > 0.f && m <= 3.4028235e38f) {
+      (void)frexpf(m, &e);
+      e = 15 - e;
+      e = e > 126 ? 126 : (e < -126 ? -126 : e);
+    }
+    sq = ldexpf(1.f, e);
+    iq = ldexpf(1.f, -e);
+  }
+  auto split = [&](float4 v, float sc, uint2 (&t)[NT]) {
+    if constexpr (F16) sfx::split2h(v, sc, t); else sfx::split3(v, t);
+  };
   __shared__ __attribute__((aligned(16))) char lds[QK_BYTES + V_BYTES];
   __shared__ int rows[KMAX];
   char* Ks = lds;
@@ -195,7 +221,7 @@ window_attn_split_kernel(const float* __restrict__ qkv, const int* __restrict__ 
   if (tid < KMAX) rows[tid] = tid < Kwin ? order[key_start + tid] : -1;
   // zero padding: K columns D..KD-1 (never written by the staging below)
   if (D < KD)
-    for (int rr = tid; rr < 3 * KMAX; rr += 256)  // term rows, term-major
+    for (int rr = tid; rr < NT * KMAX; rr += 256)  // term rows, term-major
       *reinterpret_cast<uint4*>(Ks + qk_off(rr, D / 8)) = make_uint4(0, 0, 0, 0);
   __syncthreads();
   // gather + split, one matrix at a time (wave-uniform paths): q, k rows as KMAX x D/4 float4; v as
@@ -204,7 +230,7 @@ window_attn_split_kernel(const float* __restrict__ qkv, const int* __restrict__ 
   constexpr int CH = D / 4;
   typedef unsigned uintx4 __attribute__((ext_vector_type(4)));
   // this lane's query slices (B operand of S^T = K Q^T): dd = 16 ks + 8h + j, zero past D
-  bf16x8 qf[NKS][3];
+  bf16x8 qf[NKS][NT];
   {
     const int src = rows[32 * wid + l32];
 #pragma unroll
@@ -220,11 +246,11 @@ window_attn_split_kernel(const float* __restrict__ qkv, const int* __restrict__ 
       const float qs = scale * 1.4426950408889634f;
       a.x *= qs; a.y *= qs; a.z *= qs; a.w *= qs;
       b.x *= qs; b.y *= qs; b.z *= qs; b.w *= qs;
-      uint2 ta[3], tb[3];
-      sfx::split3(a, ta);
-      sfx::split3(b, tb);
+      uint2 ta[NT], tb[NT];
+      split(a, sq, ta);  // (|q * qs| <= |q|: the qkv bound holds)
+      split(b, sq, tb);
 #pragma unroll
-      for (int q = 0; q < 3; ++q) qf[ks][q] = __builtin_bit_cast(bf16x8, (uintx4){ta[q].x, ta[q].y, tb[q].x, tb[q].y});
+      for (int q = 0; q < NT; ++q) qf[ks][q] = __builtin_bit_cast(bf16x8, (uintx4){ta[q].x, ta[q].y, tb[q].x, tb[q].y});
     }
   }
   for (int e = tid; e < KMAX * CH; e += 256) {
@@ -232,11 +258,11 @@ window_attn_split_kernel(const float* __restrict__ qkv, const int* __restrict__ 
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
     const int src = rows[row];
     if (src >= 0) v = *reinterpret_cast<const float4*>(qkv + (long long)src * ld + C + head * D + 4 * ch);
-    uint2 t[3];
-    sfx::split3(v, t);
+    uint2 t[NT];
+    split(v, sq, t);
     const int o = qk_off(row, ch >> 1) + ((ch & 1) << 3);
 #pragma unroll
-    for (int q = 0; q < 3; ++q) *reinterpret_cast<uint2*>(Ks + q * KMAX * QROW + o) = t[q];
+    for (int q = 0; q < NT; ++q) *reinterpret_cast<uint2*>(Ks + q * KMAX * QROW + o) = t[q];
   }
   for (int e = tid; e < (KMAX / 2) * CH; e += 256) {
     const int kp = e / CH, ch = e - kp * CH;
@@ -245,13 +271,13 @@ window_attn_split_kernel(const float* __restrict__ qkv, const int* __restrict__ 
     float4 v0 = make_float4(0.f, 0.f, 0.f, 0.f), v1 = v0;
     if (s0 >= 0) v0 = *reinterpret_cast<const float4*>(qkv + (long long)s0 * ld + 2 * C + head * D + 4 * ch);
     if (s1 >= 0) v1 = *reinterpret_cast<const float4*>(qkv + (long long)s1 * ld + 2 * C + head * D + 4 * ch);
-    uint2 t0[3], t1[3];
-    sfx::split3(v0, t0);
-    sfx::split3(v1, t1);
+    uint2 t0[NT], t1[NT];
+    split(v0, sq, t0);
+    split(v1, sq, t1);
     const int kk = row & 15;  // even: keys row, row + 1 land on adjacent positions
     const int pos = (row & ~15) + 8 * ((kk >> 2) & 1) + (((kk >> 3) << 2) | (kk & 3));
 #pragma unroll
-    for (int q = 0; q < 3; ++q) {
+    for (int q = 0; q < NT; ++q) {
       unsigned* vt = reinterpret_cast<unsigned*>(Vt + (q * D + 4 * ch) * VST + pos);
       vt[0] = (t0[q].x & 0xffffu) | (t1[q].x << 16);
       vt[VST / 2] = (t0[q].x >> 16) | (t1[q].x & 0xffff0000u);
@@ -261,7 +287,13 @@ window_attn_split_kernel(const float* __restrict__ qkv, const int* __restrict__ 
   }
   __syncthreads();
 
-  constexpr int QA[6] = {2, 1, 0, 1, 0, 0}, QB[6] = {0, 1, 2, 0, 1, 0};
+  // term products, smallest first
+  constexpr int NP = F16 ? 3 : 6;
+  constexpr int QA[6] = {F16 ? 1 : 2, F16 ? 0 : 1, 0, 1, 0, 0}, QB[6] = {0, 1, F16 ? 0 : 2, 0, 1, 0};
+  auto mfma = [](const bf16x8& a, const bf16x8& b, floatx16 c) -> floatx16 {
+    if constexpr (F16) return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+    else return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+  };
   // S^T[key][query] for this wave's 32 queries, 4 key blocks of 32
   floatx16 s[4];
 #pragma unroll
@@ -272,15 +304,20 @@ window_attn_split_kernel(const float* __restrict__ qkv, const int* __restrict__ 
   for (int ks = 0; ks < NKS; ++ks) {
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb) {
-      bf16x8 kf[3];
+      bf16x8 kf[NT];
 #pragma unroll
-      for (int q = 0; q < 3; ++q)
+      for (int q = 0; q < NT; ++q)
         kf[q] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(
                                                Ks + q * KMAX * QROW + qk_off(kb * 32 + l32, 2 * ks + h)));
 #pragma unroll
-      for (int j = 0; j < 6; ++j)
-        s[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[QA[j]], qf[ks][QB[j]], s[kb], 0, 0, 0);
+      for (int j = 0; j < NP; ++j) s[kb] = mfma(kf[QA[j]], qf[ks][QB[j]], s[kb]);
     }
+  }
+  if constexpr (F16) {  // S was formed from sq-scaled q and k
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s[kb][r] = s[kb][r] * iq * iq;
   }
   // softmax over keys (register axis + the other half-wave); keys >= Kwin only exist in short windows
   if (Kwin < KMAX) {
@@ -318,24 +355,25 @@ window_attn_split_kernel(const float* __restrict__ qkv, const int* __restrict__ 
   for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
     for (int st = 0; st < 2; ++st) {
-      uint2 a[3], b[3];
-      // unnormalised exp values (0, 1]; 1/sum is applied to O
-      sfx::split3(make_float4(s[kb][8 * st + 0], s[kb][8 * st + 1], s[kb][8 * st + 2], s[kb][8 * st + 3]), a);
-      sfx::split3(make_float4(s[kb][8 * st + 4], s[kb][8 * st + 5], s[kb][8 * st + 6], s[kb][8 * st + 7]), b);
-      bf16x8 pf[3], vf[3];
+      uint2 a[NT], b[NT];
+      // unnormalised exp values (0, 1] (F16: scaled by 2^14); 1/sum is applied to O
+      split(make_float4(s[kb][8 * st + 0], s[kb][8 * st + 1], s[kb][8 * st + 2], s[kb][8 * st + 3]), 16384.f, a);
+      split(make_float4(s[kb][8 * st + 4], s[kb][8 * st + 5], s[kb][8 * st + 6], s[kb][8 * st + 7]), 16384.f, b);
+      bf16x8 pf[NT], vf[NT];
 #pragma unroll
-      for (int q = 0; q < 3; ++q) {
+      for (int q = 0; q < NT; ++q) {
         pf[q] = __builtin_bit_cast(bf16x8, make_uint4(a[q].x, a[q].y, b[q].x, b[q].y));
         uint4 vv = make_uint4(0, 0, 0, 0);  // dd = l32 >= D: zero rows of V^T
         if (l32 < D) vv = *reinterpret_cast<const uint4*>(Vt + (q * D + l32) * VST + (2 * kb + st) * 16 + 8 * h);
         vf[q] = __builtin_bit_cast(bf16x8, vv);
       }
 #pragma unroll
-      for (int j = 0; j < 6; ++j) o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[QA[j]], pf[QB[j]], o, 0, 0, 0);
+      for (int j = 0; j < NP; ++j) o = mfma(vf[QA[j]], pf[QB[j]], o);
     }
 
+  const float oscale = F16 ? rinv * iq * (1.f / 16384.f) : rinv;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) o[r] *= rinv;
+  for (int r = 0; r < 16; ++r) o[r] *= oscale;
   // scatter: query 32*wid + l32 (lane column), dd rows (r&3) + 8(r>>2) + 4h
   const int qi = 32 * wid + l32;
   const int qpos = key_start + qi;
@@ -597,7 +635,8 @@ extern "C" {
 
 // qkv [N, 3C] (point order), order [N] serialized->point, win [num_windows][2], out [N, C]
 int sfx_window_attention(int num_windows, int window, int heads, int head_dim, int channels, const float* qkv,
-                         const int* order, const int* win, float scale, float* out, void* stream) {
+                         const int* order, const int* win, float scale, float* out,
+                         const unsigned long long* qkv_amax, unsigned qkv_tag, void* stream) {
   SFX_REQUIRE(num_windows >= 0, "sfx_window_attention: num_windows < 0");
   SFX_REQUIRE(window >= 1 && window <= KMAX, "sfx_window_attention: window must be in [1, 128]");
   SFX_REQUIRE(heads * head_dim == channels, "sfx_window_attention: heads * head_dim != channels");
@@ -619,13 +658,18 @@ int sfx_window_attention(int num_windows, int window, int heads, int head_dim, i
       window_attn_kernel<24><<<grid, 256, 0, st>>>(qkv, order, win, window, channels, scale, out);
     else
       window_attn_kernel<32><<<grid, 256, 0, st>>>(qkv, order, win, window, channels, scale, out);
+  } else if (qkv_amax) {  // fp16x2 terms (the caller bounds |qkv|)
+#define SFX_ATTN(DD, F)                                                                                  \
+  window_attn_split_kernel<DD, F><<<grid, 256, 0, st>>>(qkv, order, win, window, channels, scale, out, qkv_amax, \
+                                                        qkv_tag)
+    if (head_dim == 16) SFX_ATTN(16, true);
+    else if (head_dim == 24) SFX_ATTN(24, true);
+    else SFX_ATTN(32, true);
   } else {
-    if (head_dim == 16)
-      window_attn_split_kernel<16><<<grid, 256, 0, st>>>(qkv, order, win, window, channels, scale, out);
-    else if (head_dim == 24)
-      window_attn_split_kernel<24><<<grid, 256, 0, st>>>(qkv, order, win, window, channels, scale, out);
-    else
-      window_attn_split_kernel<32><<<grid, 256, 0, st>>>(qkv, order, win, window, channels, scale, out);
+    if (head_dim == 16) SFX_ATTN(16, false);
+    else if (head_dim == 24) SFX_ATTN(24, false);
+    else SFX_ATTN(32, false);
+#undef SFX_ATTN
   }
   return sfx::check_launch("sfx_window_attention");
 }

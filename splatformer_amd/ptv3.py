@@ -139,7 +139,7 @@ class Block(nn.Module):
                                  w_amax=ops.weight_amax(self.attn.qkv.weight), y_amax=True)
         K, win, nw = point_windows(point, self.attn.patch_size_max)
         oi = point.order_type[self.attn.order_index]
-        a = ops.window_attention(qkv, point.order_phys[oi], win, nw, K, self.attn.num_heads, C)
+        a = ops.window_attention(qkv, point.order_phys[oi], win, nw, K, self.attn.num_heads, C, qkv_amax=q_amax)
         x2 = ops.linear(a, self.attn.proj.weight, self.attn.proj.bias, residual=x1, a_amax=q_amax,
                         w_amax=ops.weight_amax(self.attn.proj.weight))
         ln2 = self.norm2[0]

@@ -20,7 +20,7 @@ _lib.register("sfx_amax_f32", [I, I, P, L, P, I, P])
 _lib.register("sfx_ln_amax_bound", [I, P, P, P, I, P])
 _lib.register("sfx_layernorm", [I, I, P, L, P, P, F, P, L, P])
 _lib.register("sfx_cpe_residual_ln", [I, I, P, P, P, P, P, P, F, P, P, P])
-_lib.register("sfx_window_attention", [I, I, I, I, I, P, P, P, F, P, P])
+_lib.register("sfx_window_attention", [I, I, I, I, I, P, P, P, F, P, P, I, P])
 _lib.register("sfx_serialize_keys", [I, P, P, I, I, I, I, I, I, I, P, P, P])
 _lib.register("sfx_serialize_finalize", [I, I, P, P, P, P])
 _lib.register("sfx_pool_flags", [I, P, I, P, P])
@@ -209,13 +209,15 @@ def window_table(offsets: Sequence[int], K: int) -> List[Tuple[int, int]]:
 
 
 def window_attention(qkv: Tensor, order: Tensor, win: Tensor, num_windows: int, K: int, heads: int, channels: int,
-                     out: Optional[Tensor] = None) -> Tensor:
+                     out: Optional[Tensor] = None, qkv_amax: Optional[Tuple[int, int]] = None) -> Tensor:
+    """Windowed softmax attention (attention.hip); with an amax slot bounding |qkv| the MFMA terms are fp16x2,
+    otherwise bf16x3 (both fp32-accurate)."""
     n = qkv.shape[0]
     d = channels // heads
     if out is None:
         out = torch.empty(n, channels, device=qkv.device, dtype=torch.float32)
     call("sfx_window_attention", num_windows, K, heads, d, channels, ptr(qkv), ptr(order, torch.int32),
-         ptr(win, torch.int32), float(d ** -0.5), ptr(out), stream())
+         ptr(win, torch.int32), float(d ** -0.5), ptr(out), *_slot_args(qkv_amax), stream())
     return out
 
 

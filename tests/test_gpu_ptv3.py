@@ -126,11 +126,13 @@ def test_serialization_batched(device):
     assert np.array_equal(inverse.cpu().numpy(), i_ref)
 
 
+@pytest.mark.parametrize("terms", ["bf16x3", "fp16x2"])
 @pytest.mark.parametrize("n,heads,C", [(1000, 2, 64), (777, 4, 96), (300, 8, 128), (100, 2, 32)])
-def test_window_attention_vs_reference_padding(device, n, heads, C):
-    """Window table == Pointcept get_padding_and_inverse duplication semantics (incl. K = n < 128)."""
+def test_window_attention_vs_reference_padding(device, n, heads, C, terms):
+    """Window table == Pointcept get_padding_and_inverse duplication semantics (incl. K = n < 128); both MFMA
+    term forms (fp16x2 needs an amax slot bounding |qkv|: here measured, and 8x loose)."""
     g = torch.Generator().manual_seed(n)
-    qkv = torch.randn(n, 3 * C, generator=g)
+    qkv = torch.randn(n, 3 * C, generator=g) * (1e-3 if terms == "fp16x2" else 1.0)
     order = torch.randperm(n, generator=g)
     inverse = torch.empty_like(order)
     inverse[order] = torch.arange(n)
@@ -144,7 +146,14 @@ def test_window_attention_vs_reference_padding(device, n, heads, C):
     ref = (att @ v).transpose(1, 2).reshape(-1, C)[inv]
     tab = ops.window_table([n], K)
     win = torch.tensor(tab, dtype=torch.int32).to(device)
-    out = ops.window_attention(qkv.to(device), order.int().to(device), win, len(tab), K, heads, C)
+    slot = None
+    qd = qkv.to(device)
+    if terms == "fp16x2":
+        slot = ops.new_amax(qd.device)
+        big = qd * 8  # a loose bound must do as well as the exact one
+        from splatformer_amd._lib import call, ptr, stream
+        call("sfx_amax_f32", n, 3 * C, ptr(big), 3 * C, slot[0], slot[1], stream())
+    out = ops.window_attention(qd, order.int().to(device), win, len(tab), K, heads, C, qkv_amax=slot)
     assert rel_l2(out.cpu(), ref) < 2e-6
 
 
