@@ -1026,6 +1026,30 @@ void gemm_amax_jobs(const GemmArgs& a, int groups, AmaxJob& ja, AmaxJob& jw) {
   jw = AmaxJob{a.W, a.ldw, a.gW, a.N, a.K, groups, nullptr, 0, 1};
 }
 
+// Measured per-launch best (tile configuration, Stream-K) for the config-B refine's dense linears under fp16x2
+// operands (tools/gemm_tune.py, profiles/r01_gemm_tune_f16x2.jsonl) where it beats the cost model by > 2 us;
+// applied when N and K match and M is within 0.8-1.25x of the tuned M (stage point counts vary per scene).
+struct TunedLaunch {
+  int M, N, K, cfg, sk;
+};
+constexpr TunedLaunch kTuned[] = {
+    {100000, 64, 23, 2, 1},
+    {100000, 256, 64, 1, 1},
+    {90434, 128, 96, 2, 1},
+    {70349, 384, 128, 1, 0},
+    {70349, 128, 128, 2, 1},
+    {70349, 512, 128, 2, 0},
+    {70349, 128, 512, 2, 0},
+    {70349, 256, 128, 2, 1},
+    {37759, 768, 256, 6, 0},
+    {37759, 256, 256, 1, 1},
+    {37759, 256, 1024, 1, 0},
+    {37759, 512, 256, 6, 1},
+    {14764, 1536, 512, 6, 0},
+    {14764, 2048, 512, 6, 1},
+    {14764, 512, 2048, 6, 1},
+    {100000, 768, 120, 1, 0}};
+
 // tuning / test hooks: SFX_GEMM_CFG=<index into kCfgs>, SFX_GEMM_SK=0|1, or sfx_gemm_force_config()
 int forced = -2, forced_sk = -2;
 void read_force_env() {
@@ -1050,6 +1074,16 @@ int pick_cfg(GemmArgs& a, int groups, bool vec) {
                      !a.y_amax &&
                      !(a.R && a.R == a.Y) && a.M > 0 && forced_sk != 0;
   const double sk_overhead = a.pair_mode ? 2.5 : 4.0;  // slab-equivalents: partial epilogues (+ memset)
+  if (force < 0 && forced_sk < 0 && !a.pair_mode && !a.gidx && groups == 1) {
+    for (const TunedLaunch& t : kTuned) {
+      if (t.N == a.N && t.K == a.K && 5ll * a.M >= 4ll * t.M && 4ll * a.M <= 5ll * t.M &&
+          !((kCfgs[t.cfg].nw == 8) && !split)) {
+        a.sk = (t.sk && sk_ok && kCfgs[t.cfg].bm >= 128) ? 1 : 0;
+        tiles_m_of(a, kCfgs[t.cfg].bm);
+        return t.cfg;
+      }
+    }
+  }
   int best = 0;
   bool best_sk = false;
   double best_cost = 1e300;
