@@ -38,7 +38,7 @@ F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense fp16 / bf16 MFMA (no
 # fp32-equivalent ceiling is the dense fp16 peak / 3.
 SPLIT_PEAK_TFLOPS = round(F16_MFMA_PEAK_TFLOPS / 3, 1)
 # rocprofv3 FETCH_SIZE / WRITE_SIZE passes over this bench (tools/traffic_summary.py), committed per round
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r01_traffic_splitgemm.json")
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r01_traffic_f16x2.json")
 HBM_PEAK_GBS = 8000.0
 
 
