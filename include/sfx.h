@@ -223,11 +223,22 @@ int sfx_serialize_keys(int n, const int* grid_coord, const int* batch, int depth
                        int t2, int t3, int code_bits, int64_t* codes, uint64_t* keys, void* stream);
 int sfx_serialize_finalize(int n, int num_orders, const int* sorted_pos, int* order, int* inverse, void* stream);
 
-/* SerializedPooling: run heads of the code[0] >> shift sort, cluster ids / idx_ptr / head indices,
- * pooled codes+grid+batch, segment max (+BN affine +GELU) of the projected features, mean of coords. */
-int sfx_pool_flags(int n, const uint64_t* sorted_keys, int shift, int* flags, void* stream);
-int sfx_pool_assign(int n, const int* sorted_idx, const int* cid_inclusive, const int* flags, int* cluster,
-                    int* idx_ptr, int* head, void* stream);
+/* SerializedPooling (reference models/pointtransformer_v3.py:290-299 -> upstream Pointcept), sort-free: the parent's serialized
+ * orders already list every coarse cell's points contiguously (codes are hierarchical, code >> 3pd is the
+ * pooled code), so run starts replace torch.unique(code[0] >> 3pd), torch.sort(cluster) and the pooled argsort.
+ *   run_flags:   flags[r*n + j] = 1 where order row r's j-th point starts a run of equal code >> shift;
+ *                inclusive-scan the R*n flags (sfx_scan_i32) into `pos`; every row must count the same m runs.
+ *   assign_runs: row0 (the first order type): cluster id per point (pooling_inverse), CSR members
+ *                (sorted_idx, idx_ptr[m+1]; members in row0 order), one head point per cluster.
+ *   reorder:     order / inverse [R][m] of the pooled points for every row.
+ *   gather:      pooled codes [R][m], grid >> pd, batch from the heads (keys may be NULL).
+ * Then segment max (+BN affine +GELU) of the projected features and the mean of the coords. */
+int sfx_pool_run_flags(int n, int num_orders, const int* order, const int64_t* codes, int shift, int* flags,
+                       void* stream);
+int sfx_pool_assign_runs(int n, int m, int row0, const int* order, const int* pos, const int* flags, int* cluster,
+                         int* idx_ptr, int* head, int* sorted_idx, void* stream);
+int sfx_pool_reorder(int n, int m, int num_orders, const int* order, const int* pos, const int* flags,
+                     const int* cluster, int* new_order, int* new_inverse, void* stream);
 int sfx_pool_gather(int m, int n, int num_orders, const int* head, const int64_t* codes, int pooling_depth,
                     const int* grid_coord, const int* batch, int code_bits, int64_t* new_codes, uint64_t* keys,
                     int* new_grid, int* new_batch, void* stream);

@@ -94,25 +94,51 @@ __global__ void serialize_finalize_kernel(int n, int R, const int* __restrict__ 
 }
 
 // ---- pooling -------------------------------------------------------------
-__global__ void pool_flags_kernel(int n, const uint64_t* __restrict__ sorted_keys, int shift, int* __restrict__ flags) {
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= n) return;
-  flags[p] = (p == 0 || (sorted_keys[p] >> shift) != (sorted_keys[p - 1] >> shift)) ? 1 : 0;
+// Sort-free SerializedPooling.  Every order type's code is hierarchical: code_r(g) >> 3pd == code_r(g >> pd) at
+// depth - pd (z-order and Hilbert alike, batch bits on top), so along the parent's sorted order of row r the
+// points of one coarse cell (= one cluster) are contiguous and the runs appear in ascending pooled-code order.
+// Run starts therefore give torch.unique(code[0] >> 3pd) (row0) and the argsort of the pooled codes (every row)
+// without sorting anything.  Each row holds exactly m runs; the host checks that before the assign kernels run.
+__global__ void pool_run_flags_kernel(int n, int R, const int* __restrict__ order, const int64_t* __restrict__ codes,
+                                      int shift, int* __restrict__ flags) {
+  const long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= (long long)R * n) return;
+  const int r = (int)(q / n), j = (int)(q - (long long)r * n);
+  const int64_t* cr = codes + (long long)r * n;
+  const uint64_t c = (uint64_t)cr[order[q]] >> shift;
+  flags[q] = (j == 0 || c != ((uint64_t)cr[order[q - 1]] >> shift)) ? 1 : 0;
 }
 
-__global__ void pool_assign_kernel(int n, const int* __restrict__ sorted_idx, const int* __restrict__ cid_incl,
-                                   const int* __restrict__ flags, int* __restrict__ cluster, int* __restrict__ idx_ptr,
-                                   int* __restrict__ head) {
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= n) return;
-  const int c = cid_incl[p] - 1;
-  const int src = sorted_idx[p];
-  cluster[src] = c;
-  if (flags[p]) {
-    idx_ptr[c] = p;
-    head[c] = src;
+// row0's runs -> cluster id of every point, CSR of the members (sidx / idx_ptr), one head per cluster
+__global__ void pool_assign_runs_kernel(int n, int m, int row0, const int* __restrict__ order,
+                                        const int* __restrict__ pos, const int* __restrict__ flags,
+                                        int* __restrict__ cluster, int* __restrict__ idx_ptr, int* __restrict__ head,
+                                        int* __restrict__ sidx) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const long long q = (long long)row0 * n + j;
+  const int p = order[q];
+  const int c = pos[q] - 1 - row0 * m;
+  cluster[p] = c;
+  sidx[j] = p;
+  if (flags[q]) {
+    idx_ptr[c] = j;
+    head[c] = p;
   }
-  if (p == n - 1) idx_ptr[c + 1] = n;
+  if (j == n - 1) idx_ptr[m] = n;
+}
+
+// every row's runs -> order / inverse of the pooled points (the argsort of the pooled codes)
+__global__ void pool_reorder_kernel(int n, int m, int R, const int* __restrict__ order, const int* __restrict__ pos,
+                                    const int* __restrict__ flags, const int* __restrict__ cluster,
+                                    int* __restrict__ new_order, int* __restrict__ new_inverse) {
+  const long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= (long long)R * n || !flags[q]) return;
+  const int r = (int)(q / n);
+  const int k = pos[q] - 1 - r * m;
+  const int c = cluster[order[q]];
+  new_order[(long long)r * m + k] = c;
+  new_inverse[(long long)r * m + c] = k;
 }
 
 // new codes / grid / batch of the pooled point; keys for the combined sort
@@ -127,7 +153,7 @@ __global__ void pool_gather_kernel(int m, int n, int R, const int* __restrict__ 
   for (int r = 0; r < R; ++r) {
     const uint64_t code = ((uint64_t)codes[(long long)r * n + hd]) >> (3 * pd);
     new_codes[(long long)r * m + c] = (int64_t)code;
-    keys[(long long)r * m + c] = ((uint64_t)r << code_bits) | code;
+    if (keys) keys[(long long)r * m + c] = ((uint64_t)r << code_bits) | code;
   }
   for (int k = 0; k < 3; ++k) new_grid[3 * c + k] = grid[3 * hd + k] >> pd;
   if (new_batch) new_batch[c] = batch ? batch[hd] : 0;
@@ -189,22 +215,38 @@ int sfx_serialize_finalize(int n, int num_orders, const int* sorted_pos, int* or
   return sfx::check_launch("sfx_serialize_finalize");
 }
 
-int sfx_pool_flags(int n, const uint64_t* sorted_keys, int shift, int* flags, void* stream) {
-  SFX_REQUIRE(n >= 0 && shift >= 0 && shift < 64, "sfx_pool_flags: bad args");
+int sfx_pool_run_flags(int n, int num_orders, const int* order, const int64_t* codes, int shift, int* flags,
+                       void* stream) {
+  SFX_REQUIRE(n >= 0 && num_orders >= 1 && shift >= 0 && shift < 64, "sfx_pool_run_flags: bad args");
   if (n == 0) return SFX_OK;
-  SFX_REQUIRE(sorted_keys && flags, "sfx_pool_flags: null buffer");
-  pool_flags_kernel<<<sfx::ceil_div(n, 256), 256, 0, sfx::as_stream(stream)>>>(n, sorted_keys, shift, flags);
-  return sfx::check_launch("sfx_pool_flags");
+  SFX_REQUIRE(order && codes && flags, "sfx_pool_run_flags: null buffer");
+  const long long tot = (long long)n * num_orders;
+  pool_run_flags_kernel<<<sfx::ceil_div(tot, 256), 256, 0, sfx::as_stream(stream)>>>(n, num_orders, order, codes,
+                                                                                     shift, flags);
+  return sfx::check_launch("sfx_pool_run_flags");
 }
 
-int sfx_pool_assign(int n, const int* sorted_idx, const int* cid_inclusive, const int* flags, int* cluster,
-                    int* idx_ptr, int* head, void* stream) {
-  SFX_REQUIRE(n >= 0, "sfx_pool_assign: n < 0");
+int sfx_pool_assign_runs(int n, int m, int row0, const int* order, const int* pos, const int* flags, int* cluster,
+                         int* idx_ptr, int* head, int* sorted_idx, void* stream) {
+  SFX_REQUIRE(n >= 0 && m >= 0 && m <= n && row0 >= 0, "sfx_pool_assign_runs: bad sizes");
   if (n == 0) return SFX_OK;
-  SFX_REQUIRE(sorted_idx && cid_inclusive && flags && cluster && idx_ptr && head, "sfx_pool_assign: null buffer");
-  pool_assign_kernel<<<sfx::ceil_div(n, 256), 256, 0, sfx::as_stream(stream)>>>(n, sorted_idx, cid_inclusive, flags,
-                                                                                 cluster, idx_ptr, head);
-  return sfx::check_launch("sfx_pool_assign");
+  SFX_REQUIRE(order && pos && flags && cluster && idx_ptr && head && sorted_idx, "sfx_pool_assign_runs: null buffer");
+  pool_assign_runs_kernel<<<sfx::ceil_div(n, 256), 256, 0, sfx::as_stream(stream)>>>(n, m, row0, order, pos, flags,
+                                                                                     cluster, idx_ptr, head,
+                                                                                     sorted_idx);
+  return sfx::check_launch("sfx_pool_assign_runs");
+}
+
+int sfx_pool_reorder(int n, int m, int num_orders, const int* order, const int* pos, const int* flags,
+                     const int* cluster, int* new_order, int* new_inverse, void* stream) {
+  SFX_REQUIRE(n >= 0 && m >= 0 && m <= n && num_orders >= 1, "sfx_pool_reorder: bad sizes");
+  if (n == 0) return SFX_OK;
+  SFX_REQUIRE(order && pos && flags && cluster && new_order && new_inverse, "sfx_pool_reorder: null buffer");
+  const long long tot = (long long)n * num_orders;
+  pool_reorder_kernel<<<sfx::ceil_div(tot, 256), 256, 0, sfx::as_stream(stream)>>>(n, m, num_orders, order, pos,
+                                                                                   flags, cluster, new_order,
+                                                                                   new_inverse);
+  return sfx::check_launch("sfx_pool_reorder");
 }
 
 int sfx_pool_gather(int m, int n, int num_orders, const int* head, const int64_t* codes, int pooling_depth,
@@ -212,7 +254,7 @@ int sfx_pool_gather(int m, int n, int num_orders, const int* head, const int64_t
                     int* new_grid, int* new_batch, void* stream) {
   SFX_REQUIRE(m >= 0 && n >= m && num_orders >= 1 && pooling_depth >= 0, "sfx_pool_gather: bad sizes");
   if (m == 0) return SFX_OK;
-  SFX_REQUIRE(head && codes && grid_coord && new_codes && keys && new_grid, "sfx_pool_gather: null buffer");
+  SFX_REQUIRE(head && codes && grid_coord && new_codes && new_grid, "sfx_pool_gather: null buffer");
   pool_gather_kernel<<<sfx::ceil_div(m, 256), 256, 0, sfx::as_stream(stream)>>>(
       m, n, num_orders, head, codes, pooling_depth, grid_coord, batch, nullptr, code_bits, new_codes, keys, new_grid,
       new_batch);

@@ -184,12 +184,11 @@ class SerializedPooling(nn.Module):
         pd = (math.ceil(self.stride) - 1).bit_length()
         if pd > point.serialized_depth:
             pd = 0
-        row0 = point.order_type[0]
-        sidx, cluster, idx_ptr, head, m = ops.pool_clusters(point.codes_phys[row0], pd, point.code_bits)
         depth = point.serialized_depth - pd
         code_bits = point.code_bits - 3 * pd
-        codes, order, inverse, grid, batch = ops.pool_gather(head, m, point.codes_phys, pd, point.grid_coord,
-                                                             point.get("batch"), code_bits)
+        sidx, cluster, idx_ptr, m, codes, order, inverse, grid, batch = ops.pool_geometry(
+            point.codes_phys, point.order_phys, point.order_type[0], pd, point.grid_coord, point.get("batch"),
+            point.code_bits)
         coord = ops.segment_mean(point.coord, idx_ptr, sidx, m)
         new = Point(coord=coord, grid_coord=grid, codes_phys=codes, order_phys=order,
                     inverse_phys=inverse, order_type=[point.order_type[p] for p in perm],

@@ -23,8 +23,9 @@ _lib.register("sfx_cpe_residual_ln", [I, I, P, P, P, P, P, P, F, P, P, P])
 _lib.register("sfx_window_attention", [I, I, I, I, I, P, P, P, F, P, P, I, P])
 _lib.register("sfx_serialize_keys", [I, P, P, I, I, I, I, I, I, I, P, P, P])
 _lib.register("sfx_serialize_finalize", [I, I, P, P, P, P])
-_lib.register("sfx_pool_flags", [I, P, I, P, P])
-_lib.register("sfx_pool_assign", [I, P, P, P, P, P, P, P])
+_lib.register("sfx_pool_run_flags", [I, I, P, P, I, P, P])
+_lib.register("sfx_pool_assign_runs", [I, I, I, P, P, P, P, P, P, P, P])
+_lib.register("sfx_pool_reorder", [I, I, I, P, P, P, P, P, P, P])
 _lib.register("sfx_pool_gather", [I, I, I, P, P, I, P, P, I, P, P, P, P, P])
 _lib.register("sfx_segment_max_affine_act", [I, I, P, P, P, P, P, I, P, P])
 _lib.register("sfx_segment_mean", [I, I, P, P, P, P, P])
@@ -261,34 +262,39 @@ def scan_i32(x: Tensor, inclusive: bool = True) -> Tuple[Tensor, Tensor]:
     return out, total
 
 
-def pool_clusters(code_row: Tensor, pooling_depth: int, code_bits: int):
-    """torch.unique(code >> 3pd) + sort(cluster) on device: returns (sorted_idx, cluster, idx_ptr, head, m)."""
-    n = code_row.shape[0]
-    dev = code_row.device
-    sk, sidx = _sort(code_row, None, 3 * pooling_depth, code_bits)
-    flags = torch.empty(n, device=dev, dtype=torch.int32)
-    call("sfx_pool_flags", n, ptr(sk), 3 * pooling_depth, ptr(flags), stream())
-    cid, total = scan_i32(flags)
-    m = int(total.item())  # host sync: the pooled point count sizes every later buffer
-    cluster = torch.empty(n, device=dev, dtype=torch.int32)
-    idx_ptr = torch.empty(m + 1, device=dev, dtype=torch.int32)
-    head = torch.empty(m, device=dev, dtype=torch.int32)
-    call("sfx_pool_assign", n, ptr(sidx), ptr(cid), ptr(flags), ptr(cluster), ptr(idx_ptr), ptr(head), stream())
-    return sidx, cluster, idx_ptr, head, m
-
-
-def pool_gather(head: Tensor, m: int, codes: Tensor, pooling_depth: int, grid_coord: Tensor, batch: Optional[Tensor],
-                code_bits: int):
+def pool_geometry(codes: Tensor, order: Tensor, row0: int, pooling_depth: int, grid_coord: Tensor,
+                  batch: Optional[Tensor], code_bits: int):
+    """SerializedPooling's integer half without a sort (serialize.hip): runs of equal code >> 3pd along the
+    parent's serialized orders are the clusters, in ascending pooled-code order for every row.
+    -> (sorted_idx, cluster, idx_ptr, m, new codes [R,m], new order, new inverse, new grid, new batch)."""
     R, n = codes.shape
     dev = codes.device
+    shift = 3 * pooling_depth
+    flags = torch.empty(R * n, device=dev, dtype=torch.int32)
+    call("sfx_pool_run_flags", n, R, ptr(order, torch.int32), ptr(codes, torch.int64), shift, ptr(flags), stream())
+    pos, _ = scan_i32(flags)
+    ends = pos.view(R, n)[:, -1].cpu().tolist()  # host sync: the pooled point count sizes every later buffer
+    runs = [ends[0]] + [ends[r] - ends[r - 1] for r in range(1, R)]
+    m = runs[0]
+    if any(c != m for c in runs):
+        raise RuntimeError(f"sfx pooling: order rows count different cluster runs {runs}; the serialization codes "
+                           "are not hierarchical (code >> 3 must be the parent cell's code)")
+    cluster = torch.empty(n, device=dev, dtype=torch.int32)
+    sidx = torch.empty(n, device=dev, dtype=torch.int32)
+    idx_ptr = torch.empty(m + 1, device=dev, dtype=torch.int32)
+    head = torch.empty(m, device=dev, dtype=torch.int32)
+    call("sfx_pool_assign_runs", n, m, row0, ptr(order), ptr(pos), ptr(flags), ptr(cluster), ptr(idx_ptr),
+         ptr(head), ptr(sidx), stream())
+    new_order = torch.empty(R, m, device=dev, dtype=torch.int32)
+    new_inverse = torch.empty(R, m, device=dev, dtype=torch.int32)
+    call("sfx_pool_reorder", n, m, R, ptr(order), ptr(pos), ptr(flags), ptr(cluster), ptr(new_order),
+         ptr(new_inverse), stream())
     new_codes = torch.empty(R, m, device=dev, dtype=torch.int64)
-    keys = torch.empty(R * m, device=dev, dtype=torch.int64)
     new_grid = torch.empty(m, 3, device=dev, dtype=torch.int32)
     new_batch = torch.empty(m, device=dev, dtype=torch.int32) if batch is not None else None
-    call("sfx_pool_gather", m, n, R, ptr(head), ptr(codes), pooling_depth, ptr(grid_coord), ptr(batch), code_bits,
-         ptr(new_codes), ptr(keys), ptr(new_grid), ptr(new_batch), stream())
-    order, inverse = _finalize(keys, m, R, code_bits)
-    return new_codes, order, inverse, new_grid, new_batch
+    call("sfx_pool_gather", m, n, R, ptr(head), ptr(codes), pooling_depth, ptr(grid_coord), ptr(batch),
+         code_bits - shift, ptr(new_codes), None, ptr(new_grid), ptr(new_batch), stream())
+    return sidx, cluster, idx_ptr, m, new_codes, new_order, new_inverse, new_grid, new_batch
 
 
 def segment_max_affine_act(x: Tensor, idx_ptr: Tensor, sorted_idx: Tensor, m: int, scale: Optional[Tensor],

@@ -126,6 +126,65 @@ def test_serialization_batched(device):
     assert np.array_equal(inverse.cpu().numpy(), i_ref)
 
 
+@pytest.mark.parametrize("stride,B,perm,res", [(2, 1, [0, 1, 2, 3], 384), (2, 3, [2, 0, 3, 1], 384),
+                                              (4, 2, [3, 2, 1, 0], 384), (2, 1, [1, 3, 0, 2], 1)])
+def test_pooling_geometry_exact(device, stride, B, perm, res):
+    """Sort-free SerializedPooling geometry vs the reference's integer math (pointtransformer_v3.py:290-299 ->
+    Pointcept SerializedPooling: torch.unique(code[0] >> 3pd), stable sort(cluster), argsort of the pooled
+    codes): clusters, CSR pointers, pooled codes / orders / inverses / grid / batch bit-exact; the members of a
+    cluster as a set (listed in row0 serialized order here, index order in the reference); pooled coords
+    (an fp32 mean of the same members in that order) to 1e-6."""
+    from splatformer_amd.ptv3 import Point, SerializedPooling
+    s = make_scene(5000, 1, seed=11, unique_voxels=False)
+    grid = torch.floor(s["means"] * res).int()
+    n = grid.shape[0]
+    cuts = [0] + sorted(torch.randperm(n - 1, generator=torch.Generator().manual_seed(3))[:B - 1].add(1).tolist()) \
+        + [n]
+    batch = torch.repeat_interleave(torch.arange(B), torch.tensor(np.diff(cuts)))
+    depth = int(grid.max()).bit_length()
+    cb = 3 * depth + max(0, (B - 1).bit_length())
+    bt = batch.int().to(device) if B > 1 else None
+    codes, order, inverse = ops.serialize(grid.to(device), bt, depth, cb, ptv3_ref.ORDERS)
+    pt = Point(coord=s["means"].to(device), grid_coord=grid.to(device), offset=cuts[1:], codes_phys=codes,
+               order_phys=order, inverse_phys=inverse, order_type=list(perm), serialized_depth=depth, code_bits=cb)
+    if bt is not None:
+        pt.batch = bt
+    new, sidx, idx_ptr, m = SerializedPooling(8, 8, stride=stride, norm_layer=torch.nn.BatchNorm1d,
+                                                  act_layer=torch.nn.GELU).geometry(pt, [0, 1, 2, 3])
+
+    # the reference's integer math on the oracle's serialization, rows in logical (permuted) order
+    c_ref, _, _, _ = serialize_ref.serialization(grid.numpy(), batch.numpy(), ptv3_ref.ORDERS, None)
+    code = torch.from_numpy(c_ref)[perm]
+    pd = (stride - 1).bit_length()
+    if pd > depth:
+        pd = 0
+    code = code >> 3 * pd
+    _, cluster, counts = torch.unique(code[0], sorted=True, return_inverse=True, return_counts=True)
+    indices = torch.sort(cluster, stable=True).indices
+    ptr_ref = torch.cat([counts.new_zeros(1), torch.cumsum(counts, 0)])
+    head = indices[ptr_ref[:-1]]
+    code_h = code[:, head]
+    order_ref = torch.argsort(code_h, stable=True)
+    inv_ref = torch.zeros_like(order_ref).scatter_(1, order_ref, torch.arange(code_h.shape[1]).repeat(4, 1))
+
+    assert m == len(counts)
+    assert torch.equal(new.pooling_inverse.cpu().long(), cluster)
+    assert torch.equal(idx_ptr.cpu().long(), ptr_ref)
+    rows = new.order_type  # logical -> physical rows of the pooled point
+    assert torch.equal(new.codes_phys.cpu()[rows], code_h)
+    assert torch.equal(new.order_phys.cpu().long()[rows], order_ref)
+    assert torch.equal(new.inverse_phys.cpu().long()[rows], inv_ref)
+    assert torch.equal(new.grid_coord.cpu(), grid[head] >> pd)
+    if B > 1:
+        assert torch.equal(new.batch.cpu().long(), batch[head])
+        assert new.offset == torch.cumsum(torch.bincount(batch[head]), 0).tolist()
+    seg = torch.repeat_interleave(torch.arange(m), counts)
+    key = seg * n + sidx.cpu().long()
+    assert torch.equal(torch.sort(key).values, seg * n + indices)  # same members per cluster
+    mean = torch.zeros(m, 3, dtype=torch.float64).index_add_(0, seg, s["means"][indices].double()) / counts[:, None]
+    assert torch.allclose(new.coord.cpu().double(), mean, rtol=1e-6, atol=1e-7)
+
+
 @pytest.mark.parametrize("terms", ["bf16x3", "fp16x2"])
 @pytest.mark.parametrize("n,heads,C", [(1000, 2, 64), (777, 4, 96), (300, 8, 128), (100, 2, 32)])
 def test_window_attention_vs_reference_padding(device, n, heads, C, terms):
