@@ -100,6 +100,25 @@ def call(name: str, *args) -> None:
         raise RuntimeError(f"{name} failed ({rc}): {msg.decode() if msg else ''}")
 
 
+class HostRead:
+    """Asynchronous device -> pinned-host copy of a small tensor: `get()` waits only for the work enqueued before
+    the copy, so GPU work enqueued between the two keeps the device busy while the host waits (the sizes that
+    must reach the host -- pooled point counts, pair offsets, the grid depth -- cost no queue drain)."""
+
+    def __init__(self, t: torch.Tensor):
+        self._h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+        self._h.copy_(t, non_blocking=True)
+        self._ev = torch.cuda.Event()
+        self._ev.record()
+        self._v = None
+
+    def get(self) -> list:
+        if self._v is None:
+            self._ev.synchronize()
+            self._v = self._h.tolist()
+        return self._v
+
+
 def require_gpu(t: torch.Tensor | None = None) -> None:
     if not torch.cuda.is_available():
         raise RuntimeError("splatformer_amd requires a ROCm GPU (MI355X); no device is visible")

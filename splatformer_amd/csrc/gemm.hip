@@ -36,6 +36,17 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 constexpr int BK = 32;
+// residency: persistent workgroups per CU for the four- and eight-wave tiles, LDS buffers of the eight-wave ones
+#ifndef SFX_PERCU4
+#define SFX_PERCU4 2
+#endif
+#ifndef SFX_PERCU8
+#define SFX_PERCU8 1
+#endif
+#ifndef SFX_NBUF8
+#define SFX_NBUF8 2
+#endif
+constexpr int kPerCu4 = SFX_PERCU4, kPerCu8 = SFX_PERCU8;
 constexpr int LDS_STRIDE = BK + 4;
 constexpr int THREADS = 256;
 constexpr unsigned OOB = 0x7ffffff0u;        // byte offset past every descriptor extent
@@ -185,7 +196,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs
   static_assert(SPLIT || NW == 4, "fp32 tiles run 4 waves");
   constexpr int A_ITERS = BM * BK / 4 / NT;
   constexpr int W_ITERS = BN * BK / 4 / NT;
-  constexpr int NBUF = SPLIT ? (NW == 8 ? 2 : 1) : 2;
+  constexpr int NBUF = SPLIT ? (NW == 8 ? SFX_NBUF8 : 1) : 2;
   // fp32: double-buffered [row][k] images (row stride 36); SPLIT: NBUF x 3 swizzled bf16 term images
   constexpr int A_FLOATS = SPLIT ? NBUF * NTERM * BM * BK / 2 : 2 * BM * LDS_STRIDE;
   constexpr int W_FLOATS = SPLIT ? NBUF * NTERM * BN * BK / 2 : 2 * BN * LDS_STRIDE;
@@ -849,7 +860,7 @@ void launch(GemmArgs a, int groups, bool vec, hipStream_t st) {
   const int total = tiles_m * tiles_n;
   // persistent grid: 2 four-wave or 1 eight-wave workgroup per CU (LDS/VGPR bound), balanced so every
   // workgroup gets the same number of tiles (+-1)
-  const int per_cu = NW == 4 ? 2 : 1;
+  const int per_cu = NW == 4 ? kPerCu4 : kPerCu8;
   const int slots = per_cu * num_cus() / groups > 0 ? per_cu * num_cus() / groups : 1;
   int grid_x;
   if (a.sk) {
@@ -1090,9 +1101,10 @@ int pick_cfg(GemmArgs& a, int groups, bool vec) {
   for (int c = 0; c < kNumCfgs; ++c) {
     if (force >= 0 && c != force) continue;
     if (kCfgs[c].nw == 8 && !split) continue;
-    const long long slots = (kCfgs[c].nw == 4 ? 2ll : 1ll) * num_cus() / groups;
-    // tile area per unit of CU throughput (an eight-wave tile has the whole CU, a four-wave one half)
-    const double area = (double)kCfgs[c].bm * kCfgs[c].bn / kCfgs[c].eff / (kCfgs[c].nw / 4);
+    const int per_cu = kCfgs[c].nw == 4 ? kPerCu4 : kPerCu8;
+    const long long slots = (long long)per_cu * num_cus() / groups;
+    // tile area per unit of CU throughput (a resident tile has 1 / per_cu of its CU)
+    const double area = (double)kCfgs[c].bm * kCfgs[c].bn / kCfgs[c].eff * per_cu / 2;
     const long long tiles = (long long)tiles_m_of(a, kCfgs[c].bm) * sfx::ceil_div(a.N, kCfgs[c].bn) * groups;
     const long long rounds = (tiles + slots - 1) / slots;
     // cost in slab-area units: K slabs + ~1 slab-equivalent of epilogue per tile

@@ -143,8 +143,10 @@ class FeaturePredictor(nn.Module):
         grid = torch.empty(n, 3, device=dev, dtype=torch.int32)
         gmax = torch.zeros(1, device=dev, dtype=torch.int32)
         ops.gs_pack(gs, feat, float(self.grid_resolution), grid, gmax)
-        depth = int(gmax.item()).bit_length()  # host sync (Pointcept: int(grid_coord.max()).bit_length())
-        data = {"coord": means, "grid_coord": grid, "offset": [n], "feat": feat, "serialized_depth": depth}
+        # Pointcept: int(grid_coord.max()).bit_length(), read back asynchronously (the backbone's embedding
+        # GEMM runs while the host waits for it)
+        data = {"coord": means, "grid_coord": grid, "offset": [n], "feat": feat,
+                "serialized_depth": _lib.HostRead(gmax)}
         self.backbone(data, perms=perms, out=h0[:, :cb])
         w1, b1, mids, wl, bl, out_dim = self._packed_heads()
         x = h0[:, :w1.shape[1]]  # [y | feat | 0-pad]

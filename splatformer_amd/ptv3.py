@@ -178,16 +178,21 @@ class SerializedPooling(nn.Module):
         self.norm = PointSequential(norm_layer(out_channels))
         self.act = PointSequential(act_layer())
 
-    def geometry(self, point: Point, perm: Sequence[int]):
-        """The integer half of SerializedPooling.forward: clusters (code >> 3*pd, unique), their sorted members
-        (sidx / idx_ptr CSR), the pooled coords, codes, orders and neighbour map.  -> (new Point, sidx, idx_ptr, m)"""
+    def _pd(self, point: Point) -> int:
         pd = (math.ceil(self.stride) - 1).bit_length()
-        if pd > point.serialized_depth:
-            pd = 0
+        return 0 if pd > point.serialized_depth else pd
+
+    def geometry_begin(self, point: Point):
+        return ops.pool_geometry_begin(point.codes_phys, point.order_phys, self._pd(point))
+
+    def geometry_end(self, point: Point, perm: Sequence[int], state):
+        """The integer half of SerializedPooling.forward: clusters (code >> 3*pd, unique), their members
+        (sidx / idx_ptr CSR), the pooled coords, codes, orders and neighbour map.  -> (new Point, sidx, idx_ptr, m)"""
+        pd = self._pd(point)
         depth = point.serialized_depth - pd
         code_bits = point.code_bits - 3 * pd
-        sidx, cluster, idx_ptr, m, codes, order, inverse, grid, batch = ops.pool_geometry(
-            point.codes_phys, point.order_phys, point.order_type[0], pd, point.grid_coord, point.get("batch"),
+        sidx, cluster, idx_ptr, m, codes, order, inverse, grid, batch = ops.pool_geometry_end(
+            state, point.codes_phys, point.order_phys, point.order_type[0], pd, point.grid_coord, point.get("batch"),
             point.code_bits)
         coord = ops.segment_mean(point.coord, idx_ptr, sidx, m)
         new = Point(coord=coord, grid_coord=grid, codes_phys=codes, order_phys=order,
@@ -201,10 +206,15 @@ class SerializedPooling(nn.Module):
         new.nbr = ops.subm_neighbors(grid, new.get("batch"))
         return new, sidx, idx_ptr, m
 
+    def geometry(self, point: Point, perm: Sequence[int]):
+        return self.geometry_end(point, perm, self.geometry_begin(point))
+
     def run(self, point: Point, perm: Sequence[int]) -> Point:
-        new, sidx, idx_ptr, m = self.geometry(point, perm)
+        st = self.geometry_begin(point)
+        # the projection does not depend on the clusters: enqueued while the host waits for the pooled count
         pf = ops.linear(point.feat, self.proj.weight, self.proj.bias, a_amax=point.get("feat_amax"),
                         w_amax=ops.weight_amax(self.proj.weight))
+        new, sidx, idx_ptr, m = self.geometry_end(point, perm, st)
         sc, sh = bn_affine(self.norm[0])
         new.feat = ops.segment_max_affine_act(pf, idx_ptr, sidx, m, sc, sh, ops.ACT_GELU)
         return new
@@ -241,9 +251,8 @@ def point_windows(point: Point, patch_size_max: int):
     K = min(min(counts), patch_size_max)
     key = ("win", K)
     if key not in point:
-        tab = ops.window_table(point.offset, K)
-        t = torch.tensor(tab, dtype=torch.int32).reshape(-1, 2)
-        point[key] = (t.to(point.feat.device, non_blocking=False), len(tab))
+        t = torch.from_numpy(ops.window_table_np(point.offset, K)).pin_memory()
+        point[key] = (t.to(point.feat.device, non_blocking=True), t.shape[0])  # no queue drain
     win, nw = point[key]
     return K, win, nw
 
@@ -333,8 +342,11 @@ class PointTransformerV3(nn.Module):
             batch = torch.empty(n, device=dev, dtype=torch.int32)
             offs = torch.tensor(offset, dtype=torch.int64, device=dev)
             _lib.call("sfx_offsets_to_batch", n, B, offs.data_ptr(), batch.data_ptr(), _lib.stream())
-        depth = int(data_dict["serialized_depth"]) if "serialized_depth" in data_dict else \
-            int(grid.max().item()).bit_length()
+        d = data_dict.get("serialized_depth")
+        if isinstance(d, _lib.HostRead):  # the grid max, read back while the embedding runs
+            depth = int(d.get()[0]).bit_length()
+        else:
+            depth = int(d) if d is not None else int(grid.max().item()).bit_length()
         assert depth * 3 + len(offset).bit_length() <= 63 and depth <= 16
         code_bits = 3 * depth + max(0, (B - 1).bit_length())
         self.last_perms = []
@@ -350,12 +362,15 @@ class PointTransformerV3(nn.Module):
 
     @torch.no_grad()
     def forward(self, data_dict, perms: Optional[List[Sequence[int]]] = None, out: Optional[Tensor] = None) -> Point:
-        point = self.prepare(data_dict, perms)
         feat = data_dict["feat"]
+        _lib.require_gpu(feat)
         emb, bnm = self.embedding[0], self.embedding[1]
         sc, sh = bn_affine(bnm)
-        point.feat, point.feat_amax = ops.linear(feat, emb.weight, emb.bias, scale=sc, shift=sh, act=ops.ACT_GELU,
-                                                 y_amax=True)
+        # the embedding needs no geometry: enqueued first, it runs while prepare() waits for the grid depth
+        emb_feat, emb_amax = ops.linear(feat, emb.weight, emb.bias, scale=sc, shift=sh, act=ops.ACT_GELU,
+                                        y_amax=True)
+        point = self.prepare(data_dict, perms)
+        point.feat, point.feat_amax = emb_feat, emb_amax
         k = 1
         for s in range(self.num_stages):
             stage = getattr(self.enc, f"enc{s}")

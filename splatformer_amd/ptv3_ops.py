@@ -8,6 +8,7 @@ from __future__ import annotations
 
 from typing import List, Optional, Sequence, Tuple
 
+import numpy as np
 import torch
 from torch import Tensor
 
@@ -209,6 +210,21 @@ def window_table(offsets: Sequence[int], K: int) -> List[Tuple[int, int]]:
     return tab
 
 
+def window_table_np(offsets: Sequence[int], K: int) -> np.ndarray:
+    """window_table as an int32 [num_windows, 2] array (vectorised)."""
+    parts = []
+    start = 0
+    for end in offsets:
+        n = end - start
+        nw = (n + K - 1) // K
+        qs = start + K * np.arange(nw, dtype=np.int64)
+        ks = np.minimum(qs, end - K)  # ragged last window: padded with the preceding real points
+        parts.append(np.stack([ks, qs], 1))
+        start = end
+    tab = np.concatenate(parts) if parts else np.zeros((0, 2), np.int64)
+    return np.ascontiguousarray(tab, dtype=np.int32)
+
+
 def window_attention(qkv: Tensor, order: Tensor, win: Tensor, num_windows: int, K: int, heads: int, channels: int,
                      out: Optional[Tensor] = None, qkv_amax: Optional[Tuple[int, int]] = None) -> Tensor:
     """Windowed softmax attention (attention.hip); with an amax slot bounding |qkv| the MFMA terms are fp16x2,
@@ -262,18 +278,24 @@ def scan_i32(x: Tensor, inclusive: bool = True) -> Tuple[Tensor, Tensor]:
     return out, total
 
 
-def pool_geometry(codes: Tensor, order: Tensor, row0: int, pooling_depth: int, grid_coord: Tensor,
-                  batch: Optional[Tensor], code_bits: int):
-    """SerializedPooling's integer half without a sort (serialize.hip): runs of equal code >> 3pd along the
-    parent's serialized orders are the clusters, in ascending pooled-code order for every row.
-    -> (sorted_idx, cluster, idx_ptr, m, new codes [R,m], new order, new inverse, new grid, new batch)."""
+def pool_geometry_begin(codes: Tensor, order: Tensor, pooling_depth: int):
+    """First half of pool_geometry: run flags + their scan, and an asynchronous read of the per-row run counts
+    (work the caller enqueues before pool_geometry_end overlaps the host wait)."""
+    R, n = codes.shape
+    flags = torch.empty(R * n, device=codes.device, dtype=torch.int32)
+    call("sfx_pool_run_flags", n, R, ptr(order, torch.int32), ptr(codes, torch.int64), 3 * pooling_depth,
+         ptr(flags), stream())
+    pos, _ = scan_i32(flags)
+    return flags, pos, _lib.HostRead(pos.view(R, n)[:, -1])
+
+
+def pool_geometry_end(state, codes: Tensor, order: Tensor, row0: int, pooling_depth: int, grid_coord: Tensor,
+                      batch: Optional[Tensor], code_bits: int):
+    flags, pos, ends_rd = state
     R, n = codes.shape
     dev = codes.device
     shift = 3 * pooling_depth
-    flags = torch.empty(R * n, device=dev, dtype=torch.int32)
-    call("sfx_pool_run_flags", n, R, ptr(order, torch.int32), ptr(codes, torch.int64), shift, ptr(flags), stream())
-    pos, _ = scan_i32(flags)
-    ends = pos.view(R, n)[:, -1].cpu().tolist()  # host sync: the pooled point count sizes every later buffer
+    ends = ends_rd.get()  # the pooled point count sizes every later buffer
     runs = [ends[0]] + [ends[r] - ends[r - 1] for r in range(1, R)]
     m = runs[0]
     if any(c != m for c in runs):
@@ -297,6 +319,15 @@ def pool_geometry(codes: Tensor, order: Tensor, row0: int, pooling_depth: int, g
     return sidx, cluster, idx_ptr, m, new_codes, new_order, new_inverse, new_grid, new_batch
 
 
+def pool_geometry(codes: Tensor, order: Tensor, row0: int, pooling_depth: int, grid_coord: Tensor,
+                  batch: Optional[Tensor], code_bits: int):
+    """SerializedPooling's integer half without a sort (serialize.hip): runs of equal code >> 3pd along the
+    parent's serialized orders are the clusters, in ascending pooled-code order for every row.
+    -> (sorted_idx, cluster, idx_ptr, m, new codes [R,m], new order, new inverse, new grid, new batch)."""
+    st = pool_geometry_begin(codes, order, pooling_depth)
+    return pool_geometry_end(st, codes, order, row0, pooling_depth, grid_coord, batch, code_bits)
+
+
 def segment_max_affine_act(x: Tensor, idx_ptr: Tensor, sorted_idx: Tensor, m: int, scale: Optional[Tensor],
                            shift: Optional[Tensor], act: int) -> Tensor:
     C = x.shape[1]
@@ -314,13 +345,27 @@ def segment_mean(x: Tensor, idx_ptr: Tensor, sorted_idx: Tensor, m: int) -> Tens
 
 
 class SubmMap:
-    """Per-stage SubMConv3d indice map (indice_key=stage{s}): nbr [n,27] + offset-major pair lists."""
+    """Per-stage SubMConv3d indice map (indice_key=stage{s}): nbr [n,27] + offset-major pair lists.  The 28 pair
+    offsets reach the host asynchronously; the first conv that needs them waits for that copy only."""
 
-    def __init__(self, nbr: Tensor, mask: Tensor, pair_in: Tensor, pair_out: Tensor, pair_off: List[int]):
+    def __init__(self, nbr: Tensor, mask: Tensor, pair_in: Tensor, pair_out: Tensor, pair_off):
         self.nbr, self.mask, self.pair_in, self.pair_out = nbr, mask, pair_in, pair_out
-        self.pair_off = pair_off
-        import ctypes
-        self._off_host = (ctypes.c_int * 28)(*pair_off)
+        self._off_src = pair_off  # list or _lib.HostRead
+        self._off = None
+        self._off_c = None
+
+    @property
+    def pair_off(self) -> List[int]:
+        if self._off is None:
+            self._off = self._off_src if isinstance(self._off_src, list) else self._off_src.get()
+        return self._off
+
+    @property
+    def _off_host(self):
+        if self._off_c is None:
+            import ctypes
+            self._off_c = (ctypes.c_int * 28)(*self.pair_off)
+        return self._off_c
 
     @property
     def shape(self):
@@ -332,7 +377,7 @@ class SubmMap:
 
 
 def subm_neighbors(grid_coord: Tensor, batch: Optional[Tensor], with_pairs: bool = True):
-    """27-neighbour map; with_pairs also builds the offset-major pair lists (one host sync for their offsets)."""
+    """27-neighbour map; with_pairs also builds the offset-major pair lists (their offsets read back asynchronously)."""
     n = grid_coord.shape[0]
     dev = grid_coord.device
     l2 = _lib.fn("sfx_subm_table_log2")(n)
@@ -350,7 +395,7 @@ def subm_neighbors(grid_coord: Tensor, batch: Optional[Tensor], with_pairs: bool
     poff = torch.empty(28, device=dev, dtype=torch.int32)
     ws = _lib.workspace(_lib.fn("sfx_subm_pairs_workspace_bytes")(n), dev)
     call("sfx_subm_pairs", n, ptr(nbr), ptr(ws), ws.numel(), ptr(pin), ptr(pout), ptr(poff), stream())
-    return SubmMap(nbr, mask, pin, pout, poff.tolist())
+    return SubmMap(nbr, mask, pin, pout, _lib.HostRead(poff))
 
 
 def subm_conv(x: Tensor, smap: "SubmMap", weight: Tensor, bias: Optional[Tensor],
