@@ -178,7 +178,7 @@ template <int D, bool F16>
 __global__ void __launch_bounds__(256, D == 16 ? 4 : 3)
 window_attn_split_kernel(const float* __restrict__ qkv, const int* __restrict__ order, const int* __restrict__ win,
                          int Kwin, int C, float scale, float* __restrict__ out,
-                         const unsigned long long* __restrict__ qkv_amax, unsigned qkv_tag) {
+                         const unsigned long long* __restrict__ qkv_amax, unsigned qkv_tag, int nwin) {
   typedef typename std::conditional<F16, _Float16, __bf16>::type elem_t;
   typedef elem_t bf16x8 __attribute__((ext_vector_type(8)));  // (fragment type: bf16 or fp16 terms)
   constexpr int NT = F16 ? 2 : 3;            // terms per operand
@@ -213,7 +213,14 @@ window_attn_split_kernel(const float* __restrict__ qkv, const int* __restrict__ 
     return KD == 16 ? r * 48 + c * 16 : r * 64 + (((c ^ (r >> 2)) & 3) << 4);
   };
 
-  const int w = blockIdx.x, head = blockIdx.y;
+  // XCD-aware numbering over a 1-D grid padded to a multiple of 8: consecutive blocks go round-robin to the 8
+  // XCDs, so logical id L = xcd * (grid / 8) + slot puts all heads of a window on one XCD back to back -- the
+  // 128-byte qkv lines its heads share (d = 16: two heads per line) are fetched from HBM once into that L2.
+  const int heads = C / D;
+  const int nb = (int)gridDim.x;
+  const int L = (int)(blockIdx.x % 8) * (nb / 8) + (int)(blockIdx.x / 8);
+  if (L >= nwin * heads) return;
+  const int w = L / heads, head = L - w * heads;
   const int key_start = win[2 * w], query_start = win[2 * w + 1];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, h = lane >> 5, l32 = lane & 31;
   const long long ld = 3ll * C;
@@ -645,6 +652,8 @@ int sfx_window_attention(int num_windows, int window, int heads, int head_dim, i
   if (num_windows == 0) return SFX_OK;
   SFX_REQUIRE(qkv && order && win && out, "sfx_window_attention: null buffer");
   dim3 grid(num_windows, heads);
+  const long long nblk = ((long long)num_windows * heads + 7) / 8 * 8;
+  SFX_REQUIRE(nblk < (1ll << 31), "sfx_window_attention: too many windows");
   hipStream_t st = sfx::as_stream(stream);
   static int exact = -1;  // SFX_ATTN_PREC=fp32: the v_mfma_f32_32x32x2_f32 kernel
   if (exact < 0) {
@@ -660,8 +669,8 @@ int sfx_window_attention(int num_windows, int window, int heads, int head_dim, i
       window_attn_kernel<32><<<grid, 256, 0, st>>>(qkv, order, win, window, channels, scale, out);
   } else if (qkv_amax) {  // fp16x2 terms (the caller bounds |qkv|)
 #define SFX_ATTN(DD, F)                                                                                  \
-  window_attn_split_kernel<DD, F><<<grid, 256, 0, st>>>(qkv, order, win, window, channels, scale, out, qkv_amax, \
-                                                        qkv_tag)
+  window_attn_split_kernel<DD, F><<<dim3((unsigned)nblk), 256, 0, st>>>(qkv, order, win, window, channels, scale, \
+                                                                        out, qkv_amax, qkv_tag, num_windows)
     if (head_dim == 16) SFX_ATTN(16, true);
     else if (head_dim == 24) SFX_ATTN(24, true);
     else SFX_ATTN(32, true);
