@@ -317,6 +317,20 @@ size_t sfx_ssim_workspace_bytes(int num_images, int height, int width, int chann
 int sfx_ssim(int num_images, int height, int width, int channels, const float* img1, const float* img2,
              const float* window, int quantize_u8, float* out, void* ws, size_t ws_bytes, void* stream);
 
+/* Point-cloud downsampling experiments (reference models/pcd_downsampling_methods.py; FeaturePredictor
+ * additional_info["downsample"], models/feature_predictor.py:159-196).
+ * sfx_voxel_keys: voxel_downsample's ids (:96-100) as sort keys: floor(p / voxel_size) in fp32, the int32 hash
+ *   x*1000000 + y*1000 + z, biased (id ^ 0x80000000) so unsigned order = signed order.  points: [n][ld] f32.
+ * sfx_nn1: out[i] = index of the nearest of the m reference points to query i (float64 squared distance of the
+ *   f32 coordinates, lowest index on ties) -- the sklearn NearestNeighbors(n_neighbors=1) queries of
+ *   fps_knn_downsample (:45-48) and knn_map_back (:192-195).  queries [n][3], refs [m][3] f32 contiguous.
+ * sfx_fps: furthest_point_sampling (:8-26) from `start` (the caller's torch.randint draw): out[m] indices;
+ *   dist_ws: n floats. */
+int sfx_voxel_keys(int n, const float* points, long long ld, float voxel_size, unsigned long long* keys,
+                   void* stream);
+int sfx_nn1(int n, int m, const float* queries, const float* refs, int* out, void* stream);
+int sfx_fps(int n, int m, const float* xyz, int start, int* out, float* dist_ws, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

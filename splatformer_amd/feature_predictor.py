@@ -147,7 +147,14 @@ class FeaturePredictor(nn.Module):
         # GEMM runs while the host waits for it)
         data = {"coord": means, "grid_coord": grid, "offset": [n], "feat": feat,
                 "serialized_depth": _lib.HostRead(gmax)}
-        self.backbone(data, perms=perms, out=h0[:, :cb])
+        method = self.additional_info.get("downsample")
+        if method is None:
+            self.backbone(data, perms=perms, out=h0[:, :cb])
+        else:  # fork experiment (feature_predictor.py:159-196): backbone on the downsampled cloud, mapped back
+            from .downsample import downsample_for_backbone
+            c, f, g, mapper = downsample_for_backbone(method, self.additional_info, means, feat, grid)
+            y = self.backbone({"coord": c, "grid_coord": g, "offset": [c.shape[0]], "feat": f}, perms=perms).feat
+            h0[:, :cb] = mapper(y)
         w1, b1, mids, wl, bl, out_dim = self._packed_heads()
         x = h0[:, :w1.shape[1]]  # [y | feat | 0-pad]
         # fp16x2 operand bounds: each head layer's epilogue publishes max |output| for the next layer
