@@ -20,8 +20,6 @@ make_golden_downsample.py) and oracle/downsample_ref.py; tests/test_gpu_downsamp
 """
 from __future__ import annotations
 
-from typing import Tuple
-
 import torch
 from torch import Tensor
 
@@ -62,9 +60,8 @@ def _means(points: Tensor, features: Tensor, grid_coords: Tensor, idx_ptr: Tenso
     return p, f, g.round().long()
 
 
-def voxel_downsample(points: Tensor, features: Tensor, grid_coords: Tensor, voxel_size: float):
-    """-> (downsampled points [M,3], features [M,C], grid coords [M,3] long); `last_inverse` holds the voxel of
-    every input point (used by voxel_downsample_map_logits_to_original)."""
+def voxel_downsample_with_inverse(points: Tensor, features: Tensor, grid_coords: Tensor, voxel_size: float):
+    """voxel_downsample plus the voxel (cluster id, int32) of every input point."""
     assert points.shape[0] == features.shape[0]
     _lib.require_gpu(points)
     n = points.shape[0]
@@ -72,16 +69,19 @@ def voxel_downsample(points: Tensor, features: Tensor, grid_coords: Tensor, voxe
     pts = _xyz(points)
     call("sfx_voxel_keys", n, ptr(pts), pts.stride(0), float(voxel_size), ptr(keys), stream())
     sidx, cluster, idx_ptr, m = _clusters(keys)
-    voxel_downsample.last_inverse = cluster
-    return _means(points, features, grid_coords, idx_ptr, sidx, m)
+    return (*_means(points, features, grid_coords, idx_ptr, sidx, m), cluster)
+
+
+def voxel_downsample(points: Tensor, features: Tensor, grid_coords: Tensor, voxel_size: float):
+    """-> (downsampled points [M,3], features [M,C], grid coords [M,3] long)."""
+    return voxel_downsample_with_inverse(points, features, grid_coords, voxel_size)[:3]
 
 
 def voxel_downsample_map_logits_to_original(points: Tensor, downsampled_points: Tensor, logits: Tensor,
                                             voxel_size: float, inverse: Tensor = None) -> Tensor:
-    if inverse is None:  # recompute the voxels of the original points (same keys, same stable clusters)
-        voxel_downsample(points, torch.zeros(points.shape[0], 1, device=points.device),
-                         torch.zeros(points.shape[0], 3, device=points.device), voxel_size)
-        inverse = voxel_downsample.last_inverse
+    if inverse is None:  # the voxels of the original points (same keys, same stable clusters)
+        z = torch.zeros(points.shape[0], 1, device=points.device)
+        inverse = voxel_downsample_with_inverse(points, z, z, voxel_size)[3]
     return logits.index_select(0, inverse.long())
 
 
@@ -139,8 +139,7 @@ def downsample_for_backbone(method: str, info: dict, coord: Tensor, feat: Tensor
     where mapper(y) maps the backbone output of the downsampled points back to the originals (:186-196)."""
     if method == "voxel":
         vs = info["voxel_size"]
-        c, f, g = voxel_downsample(coord, feat, grid, vs)
-        inv = voxel_downsample.last_inverse
+        c, f, g, inv = voxel_downsample_with_inverse(coord, feat, grid, vs)
         return c, f, g.int(), lambda y: voxel_downsample_map_logits_to_original(coord, c, y, vs, inverse=inv)
     if method == "fps":
         c, f, g, a = fps_knn_downsample(coord, feat, grid, info["downsample_ratio"])
