@@ -43,37 +43,36 @@ __global__ void subm_insert_kernel(int n, const int* __restrict__ grid, const in
   }
 }
 
+// one thread per (point, offset): 27x the threads of a per-point loop to hide the probe chains' latency, and
+// coalesced nbr stores (consecutive threads write consecutive offsets of a point)
 __global__ void subm_query_kernel(int n, const int* __restrict__ grid, const int* __restrict__ batch,
                                   const unsigned long long* __restrict__ keys, const int* __restrict__ vals,
                                   int log2cap, int* __restrict__ nbr, unsigned* __restrict__ mask_out,
                                   unsigned long long* __restrict__ mask_keys) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const int gx = grid[3 * i], gy = grid[3 * i + 1], gz = grid[3 * i + 2];
-  const int b = batch ? batch[i] : 0;
+  const long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= 27ll * n) return;
+  const int i = (int)(q / 27), k = (int)(q - 27ll * i);
+  const int x = grid[3 * i] + k / 9 - 1, y = grid[3 * i + 1] + (k / 3) % 3 - 1, z = grid[3 * i + 2] + k % 3 - 1;
   const unsigned cmask = (1u << log2cap) - 1u;
-  unsigned mask = 0u;
-  for (int k = 0; k < 27; ++k) {
-    const int x = gx + k / 9 - 1, y = gy + (k / 3) % 3 - 1, z = gz + k % 3 - 1;
-    int out = -1;
-    if (x >= 0 && y >= 0 && z >= 0) {
-      const unsigned long long key = pack(b, x, y, z);
-      unsigned s = slot_of(key, log2cap);
-      while (true) {
-        const unsigned long long kk = keys[s];
-        if (kk == key) {
-          out = vals[s];
-          break;
-        }
-        if (kk == EMPTY) break;
-        s = (s + 1) & cmask;
+  int out = -1;
+  if (x >= 0 && y >= 0 && z >= 0) {
+    const unsigned long long key = pack(batch ? batch[i] : 0, x, y, z);
+    unsigned s = slot_of(key, log2cap);
+    while (true) {
+      const unsigned long long kk = keys[s];
+      if (kk == key) {
+        out = vals[s];
+        break;
       }
+      if (kk == EMPTY) break;
+      s = (s + 1) & cmask;
     }
-    nbr[27ll * i + k] = out;
-    if (out >= 0) mask |= 1u << k;
   }
-  if (mask_out) mask_out[i] = mask;
-  if (mask_keys) mask_keys[i] = mask;
+  nbr[q] = out;
+  if (out >= 0) {  // (masks zeroed by the launcher)
+    if (mask_out) atomicOr(&mask_out[i], 1u << k);
+    if (mask_keys) atomicOr(&mask_keys[i], 1ull << k);
+  }
 }
 
 // rows of nbr / mask in mask-sorted order (perm from a radix sort of the masks)
@@ -136,8 +135,10 @@ int sfx_subm_neighbors(int n, const int* grid_coord, const int* batch, int log2c
   hipMemsetAsync(table_keys, 0xff, cap * sizeof(unsigned long long), st);
   hipMemsetAsync(table_vals, 0x7f, cap * sizeof(int), st);
   subm_insert_kernel<<<sfx::ceil_div(n, 256), 256, 0, st>>>(n, grid_coord, batch, table_keys, table_vals, log2cap);
-  subm_query_kernel<<<sfx::ceil_div(n, 256), 256, 0, st>>>(n, grid_coord, batch, table_keys, table_vals, log2cap,
-                                                            nbr, mask, mask_keys);
+  if (mask) hipMemsetAsync(mask, 0, (size_t)n * sizeof(unsigned), st);
+  if (mask_keys) hipMemsetAsync(mask_keys, 0, (size_t)n * sizeof(unsigned long long), st);
+  subm_query_kernel<<<sfx::ceil_div(27ll * n, 256), 256, 0, st>>>(n, grid_coord, batch, table_keys, table_vals,
+                                                                  log2cap, nbr, mask, mask_keys);
   return sfx::check_launch("sfx_subm_neighbors");
 }
 
