@@ -1,30 +1,47 @@
 """Benchmark of the SplatFormer hot path on MI355X (BASELINE.json configs).
 
 Default (the driver's line) = config B: refined renders/sec on 100k-Gaussian x 800x800 scenes.  One step =
-one scene per rank: FeaturePredictor forward (full ptv3_base PTv3 + heads, fp32) over 100k Gaussians, then
-the 9 OOD test views (800x800) of the refined Gaussians through the gsplat-v0.1.11-semantics renderer -- the
-reference's evaluation() hot loop (train.py:86-100).  Synthetic seeded scene and random-init weights of the
-ptv3_base architecture (no datasets/checkpoints offline).  Multi-GPU: one process per GPU, one scene per
-rank (weak scaling, no collective on the data path; barrier + max-over-ranks timing only).
+one scene per rank: FeaturePredictor forward (full ptv3_base PTv3 + heads, fp32-accurate) over 100k
+Gaussians, then the 9 OOD test views (800x800) of the refined Gaussians through the gsplat-v0.1.11-semantics
+renderer -- the reference's evaluation() hot loop (train.py:86-100).  Synthetic seeded scene and random-init
+weights of the ptv3_base architecture (no datasets/checkpoints offline).
 
+Multi-GPU: one process per GPU.  `python bench.py --gpus N` (N > 1, outside torchrun) starts
+`torch.distributed.run --nproc-per-node N` as a child process before anything touches the GPU and exits
+with its status; under torchrun (WORLD_SIZE set) every rank refines and renders its own scene (weak scaling,
+no collective on the data path; barrier + max-over-ranks timing only), `n_gpus` = the real world size.
+
+--config A: 20k Gaussians SH0 (Cin 14), depth-1 PTv3, 4 views 256x256 (the reference's CPU-runnable case).
 --config C: training -- a step = a batch of 8 scenes (100k GS, SH1), each refined in train mode, rendered to
   4 training views (800x800), image-L1 loss, backward through renderer + refiner, then clip + Adam
   (train.py:236-303); renders/s = 8*4 / step time.
---config D: DDP training under torchrun -- per rank one scene per micro-step, 4 micro-steps per optimiser
-  step (accumulate 4), RCCL all-reduce of the gradient bucket + SyncBatchNorm; a step = one optimiser step.
+--config D: DDP training -- per rank one scene per micro-step, 4 micro-steps per optimiser step (accumulate
+  4), RCCL all-reduce of the gradient bucket + SyncBatchNorm; a step = one optimiser step.
 --config E: 500k Gaussians, SH3, 1920x1080, 9 views, forward (HBM-bound stress).
 
-Prints ONE JSON line (rank 0) with `roofline` for the dominant kernel (the fp32 MFMA GEMM, every launch of
-one refine replayed between HIP events on the launch stream) and `cpu_baseline` (the CPU oracle on a
-bounded sample, rank 0 at N=1 only).
+Prints ONE JSON line (rank 0) with
+  * `roofline` for the dominant kernel family (the fp32-accurate MFMA GEMMs): algorithmic FLOP of every GEMM
+    launch of one unit of work (a refine; for C/D one training micro-step, forward + backward) / the summed
+    in-context launch durations (HIP events around each launch on the launch stream, in the real sequence,
+    median of 3 passes); `algorithmic_bytes` of the same launches; `traffic` = HBM bytes of those launches
+    from rocprofv3 PMC passes run by this script (child processes; 2*FETCH_SIZE + WRITE_SIZE per
+    MI355X_MICROARCH.md), or null when the profiler is unavailable;
+  * `cpu_baseline`: the CPU oracle (oracle/) on the box's host cores, rank 0 at N=1 only (protocol below).
 """
 from __future__ import annotations
 
 import argparse
+import csv
+import glob
 import json
-import math
 import os
+import platform
+import shutil
+import socket
+import statistics
+import subprocess
 import sys
+import tempfile
 import time
 
 import torch
@@ -37,28 +54,36 @@ F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense fp16 / bf16 MFMA (no
 # The GEMM computes fp32-accurate products as three fp16 term products (fp16x2 split operands, gemm.hip): its
 # fp32-equivalent ceiling is the dense fp16 peak / 3.
 SPLIT_PEAK_TFLOPS = round(F16_MFMA_PEAK_TFLOPS / 3, 1)
-# rocprofv3 FETCH_SIZE / WRITE_SIZE passes over this bench (tools/traffic_summary.py), committed per round
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r01_traffic_f16x2.json")
 HBM_PEAK_GBS = 8000.0
+GEMM_FAMILY = ("gemm_kernel", "wgrad_kernel")  # kernel-name prefixes of the dominant family
+
+DEFAULTS = {  # n, res, views, sh, batch
+    "A": (20_000, "256", 4, 0, 1), "B": (100_000, "800", 9, 1, 1), "C": (100_000, "800", 4, 1, 8),
+    "D": (100_000, "800", 4, 1, 4), "E": (500_000, "1920x1080", 9, 3, 1)}
+DEPTH1 = dict(enc_depths=(1, 1, 1, 1, 1), dec_depths=(1, 1, 1, 1))
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", choices=["B", "C", "D", "E"], default="B")
+    ap.add_argument("--config", choices=sorted(DEFAULTS), default="B")
     ap.add_argument("--n", type=int, default=None)
     ap.add_argument("--res", type=str, default=None, help="W or WxH")
     ap.add_argument("--views", type=int, default=None)
     ap.add_argument("--sh", type=int, default=None)
     ap.add_argument("--batch", type=int, default=None, help="scenes per step (C) / micro-steps (D)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample", type=int, default=20_000, help="Gaussians in the CPU-oracle sample")
-    ap.add_argument("--profile-only", action="store_true", help="skip roofline probe and CPU baseline")
-    a = ap.parse_args()
-    dflt = {"B": (100_000, "800", 9, 1, 1), "C": (100_000, "800", 4, 1, 8), "D": (100_000, "800", 4, 1, 4),
-            "E": (500_000, "1920x1080", 9, 3, 1)}[a.config]
+    ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC passes")
+    ap.add_argument("--cpu-sample", type=int, default=None,
+                    help="Gaussians in the CPU-oracle sample (default: the whole scene for A, 20000 otherwise)")
+    ap.add_argument("--profile-only", action="store_true", help="skip roofline probe, traffic and CPU baseline")
+    ap.add_argument("--markers", action="store_true",
+                    help="launch sfx_profile_marker before every timed step and after the last (PMC passes)")
+    ap.add_argument("--dry-launch", action="store_true", help=argparse.SUPPRESS)  # launcher test: no GPU work
+    a = ap.parse_args(argv)
+    dflt = DEFAULTS[a.config]
     a.n = a.n if a.n is not None else dflt[0]
     res = a.res if a.res is not None else dflt[1]
     a.width, a.height = (int(res.split("x")[0]), int(res.split("x")[1])) if "x" in res else (int(res), int(res))
@@ -68,168 +93,333 @@ def parse():
     return a
 
 
-class GemmRecorder:
-    """Records the GEMM-kernel launches (sfx_linear / sfx_subm_conv) of one refine pass."""
+# ---- multi-GPU launcher ---------------------------------------------------------------------------------------
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_cmd(gpus: int, argv, port: int):
+    """The torchrun command that runs this script once per GPU (one process per GPU, rendezvous on
+    127.0.0.1); the children see WORLD_SIZE and do not relaunch."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+
+
+def needs_launch(gpus: int, env=None) -> bool:
+    env = os.environ if env is None else env
+    return gpus > 1 and "WORLD_SIZE" not in env
+
+
+def world_size_check(gpus: int, world: int) -> None:
+    if gpus not in (1, world):  # --gpus 1 is the default: accept any torchrun world
+        raise SystemExit(f"bench.py: --gpus {gpus} but the launcher started {world} ranks")
+
+
+# ---- GEMM family: in-context launch timing, FLOP and byte accounting -----------------------------------------
+def _gemm_cost(kind, args, kw, res):
+    """(FLOP, algorithmic bytes, shape) of one GEMM-family launch (fp32 operands, 4-byte elements)."""
+    f4 = 4
+    if kind == "linear":
+        x, w = args[0], args[1]
+        out = res[0] if isinstance(res, tuple) else res
+        M, (N, K) = out.shape[0], w.shape
+        by = (M * K + N * K + M * N) * f4
+        by += sum(M * N * f4 for k in ("residual", "pre_out") if kw.get(k) is not None)
+        return 2.0 * M * N * K, by, (M, N, K)
+    if kind == "grouped_linear":
+        x, w = args[0], args[1]
+        G, N, K = w.shape
+        M = x.shape[0]
+        return 2.0 * M * G * N * K, (M * G * K + G * N * K + M * G * N) * f4, (M, G * N, K)
+    if kind == "subm_conv":
+        x, smap, w = args[0], args[1], args[2]
+        n, cin = x.shape
+        cout = w.shape[0]
+        fl = 2.0 * (n + smap.num_pairs) * cin * cout
+        return fl, (n * cin + 27 * cin * cout + n * cout + 27 * n) * f4, (n, cout, cin)
+    if kind == "linear_bwd_data":
+        dy, wt = args[0], args[1]
+        M, N = dy.shape
+        K = wt.shape[0]
+        by = (M * N + K * N + M * K) * f4 + (M * K * f4 if kw.get("dact_pre") is not None else 0)
+        return 2.0 * M * N * K, by, (M, K, N)
+    if kind == "linear_wgrad":
+        dy, x = args[0], args[1]
+        M, N = dy.shape
+        K = x.shape[1]
+        return 2.0 * M * N * K, (M * N + M * K + 2 * N * K) * f4, (N, K, M)
+    if kind == "subm_conv_bwd_data":
+        dy, smap, wt, dx = args[0], args[1], args[2], args[3]
+        n, cout = dy.shape
+        cin = dx.shape[1]
+        fl = 2.0 * (n + smap.num_pairs) * cin * cout
+        return fl, (n * cout + 27 * cin * cout + 2 * n * cin + 27 * n) * f4, (n, cin, cout)
+    raise KeyError(kind)
+
+
+class GemmTimer:
+    """Wraps the GEMM-family entry points (ptv3_ops.linear / subm_conv / grouped_linear, train_ops
+    linear_bwd_data / linear_wgrad / subm_conv_bwd_data) for one pass of real work: HIP events recorded on the
+    launch stream around each launch, in the real launch sequence (no replay, caches as they are)."""
 
     def __init__(self):
         self.calls = []
 
     def __enter__(self):
-        from splatformer_amd import ptv3_ops
-        self._lin, self._conv, self._grp = ptv3_ops.linear, ptv3_ops.subm_conv, ptv3_ops.grouped_linear
-        rec = self
-
-        def lin(x, weight, bias=None, **kw):
-            res = rec._lin(x, weight, bias, **kw)
-            out = res[0] if isinstance(res, tuple) else res
-            M = out.shape[0]
-            N, K = weight.shape
-            kw2 = dict(kw)
-            kw2["out"] = torch.empty_like(out) if kw.get("out") is None else torch.empty_like(kw["out"])
-            rec.calls.append(("linear", 2.0 * M * N * K, lambda: rec._lin(x, weight, bias, **kw2), (M, N, K)))
-            return res
-
-        def conv(x, smap, weight, bias, out=None, **kw):
-            o = rec._conv(x, smap, weight, bias, out=out, **kw)
-            n, cin = x.shape
-            cout = weight.shape[0]
-            scratch = torch.empty_like(o)
-            fl = 2.0 * (n + smap.num_pairs) * cin * cout
-            rec.calls.append(("subm_conv", fl, lambda: rec._conv(x, smap, weight, bias, out=scratch, **kw),
-                              (n, cout, cin)))
-            return o
-
-        def grp(x, weight, bias, groups, **kw):
-            res = rec._grp(x, weight, bias, groups, **kw)
-            out = res[0] if isinstance(res, tuple) else res
-            G, N, K = weight.shape
-            scratch = torch.empty_like(out)
-            rec.calls.append(("grouped_linear", 2.0 * x.shape[0] * G * N * K,
-                              lambda: rec._grp(x, weight, bias, groups, **dict(kw, out=scratch)),
-                              (x.shape[0], G * N, K)))
-            return res
-
-        ptv3_ops.linear, ptv3_ops.subm_conv, ptv3_ops.grouped_linear = lin, conv, grp
+        from splatformer_amd import ptv3_ops, train_ops
+        self._saved = []
+        for mod, name in [(ptv3_ops, "linear"), (ptv3_ops, "subm_conv"), (ptv3_ops, "grouped_linear"),
+                          (train_ops, "linear_bwd_data"), (train_ops, "linear_wgrad"),
+                          (train_ops, "subm_conv_bwd_data")]:
+            fn = getattr(mod, name)
+            self._saved.append((mod, name, fn))
+            setattr(mod, name, self._wrap(name, fn))
         return self
 
+    def _wrap(self, kind, fn):
+        rec = self
+
+        def wrapped(*args, **kw):
+            st = torch.cuda.current_stream()  # the stream libsfx launches on (_lib.stream())
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            res = fn(*args, **kw)
+            e1.record(st)
+            fl, by, shape = _gemm_cost(kind, args, kw, res)
+            rec.calls.append((kind, fl, by, shape, e0, e1))
+            return res
+        return wrapped
+
     def __exit__(self, *a):
-        from splatformer_amd import ptv3_ops
-        ptv3_ops.linear, ptv3_ops.subm_conv, ptv3_ops.grouped_linear = self._lin, self._conv, self._grp
+        for mod, name, fn in self._saved:
+            setattr(mod, name, fn)
 
-
-def roofline_probe(model, scene, reps=5):
-    """Replay every GEMM-kernel launch of one refine pass between HIP events (on the launch stream):
-    achieved = algorithmic FLOP of all launches / summed average launch time."""
-    with GemmRecorder() as rec:
-        model.refine_packed(scene)
-    torch.cuda.synchronize()
-    st = torch.cuda.current_stream()
-    tot_fl, tot_ms, per = 0.0, 0.0, []
-    for kind, fl, fn, shape in rec.calls:
-        fn()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(st)
-        for _ in range(reps):
-            fn()
-        e1.record(st)
+    def summary(self):
         torch.cuda.synchronize()
-        ms = e0.elapsed_time(e1) / reps
-        tot_fl += fl
-        tot_ms += ms
-        per.append((ms, kind, shape, fl))
-    achieved = tot_fl / (tot_ms * 1e-3) / 1e12
+        per = [(e0.elapsed_time(e1), kind, shape, fl, by) for kind, fl, by, shape, e0, e1 in self.calls]
+        return per
+
+
+def roofline_probe(unit_fn, passes=3):
+    """achieved = algorithmic FLOP of every GEMM-family launch of one unit of work / their summed in-context
+    durations; median over `passes` passes of the unit."""
+    runs = []
+    for _ in range(passes):
+        torch.cuda.synchronize()
+        with GemmTimer() as t:
+            unit_fn()
+        runs.append(t.summary())
+    tot = [(sum(p[0] for p in r), r) for r in runs]
+    tot.sort(key=lambda x: x[0])
+    ms, per = tot[len(tot) // 2]
+    fl = sum(p[3] for p in per)
+    by = sum(p[4] for p in per)
+    achieved = fl / (ms * 1e-3) / 1e12
     top = max(per)
-    traffic = None
-    try:  # measured HBM bytes of the same launches (PMC passes, per scene), see TRAFFIC_FILE
-        with open(TRAFFIC_FILE) as f:
-            traffic = json.load(f)["per_scene"]["gemm_kernel"]["hbm_B"]
-    except (OSError, KeyError, ValueError):
-        pass
     return {
         "bound": "mfma", "achieved": round(achieved, 2), "peak": SPLIT_PEAK_TFLOPS, "unit": "TFLOP/s",
-        "frac": round(achieved / SPLIT_PEAK_TFLOPS, 4), "traffic": traffic,
-        "traffic_unit": "HBM bytes per scene (all GEMM launches; 2*FETCH_SIZE + WRITE_SIZE, " +
-                        os.path.relpath(TRAFFIC_FILE, ROOT) + ")",
+        "frac": round(achieved / SPLIT_PEAK_TFLOPS, 4), "traffic": None,
+        "algorithmic_bytes": int(by),
         "peak_basis": (f"fp32-equivalent ceiling of the fp16x2 split GEMM = dense fp16 MFMA {F16_MFMA_PEAK_TFLOPS:.0f}"
                        f" / 3 term products; exact-fp32 MFMA peak is {FP32_MFMA_PEAK_TFLOPS}"),
         "frac_of_fp32_mfma_peak": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
-        "kernel": ("gemm_kernel (sfx_linear / sfx_subm_conv: fp32 operands scaled by powers of two and split into "
-                   "2 fp16 terms, 3 x v_mfma_f32_32x32x16_f16 per block, fp32 accumulation; K < 64: exact fp32 "
-                   "MFMA), all launches of one scene (incl. their operand-maxima passes)"),
-        "launches": len(per), "gemm_ms_per_scene": round(tot_ms, 3),
-        "algorithmic_gflop_per_scene": round(tot_fl / 1e9, 1),
-        "top_launch": {"op": top[1], "M_N_K": list(top[2]), "avg_ms": round(top[0], 4),
+        "kernel": ("GEMM family (gemm_kernel: sfx_linear / sfx_subm_conv / training data-gradient GEMMs, fp32 "
+                   "operands as power-of-two-scaled fp16x2 terms, 3 x v_mfma_f32_32x32x16_f16 per block, fp32 "
+                   "accumulation; wgrad_kernel), every launch of one unit of work incl. operand-maxima passes"),
+        "timing": "HIP events around each launch on its stream, in the real launch sequence; median of "
+                  f"{passes} passes",
+        "launches": len(per), "gemm_ms_per_unit": round(ms, 3), "algorithmic_gflop_per_unit": round(fl / 1e9, 1),
+        "top_launch": {"op": top[1], "M_N_K": list(top[2]), "ms": round(top[0], 4),
                        "tflops": round(top[3] / (top[0] * 1e-3) / 1e12, 2)},
     }
 
 
-def cpu_baseline(scene_cpu, cams_cpu, model_cpu_sd, sample_n, n_total, views, threads):
-    """The CPU oracle (oracle/) on a bounded sample of the workload (test infrastructure, not the product)."""
-    from oracle import ptv3_ref, render_ref
-    torch.set_num_threads(threads)
-    idx = torch.arange(sample_n)
-    sub = {k: v[idx].contiguous() for k, v in scene_cpu.items()}
-    perms = [[0, 1, 2, 3]] * 5
-    t0 = time.perf_counter()
-    out, _ = ptv3_ref.feature_predictor_forward(model_cpu_sd, ptv3_ref.PTv3Config(), sub, perms)
-    t_fwd = time.perf_counter() - t0
-    c2w = cams_cpu["camera_to_worlds"][0]
-    t0 = time.perf_counter()
-    render_ref.rasterize_gaussians_to_singleimg(out, c2w, **cams_cpu)
-    t_view = time.perf_counter() - t0
-    scale = n_total / sample_n
-    t_scene = t_fwd * scale + views * t_view * scale
-    return {
-        "value": round(views / t_scene, 5), "unit": "renders/s", "cores": threads, "kind": "port",
-        "sample": (f"oracle FeaturePredictor fwd on the first {sample_n} of {n_total} Gaussians ({t_fwd:.2f}s) + 1 of "
-                   f"{views} views of that refined crop ({t_view:.2f}s); both scaled linearly by N "
-                   f"({scale:.1f}x) and the view time by {views}"),
-    }
+# ---- HBM traffic from rocprofv3 PMC passes (child processes) -------------------------------------------------
+def _pmc_pass(counter, argv, outdir, timeout_s=240):
+    rp = shutil.which("rocprofv3")
+    if rp is None:
+        return None, "rocprofv3 not found"
+    cmd = ["timeout", "-s", "KILL", str(timeout_s), rp, "--pmc", counter, "-d", outdir, "-o", "run",
+           "--output-format", "csv", "--", sys.executable, os.path.abspath(__file__), *argv]
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, env=env, cwd=ROOT)
+    files = glob.glob(os.path.join(outdir, "**", "*counter_collection.csv"), recursive=True)
+    if r.returncode != 0 or not files:
+        return None, f"rocprofv3 --pmc {counter}: rc {r.returncode}: {r.stdout.decode(errors='replace')[-300:]}"
+    return files[0], None
 
 
-def _threads():
+def _per_unit(csv_path, counter):
+    """Sum of `counter` over the GEMM-family dispatches between consecutive profile markers, per unit (the
+    median unit); counters in KiB."""
+    rows = []
+    with open(csv_path) as f:
+        for r in csv.DictReader(f):
+            if r.get("Counter_Name") != counter:
+                continue
+            rows.append((int(r["Dispatch_Id"]), r["Kernel_Name"], float(r["Counter_Value"])))
+    rows.sort()
+    marks = [d for d, k, _ in rows if "profile_marker_kernel" in k]
+    if len(marks) < 2:
+        raise RuntimeError(f"{counter}: {len(marks)} profile markers in {csv_path}")
+    units = []
+    for a, b in zip(marks[:-1], marks[1:]):
+        units.append(sum(v for d, k, v in rows if a < d < b and any(p in k for p in GEMM_FAMILY)) * 1024.0)
+    return statistics.median(units), len(units)
+
+
+def measure_traffic(args):
+    """Two PMC passes (FETCH_SIZE, WRITE_SIZE: separate runs, MI355X_MICROARCH.md) of this bench in
+    --profile-only --markers mode, 1 warm-up + 2 marked units; -> HBM bytes per unit of the GEMM family
+    (2*FETCH_SIZE + WRITE_SIZE: gfx950 FETCH_SIZE counts half the bytes of wide reads), or (None, reason)."""
+    argv = ["--config", args.config, "--n", str(args.n), "--res", f"{args.width}x{args.height}",
+            "--views", str(args.views), "--sh", str(args.sh), "--batch", str(args.batch), "--steps", "2",
+            "--warmup", "1", "--profile-only", "--markers"]
+    tmp = tempfile.mkdtemp(prefix="sfx_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
+    try:
+        got = {}
+        for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+            path, err = _pmc_pass(counter, argv, os.path.join(tmp, counter))
+            if path is None:
+                return None, err
+            got[counter] = _per_unit(path, counter)
+        fetch, n_units = got["FETCH_SIZE"]
+        write, _ = got["WRITE_SIZE"]
+        return {"hbm_B": 2 * fetch + write, "fetch_B": 2 * fetch, "write_B": write, "units": n_units}, None
+    except Exception as e:  # a profiler problem must not lose the bench line
+        return None, f"traffic measurement failed: {e}"
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
+# ---- CPU baseline (the oracle on the host cores) --------------------------------------------------------------
+def _cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def _cgroup_cpus():
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            return max(1, int(float(q) / float(p)))
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def cpu_threads():
+    """(threads used, affinity cores, cgroup CPU quota): all affinity cores, capped by the
+    container's CPU quota when one is set (more threads than the quota only time-slice)."""
     try:
         aff = len(os.sched_getaffinity(0))
     except AttributeError:
         aff = os.cpu_count() or 1
-    return max(1, min(16, aff))
+    quota = _cgroup_cpus()
+    return (min(aff, quota) if quota else aff), aff, quota
 
 
-def cpu_baseline_train(scene_cpu, cams_cpu, model_cpu_sd, sample_n, n_total, views, scenes_per_step, threads):
-    """The CPU oracle's train step on a bounded sample: refiner train-mode forward + autograd backward to the
-    qkv parameters on a crop, plus one forward render of the refined crop (render backward not included)."""
+def _median_time(fn, repeats=3):
+    fn()  # warm-up
+    ts = []
+    for _ in range(repeats):
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    return statistics.median(ts), ts
+
+
+def cpu_baseline(scene_cpu, cams_cpu, sd, cfg_kw, sample_n, n_total, views, sh):
+    """The CPU oracle (oracle/, test infrastructure) on the same workload: FeaturePredictor forward on the
+    first `sample_n` Gaussians + one view of that refined sample; 1 warm-up + median of 3 each.  When the
+    sample is the whole scene (config A) nothing is extrapolated except view 1 -> `views` views."""
     from oracle import ptv3_ref, render_ref
+    threads, aff, quota = cpu_threads()
     torch.set_num_threads(threads)
     sub = {k: v[:sample_n].contiguous() for k, v in scene_cpu.items()}
     perms = [[0, 1, 2, 3]] * 5
-    sd = {k: v.clone() for k, v in model_cpu_sd.items()}
-    for k, v in sd.items():
-        if "attn.qkv" in k:
-            v.requires_grad_()
-    t0 = time.perf_counter()
-    out, _ = ptv3_ref.feature_predictor_forward(sd, ptv3_ref.PTv3Config(), sub, perms, train=True)
-    loss = sum(v.abs().mean() for v in out.values())
-    loss.backward()
-    t_ref = time.perf_counter() - t0
+    cfg = ptv3_ref.PTv3Config(in_channels=sd["backbone.backbone.embedding.0.weight"].shape[1], **cfg_kw)
+    holder = {}
+
+    def fwd():
+        holder["out"], _ = ptv3_ref.feature_predictor_forward(sd, cfg, sub, perms, sh_degree=sh)
+
+    t_fwd, ts_fwd = _median_time(fwd)
     c2w = cams_cpu["camera_to_worlds"][0]
-    t0 = time.perf_counter()
+    t_view, ts_view = _median_time(lambda: render_ref.rasterize_gaussians_to_singleimg(holder["out"], c2w,
+                                                                                       **cams_cpu))
+    scale = n_total / sample_n
+    t_scene = t_fwd * scale + views * t_view * scale
+    whole = sample_n == n_total
+    return {
+        "value": round(views / t_scene, 5), "unit": "renders/s", "cores": threads, "kind": "port",
+        "cpu_model": _cpu_model(), "affinity_cores": aff, "cgroup_cpu_quota": quota,
+        "protocol": "1 warm-up + median of 3 (refine and one view separately)",
+        "sample": (f"oracle FeaturePredictor fwd on {'all' if whole else 'the first'} {sample_n} of {n_total} "
+                   f"Gaussians (median {t_fwd:.2f}s of {[round(t, 2) for t in ts_fwd]}) + 1 of {views} views of "
+                   f"that refined {'scene' if whole else 'crop'} (median {t_view:.2f}s); "
+                   + ("view time x " + str(views) if whole else
+                      f"both scaled linearly by N ({scale:.1f}x) and the view time by {views}")),
+    }
+
+
+def cpu_baseline_train(scene_cpu, cams_cpu, sd0, sample_n, n_total, views, scenes_per_step):
+    """The CPU oracle's train step on a bounded sample: refiner train-mode forward + autograd backward to the
+    qkv parameters on a crop, plus one forward render of the refined crop (render backward not included);
+    1 warm-up + median of 3."""
+    from oracle import ptv3_ref, render_ref
+    threads, aff, quota = cpu_threads()
+    torch.set_num_threads(threads)
+    sub = {k: v[:sample_n].contiguous() for k, v in scene_cpu.items()}
+    perms = [[0, 1, 2, 3]] * 5
+    holder = {}
+
+    def step():
+        sd = {k: v.clone() for k, v in sd0.items()}
+        for k, v in sd.items():
+            if "attn.qkv" in k:
+                v.requires_grad_()
+        out, _ = ptv3_ref.feature_predictor_forward(sd, ptv3_ref.PTv3Config(), sub, perms, train=True)
+        loss = sum(v.abs().mean() for v in out.values())
+        loss.backward()
+        holder["out"] = {k: v.detach() for k, v in out.items()}
+
+    t_ref, ts = _median_time(step)
+    c2w = cams_cpu["camera_to_worlds"][0]
     with torch.no_grad():
-        render_ref.rasterize_gaussians_to_singleimg({k: v.detach() for k, v in out.items()}, c2w, **cams_cpu)
-    t_view = time.perf_counter() - t0
+        t_view, _ = _median_time(lambda: render_ref.rasterize_gaussians_to_singleimg(holder["out"], c2w, **cams_cpu))
     scale = n_total / sample_n
     t_step = scenes_per_step * (t_ref * scale + views * t_view * scale)
     return {
         "value": round(scenes_per_step * views / t_step, 6), "unit": "renders/s", "cores": threads, "kind": "port",
+        "cpu_model": _cpu_model(), "affinity_cores": aff, "cgroup_cpu_quota": quota,
+        "protocol": "1 warm-up + median of 3",
         "sample": (f"oracle FeaturePredictor train fwd+bwd (autograd, qkv grads) on the first {sample_n} of {n_total} "
-                   f"Gaussians ({t_ref:.2f}s) + 1 forward view of that crop ({t_view:.2f}s); scaled by N ({scale:.1f}x), "
-                   f"views ({views}) and scenes/step ({scenes_per_step}); render backward not timed"),
+                   f"Gaussians (median {t_ref:.2f}s) + 1 forward view of that crop ({t_view:.2f}s); scaled by N "
+                   f"({scale:.1f}x), views ({views}) and scenes/step ({scenes_per_step}); render backward not timed"),
     }
 
 
-def main():
-    args = parse()
+# ---- main -----------------------------------------------------------------------------------------------------
+def main(argv=None):
+    args = parse(argv)
+    if needs_launch(args.gpus):  # before anything touches the GPU
+        sys.exit(subprocess.call(launch_cmd(args.gpus, sys.argv[1:] if argv is None else argv, _free_port())))
     from splatformer_amd import dist as sdist
     rank, world, local_rank = sdist.env_rank()
+    world_size_check(args.gpus, world)
+    if args.dry_launch:  # the launcher's CPU test: report the rank layout, touch no GPU
+        print(json.dumps({"rank": rank, "world": world, "local_rank": local_rank}), flush=True)
+        return
     dev = torch.device("cuda", local_rank if world > 1 else 0)
     torch.cuda.set_device(dev)
     multi = sdist.init("nccl")  # RCCL: barrier + max-over-ranks timing; config D adds the gradient all-reduce
@@ -242,8 +432,9 @@ def main():
     train = args.config in ("C", "D")
     cams_cpu = make_cameras(args.width, args.height, n_views=args.views)
     cams = to_device(cams_cpu, dev)
+    bk = DEPTH1 if args.config == "A" else {}
     torch.manual_seed(0)
-    model = FeaturePredictor(sh_degree=args.sh, zeroinit=False).eval()
+    model = FeaturePredictor(sh_degree=args.sh, zeroinit=False, backbone_kwargs=bk).eval()
     sd_cpu = {k: v.detach().clone() for k, v in model.state_dict().items()}
     model = model.to(dev)
 
@@ -255,6 +446,9 @@ def main():
             out = model([scene], [rank])[0]
             rgbs, alphas = rasterize_gaussians_to_multiimgs(out, cams)
             return rgbs
+
+        def unit():  # the GEMM family's unit of work: one refine
+            model.refine_packed(scene)
         renders_per_step = args.views
     else:
         from splatformer_amd.train import Trainer
@@ -277,16 +471,22 @@ def main():
                 for i in range(n_sc):
                     tr.micro_step([scenes[i]], [cams], [gts[i]])
                 tr.optimizer_step()
+
+        def unit():  # one training micro-step of one scene: train forward + backward (no optimiser step)
+            tr.micro_step([scenes[0]], [cams], [gts[0]])
         renders_per_step = args.views * n_sc
 
+    marker = (lambda i: _lib.call("sfx_profile_marker", i, _lib.stream())) if args.markers else (lambda i: None)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
     sdist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
+        marker(i)
         step()
+    marker(args.steps)
     torch.cuda.synchronize()
     sdist.barrier()
     t1 = time.perf_counter()
@@ -295,30 +495,44 @@ def main():
 
     roof = None
     if not args.profile_only:
-        model.eval()
-        roof = roofline_probe(model, to_device(scene_cpu, dev))
+        if not train:
+            model.eval()
+        roof = roofline_probe(unit)
+        if rank == 0 and world == 1 and not args.no_traffic:
+            tr_res, err = measure_traffic(args)
+            if tr_res is not None:
+                roof["traffic"] = tr_res["hbm_B"]
+                roof["traffic_detail"] = {**tr_res, "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes run "
+                                                               "by bench.py (2*FETCH + WRITE, per unit, median)"}
+                roof["traffic_over_algorithmic"] = round(tr_res["hbm_B"] / max(1, roof["algorithmic_bytes"]), 3)
+            else:
+                roof["traffic_note"] = err
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.profile_only:
-        sample = min(args.cpu_sample, args.n)
+        sample = min(args.cpu_sample or (args.n if args.config == "A" else 20_000), args.n)
         if train:
-            cpu = cpu_baseline_train(scene_cpu, cams_cpu, sd_cpu, sample, args.n, args.views, args.batch, _threads())
+            cpu = cpu_baseline_train(scene_cpu, cams_cpu, sd_cpu, sample, args.n, args.views, args.batch)
         else:
-            cpu = cpu_baseline(scene_cpu, cams_cpu, sd_cpu, sample, args.n, args.views, _threads())
+            cpu = cpu_baseline(scene_cpu, cams_cpu, sd_cpu, bk, sample, args.n, args.views, args.sh)
 
     if rank == 0:
         res = f"{args.width}x{args.height}"
+        unit_name = "one training micro-step (train fwd + bwd of one scene)" if train else "one refine"
         if args.config == "C":
             workload = (f"C: batch {args.batch} scenes x {args.n} Gaussians SH{args.sh}, train-mode refine + "
                         f"{args.views} views {res} each, image-L1 fwd+bwd, clip + Adam (attn.qkv)")
-            par = "single-gpu"
+            par = f"scene-dp{world}" if world > 1 else "single-gpu"
         elif args.config == "D":
             workload = (f"D: DDP, per rank {args.batch} micro-steps x 1 scene ({args.n} GS SH{args.sh}, {args.views} "
                         f"views {res}) per optimiser step, RCCL grad all-reduce + SyncBN")
             par = f"ddp{world}-accum{args.batch}"
         else:
-            workload = (f"{args.config}: {args.n} Gaussians SH{args.sh}, full PTv3 (ptv3_base) + heads, "
+            depth = "depth-1 PTv3" if args.config == "A" else "full PTv3 (ptv3_base)"
+            workload = (f"{args.config}: {args.n} Gaussians SH{args.sh}, {depth} + heads, "
                         f"{args.views} views {res}, forward")
             par = f"scene-dp{world}"
+        if roof is not None:
+            roof["unit_of_work"] = unit_name
         line = {
             "metric": "refined renders/sec (100k GS, 800x800) at 1/2/4/8 MI355X; PSNR vs ref" if args.config == "B"
             else f"refined renders/sec (config {args.config})",

@@ -152,6 +152,9 @@ int sfx_linear_bwd_data(int M, int N, int K, const float* dY, long long ldy, con
 int sfx_linear_wgrad(int M, int N, int K, const float* dY, long long ldy, const float* X, long long ldx, float* dW,
                      long long ldw, float* db, void* stream);
 /* dst[c, r] = src[r, c] */
+/* An empty kernel delimiting units of work in a rocprofv3 PMC / kernel trace (bench.py measure_traffic). */
+int sfx_profile_marker(int tag, void* stream);
+
 int sfx_transpose(int rows, int cols, const float* src, long long lds, float* dst, long long ldd, void* stream);
 /* spconv SubMConv3d backward w.r.t. the input (the cpe.0 conv of every Block): dX[in] += dY[out] W_k over
  * the centre offset and every (in, out, k) pair of sfx_subm_pairs; weight_t = weight [Cout, 27*Cin]

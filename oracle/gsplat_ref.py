@@ -85,8 +85,10 @@ def spherical_harmonics_bwd(degrees_to_use: int, viewdirs: torch.Tensor, v_color
 
 
 def quat_to_rotmat(q: torch.Tensor) -> torch.Tensor:
-    """helpers.cuh quat_to_rotmat: q = (w,x,y,z), normalised by rsqrt; returns R[N,3,3] row-major."""
-    s = torch.rsqrt((q * q).sum(-1))
+    """helpers.cuh quat_to_rotmat: q = (w,x,y,z) scaled by s = 1/sqrt(w^2+x^2+y^2+z^2) (gsplat: rsqrtf; the
+    canonical form here is the correctly rounded 1/sqrt, sum left to right); returns R[N,3,3] row-major."""
+    ss = ((q[:, 0] * q[:, 0] + q[:, 1] * q[:, 1]) + q[:, 2] * q[:, 2]) + q[:, 3] * q[:, 3]
+    s = 1.0 / torch.sqrt(ss)
     w, x, y, z = q[:, 0] * s, q[:, 1] * s, q[:, 2] * s, q[:, 3] * s
     R = torch.stack([
         1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y),
@@ -106,14 +108,30 @@ def tile_bbox(xy: torch.Tensor, radius: torch.Tensor, tiles_x: int, tiles_y: int
     return x0, y0, x1, y1
 
 
+def fov_limits(fx, fy, img_width, img_height):
+    """gsplat: tan_fov = 0.5 * img_size / f (double arithmetic, stored as float), lim = 1.3f * tan_fov (float)."""
+    import numpy as np
+    tan_x = np.float32(0.5 * img_width / float(np.float32(fx)))
+    tan_y = np.float32(0.5 * img_height / float(np.float32(fy)))
+    return float(np.float32(1.3) * tan_x), float(np.float32(1.3) * tan_y)
+
+
+def _dot3(a0, a1, a2, b0, b1, b2):
+    """Canonical 3-term dot product: (a0 b0 + a1 b1) + a2 b2, every product and sum rounded (no FMA)."""
+    return (a0 * b0 + a1 * b1) + a2 * b2
+
+
 def project_gaussians(means3d, scales, glob_scale, quats, viewmat, fx, fy, cx, cy, img_height, img_width,
                       block_width, clip_thresh=0.01):
-    """project_gaussians_forward_kernel.  Returns (xys, depths, radii, conics, comp, num_tiles_hit, cov3d)."""
+    """project_gaussians_forward_kernel.  Returns (xys, depths, radii, conics, comp, num_tiles_hit, cov3d).
+
+    Canonical arithmetic (what the HIP kernel reproduces bit for bit): elementwise fp32 ops in the order
+    written, each rounded (no fused multiply-add), sums of products left to right, correctly rounded
+    division and sqrt.  gsplat's CUDA build contracts some of these into FMAs (nvcc's default), which moves
+    results by an ulp; the canonical form fixes one order so HIP vs oracle can be compared exactly."""
     means3d, scales, quats = means3d.to(f32), scales.to(f32), quats.to(f32)
     vm = viewmat.reshape(-1)[:12].to(f32)
     n = means3d.shape[0]
-    W = vm.reshape(3, 4)[:, :3]
-    tvec = vm.reshape(3, 4)[:, 3]
     px, py, pz = means3d[:, 0], means3d[:, 1], means3d[:, 2]
     tx = vm[0] * px + vm[1] * py + vm[2] * pz + vm[3]
     ty = vm[4] * px + vm[5] * py + vm[6] * pz + vm[7]
@@ -122,23 +140,26 @@ def project_gaussians(means3d, scales, glob_scale, quats, viewmat, fx, fy, cx, c
     R = quat_to_rotmat(quats)
     S = glob_scale * scales
     M = R * S[:, None, :]
-    V = M @ M.transpose(1, 2)
-    cov3d = torch.stack([V[:, 0, 0], V[:, 0, 1], V[:, 0, 2], V[:, 1, 1], V[:, 1, 2], V[:, 2, 2]], -1)
-    tan_fovx = 0.5 * img_width / fx
-    tan_fovy = 0.5 * img_height / fy
-    lim_x, lim_y = 1.3 * tan_fovx, 1.3 * tan_fovy
+    # V = M M^T (cov3d), V[r][c] = dot(M[r], M[c])
+    V = [[_dot3(M[:, r, 0], M[:, r, 1], M[:, r, 2], M[:, c, 0], M[:, c, 1], M[:, c, 2]) for c in range(3)]
+         for r in range(3)]
+    cov3d = torch.stack([V[0][0], V[0][1], V[0][2], V[1][1], V[1][2], V[2][2]], -1)
+    lim_x, lim_y = fov_limits(fx, fy, img_width, img_height)
     ctx = tz * torch.clamp(tx / tz, min=-lim_x, max=lim_x)
     cty = tz * torch.clamp(ty / tz, min=-lim_y, max=lim_y)
     rz = 1.0 / tz
     rz2 = rz * rz
-    J = torch.zeros(n, 2, 3, dtype=f32)
-    J[:, 0, 0] = fx * rz
-    J[:, 0, 2] = -fx * ctx * rz2
-    J[:, 1, 1] = fy * rz
-    J[:, 1, 2] = -fy * cty * rz2
-    T = J @ W
-    cov = T @ V @ T.transpose(1, 2)
-    c00, c01, c11 = cov[:, 0, 0], cov[:, 0, 1], cov[:, 1, 1]
+    # J = [[fx rz, 0, -fx ctx rz2], [0, fy rz, -fy cty rz2]]; T = J W (W = viewmat[:3,:3])
+    j00, j02 = fx * rz, -fx * ctx * rz2
+    j11, j12 = fy * rz, -fy * cty * rz2
+    T0 = [j00 * vm[c] + j02 * vm[8 + c] for c in range(3)]
+    T1 = [j11 * vm[4 + c] + j12 * vm[8 + c] for c in range(3)]
+    # cov2d = T V T^T
+    TV0 = [_dot3(T0[0], T0[1], T0[2], V[0][c], V[1][c], V[2][c]) for c in range(3)]
+    TV1 = [_dot3(T1[0], T1[1], T1[2], V[0][c], V[1][c], V[2][c]) for c in range(3)]
+    c00 = _dot3(TV0[0], TV0[1], TV0[2], T0[0], T0[1], T0[2])
+    c01 = _dot3(TV0[0], TV0[1], TV0[2], T1[0], T1[1], T1[2])
+    c11 = _dot3(TV1[0], TV1[1], TV1[2], T1[0], T1[1], T1[2])
     det_orig = c00 * c11 - c01 * c01
     a, b, c = c00 + 0.3, c01, c11 + 0.3
     det = a * c - b * b
@@ -164,20 +185,27 @@ def project_gaussians(means3d, scales, glob_scale, quats, viewmat, fx, fy, cx, c
 
 
 def map_gaussian_to_intersects(xys, depths, radii, cum_tiles_hit, tiles_x, tiles_y, block_width):
-    """map_gaussian_to_intersects: key = tile_id << 32 | int32 bits(depth), val = gaussian id."""
+    """map_gaussian_to_intersects: key = tile_id << 32 | int32 bits(depth), val = gaussian id; each Gaussian's
+    tiles in row-major order of its bbox, at its cumulative offset."""
     n = xys.shape[0]
     x0, y0, x1, y1 = tile_bbox(xys, radii, tiles_x, tiles_y, block_width)
     num = int(cum_tiles_hit[-1]) if n else 0
+    dbits = depths.to(f32).view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+    live = radii > 0
+    w = torch.where(live, x1 - x0, torch.zeros_like(x1)).to(torch.int64)
+    h = torch.where(live, y1 - y0, torch.zeros_like(y1)).to(torch.int64)
+    cnt = w * h
+    ids = torch.repeat_interleave(torch.arange(n), cnt)
+    start = cum_tiles_hit.to(torch.int64) - cnt  # == the exclusive cumsum for every emitting Gaussian
+    local = torch.arange(ids.numel(), dtype=torch.int64) - torch.repeat_interleave(
+        torch.cumsum(cnt, 0) - cnt, cnt)
+    ty = y0.to(torch.int64)[ids] + local // w[ids]
+    tx = x0.to(torch.int64)[ids] + local % w[ids]
+    pos = start[ids] + local
     keys = torch.zeros(num, dtype=torch.int64)
     gids = torch.zeros(num, dtype=torch.int32)
-    dbits = depths.to(f32).view(torch.int32).to(torch.int64) & 0xFFFFFFFF
-    for i in torch.nonzero(radii > 0).flatten().tolist():
-        cur = 0 if i == 0 else int(cum_tiles_hit[i - 1])
-        ty = torch.arange(int(y0[i]), int(y1[i]))
-        tx = torch.arange(int(x0[i]), int(x1[i]))
-        tid = (ty[:, None] * tiles_x + tx[None, :]).reshape(-1)
-        keys[cur:cur + tid.numel()] = (tid << 32) | dbits[i]
-        gids[cur:cur + tid.numel()] = i
+    keys[pos] = ((ty * tiles_x + tx) << 32) | dbits[ids]
+    gids[pos] = ids.to(torch.int32)
     return keys, gids
 
 

@@ -148,7 +148,10 @@ def get_padding_and_inverse(offset: torch.Tensor, patch_size: int):
     return pad, unpad
 
 
-def serialized_attention(sd, p, point: Point, C, H, patch_size_max, order_index, feat):
+def serialized_attention_heads(sd, p, point: Point, C, H, patch_size_max, order_index, feat):
+    """SerializedAttention up to (excluding) proj: the per-head softmax(q k^T d^-1/2) v of every point, heads
+    concatenated along channels, in the original point order [N, C] (restated visualize.py:140-179; pinned by
+    tests/golden/backbone_pins.npz captured from that hook)."""
     K = min(int(offset2bincount(point.offset).min()), patch_size_max)
     key = ("pad", K)
     if key not in point:
@@ -162,14 +165,20 @@ def serialized_attention(sd, p, point: Point, C, H, patch_size_max, order_index,
     attn = (q * scale) @ k.transpose(-2, -1)
     attn = torch.softmax(attn, dim=-1)
     out = (attn @ v).transpose(1, 2).reshape(-1, C)
-    out = out[inverse]
+    return out[inverse]
+
+
+def serialized_attention(sd, p, point: Point, C, H, patch_size_max, order_index, feat):
+    out = serialized_attention_heads(sd, p, point, C, H, patch_size_max, order_index, feat)
     return linear(out, sd, p + ".proj")
 
 
 # ---- Block ------------------------------------------------------------------
-def block(sd, p, point: Point, C, H, cfg: PTv3Config, order_index, conv_in=None, masks=None):
-    """Block.forward (pre_norm=True; calflops.py:45-82).  DropPath (train): `masks[p + '.attn' / '.mlp']`
-    = the per-point keep/(1-p) multipliers timm's DropPath draws (identity in eval / when absent)."""
+def block(sd, p, point: Point, C, H, cfg: PTv3Config, order_index, conv_in=None, masks=None, trace=None):
+    """Block.forward (pre_norm=True; calflops.py:45-82, pinned by tests/golden/backbone_pins.npz).  DropPath
+    (train): `masks[p + '.attn' / '.mlp']` = the per-point keep/(1-p) multipliers timm's DropPath draws
+    (identity in eval / when absent).  `trace` (a dict) receives the norm1 / norm2 outputs (attention and MLP
+    inputs) as "h1" / "h2"."""
     masks = masks or {}
     shortcut = point.feat
     x = subm_conv(point.feat if conv_in is None else conv_in, point.nbr, sd[p + ".cpe.0.weight"],
@@ -179,12 +188,16 @@ def block(sd, p, point: Point, C, H, cfg: PTv3Config, order_index, conv_in=None,
     feat = shortcut + x
     shortcut = feat
     h = ln(feat, sd, p + ".norm1.0", cfg.ln_eps)
+    if trace is not None:
+        trace["h1"] = h
     h = serialized_attention(sd, p + ".attn", point, C, H, cfg.patch_size, order_index, h)
     if masks.get(p + ".attn") is not None:
         h = h * masks[p + ".attn"][:, None]
     feat = shortcut + h
     shortcut = feat
     h = ln(feat, sd, p + ".norm2.0", cfg.ln_eps)
+    if trace is not None:
+        trace["h2"] = h
     h = linear(gelu(linear(h, sd, p + ".mlp.0.fc1")), sd, p + ".mlp.0.fc2")
     if masks.get(p + ".mlp") is not None:
         h = h * masks[p + ".mlp"][:, None]

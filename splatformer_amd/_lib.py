@@ -39,6 +39,7 @@ SIGNATURES: dict[str, list] = {
                                 P, P],
     "sfx_isect_emit": [I, P, P, P, P, I, I, I, P, P, P],
     "sfx_tile_bins": [I, P, I, P, P],
+    "sfx_profile_marker": [I, P],
     "sfx_rasterize_fwd": [I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P],
     "sfx_rasterize_bwd": [I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P],
 }

@@ -25,7 +25,7 @@ CFLAGS = [
     "-O3",
     "-fPIC",
     "-std=c++17",
-    "-ffp-contract=fast",
+    "-ffp-contract=fast-honor-pragmas",  # fused multiply-add except in `#pragma clang fp contract(off)` bodies
     "-munsafe-fp-atomics",
     "-Wno-unused-result",
     f"-I{CSRC}",
@@ -36,6 +36,17 @@ CFLAGS = [
 def _headers_mtime() -> float:
     hs = glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(ROOT, "include", "*.h"))
     return max((os.path.getmtime(h) for h in hs), default=0.0)
+
+
+def _flags_stamp() -> float:
+    """mtime of a stamp file rewritten whenever the compile flags change (so a flag change rebuilds)."""
+    stamp = os.path.join(BUILD, "flags.txt")
+    want = " ".join([HIPCC, *CFLAGS])
+    have = open(stamp).read() if os.path.exists(stamp) else None
+    if have != want:
+        with open(stamp, "w") as f:
+            f.write(want)
+    return os.path.getmtime(stamp)
 
 
 def _compile(src: str, hdr_mtime: float) -> str:
@@ -52,7 +63,7 @@ def _compile(src: str, hdr_mtime: float) -> str:
 def build(verbose: bool = False, jobs: int | None = None) -> str:
     os.makedirs(BUILD, exist_ok=True)
     srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
-    hm = _headers_mtime()
+    hm = max(_headers_mtime(), _flags_stamp())
     jobs = jobs or min(8, len(srcs))
     with cf.ThreadPoolExecutor(jobs) as ex:
         objs = list(ex.map(lambda s: _compile(s, hm), srcs))

@@ -1,6 +1,9 @@
 // Point-cloud downsampling experiments of the fork (reference models/pcd_downsampling_methods.py, selected by
 // FeaturePredictor additional_info["downsample"], reference models/feature_predictor.py:159-196):
-//   * sfx_voxel_keys -- voxel ids of voxel_downsample (:86-130): floor(p / voxel_size) in fp32, the int32 hash
+//   * sfx_voxel_keys -- voxel ids of voxel_downsample (:86-130): floor(p / voxel_size) in fp32 with the
+//     correctly rounded division (__fdiv_rn) torch's CPU true_divide computes -- the goldens were captured on the
+//     CPU; a CUDA run of the reference may compute p * (1 / voxel_size) and floor a boundary point into the
+//     neighbouring voxel, so parity against the reference's GPU run is unpinned; the int32 hash
 //     x * 1e6 + y * 1e3 + z (int32 wrap-around as torch computes it), biased to an unsigned sort key; the
 //     unique / inverse / mean steps reuse the radix sort, run-flag, scan and segment-mean kernels.
 //   * sfx_nn1 -- 1-nearest neighbour of every query among the reference points (sklearn NearestNeighbors in

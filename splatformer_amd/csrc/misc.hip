@@ -80,3 +80,15 @@ int sfx_offsets_to_batch(int n, int B, const long long* offsets, int* batch, voi
 }
 
 }  // extern "C"
+
+// ---- profiling marker ------------------------------------------------------------------------------------------
+// sfx_profile_marker: an empty one-lane kernel whose dispatches delimit units of work (one scene / one training
+// step) in a rocprofv3 PMC or kernel trace, where roctx markers are unavailable (bench.py measure_traffic).
+namespace {
+__global__ void profile_marker_kernel(int) {}
+}  // namespace
+
+extern "C" int sfx_profile_marker(int tag, void* stream) {
+  profile_marker_kernel<<<1, 1, 0, sfx::as_stream(stream)>>>(tag);
+  return sfx::check_launch("sfx_profile_marker");
+}

@@ -129,8 +129,13 @@ struct M3 {  // row-major 3x3
   float m[3][3];
 };
 
+// Canonical arithmetic of the projection (oracle/gsplat_ref.py project_gaussians): every fp32 product and sum
+// rounded on its own (contraction off in these bodies; the library builds with -ffp-contract=fast-honor-pragmas), sums of
+// products left to right, correctly rounded division and sqrt (1/sqrt instead of an approximate rsqrt) --
+// radii, tile counts, intersection keys and the projected floats are bit-identical to the oracle.
 __device__ __forceinline__ M3 quat_to_rotmat(float qw, float qx, float qy, float qz) {
-  const float s = rsqrtf(qw * qw + qx * qx + qy * qy + qz * qz);
+#pragma clang fp contract(off)
+  const float s = 1.f / sqrtf(((qw * qw + qx * qx) + qy * qy) + qz * qz);
   const float w = qw * s, x = qx * s, y = qy * s, z = qz * s;
   M3 R;
   R.m[0][0] = 1.f - 2.f * (y * y + z * z);
@@ -166,6 +171,7 @@ __device__ __forceinline__ void project_point(int i, float px, float py, float p
                                               float* __restrict__ depths, int* __restrict__ radii,
                                               float* __restrict__ conics, float* __restrict__ comp,
                                               int* __restrict__ num_tiles_hit, float* __restrict__ cov3d) {
+#pragma clang fp contract(off)
   const int tiles_x = (img_w + bw - 1) / bw, tiles_y = (img_h + bw - 1) / bw;
   float o_xy0 = 0.f, o_xy1 = 0.f, o_depth = 0.f, o_comp = 0.f;
   float o_con0 = 0.f, o_con1 = 0.f, o_con2 = 0.f;
@@ -190,11 +196,13 @@ __device__ __forceinline__ void project_point(int i, float px, float py, float p
 #pragma unroll
     for (int r = 0; r < 3; ++r)
 #pragma unroll
-      for (int c = 0; c < 3; ++c) V[r][c] = M[r][0] * M[c][0] + M[r][1] * M[c][1] + M[r][2] * M[c][2];
+      for (int c = 0; c < 3; ++c) V[r][c] = (M[r][0] * M[c][0] + M[r][1] * M[c][1]) + M[r][2] * M[c][2];
     cv[0] = V[0][0]; cv[1] = V[0][1]; cv[2] = V[0][2];
     cv[3] = V[1][1]; cv[4] = V[1][2]; cv[5] = V[2][2];
     // EWA: t clamped to 1.3 tan_fov frustum
-    const float tan_fovx = 0.5f * (float)img_w / fx, tan_fovy = 0.5f * (float)img_h / fy;
+    // gsplat: tan_fov = 0.5 * img_size / f in double, stored as float; lim = 1.3f * tan_fov in float
+    const float tan_fovx = (float)(0.5 * (double)img_w / (double)fx);
+    const float tan_fovy = (float)(0.5 * (double)img_h / (double)fy);
     const float lim_x = 1.3f * tan_fovx, lim_y = 1.3f * tan_fovy;
     const float ctx = tz * fminf(lim_x, fmaxf(-lim_x, tx / tz));
     const float cty = tz * fminf(lim_y, fmaxf(-lim_y, ty / tz));
@@ -212,12 +220,12 @@ __device__ __forceinline__ void project_point(int i, float px, float py, float p
     float TV0[3], TV1[3];
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-      TV0[c] = T0[0] * V[0][c] + T0[1] * V[1][c] + T0[2] * V[2][c];
-      TV1[c] = T1[0] * V[0][c] + T1[1] * V[1][c] + T1[2] * V[2][c];
+      TV0[c] = (T0[0] * V[0][c] + T0[1] * V[1][c]) + T0[2] * V[2][c];
+      TV1[c] = (T1[0] * V[0][c] + T1[1] * V[1][c]) + T1[2] * V[2][c];
     }
-    const float c00 = TV0[0] * T0[0] + TV0[1] * T0[1] + TV0[2] * T0[2];
-    const float c01 = TV0[0] * T1[0] + TV0[1] * T1[1] + TV0[2] * T1[2];
-    const float c11 = TV1[0] * T1[0] + TV1[1] * T1[1] + TV1[2] * T1[2];
+    const float c00 = (TV0[0] * T0[0] + TV0[1] * T0[1]) + TV0[2] * T0[2];
+    const float c01 = (TV0[0] * T1[0] + TV0[1] * T1[1]) + TV0[2] * T1[2];
+    const float c11 = (TV1[0] * T1[0] + TV1[1] * T1[1]) + TV1[2] * T1[2];
     const float det_orig = c00 * c11 - c01 * c01;
     const float a = c00 + 0.3f, b = c01, c = c11 + 0.3f;
     const float det_blur = a * c - b * b;
@@ -298,6 +306,9 @@ __global__ void render_prep_project_kernel(int n, int num_bases, const float* __
                                            float* __restrict__ opac, float* __restrict__ xys,
                                            float* __restrict__ depths, int* __restrict__ radii,
                                            float* __restrict__ conics, int* __restrict__ num_tiles_hit) {
+  // canonical glue arithmetic (oracle/render_ref.py glue_args(canonical=True)): exp / sigmoid in double rounded
+  // once, norms as left-to-right sums with a correctly rounded sqrt, no contraction
+#pragma clang fp contract(off)
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   // batched views: blockIdx.y = view, cameras [V,4,4], every output offset by view * n records
   const int view = blockIdx.y;
@@ -321,7 +332,7 @@ __global__ void render_prep_project_kernel(int n, int num_bases, const float* __
   for (int r = 0; r < 3; ++r) {
 #pragma unroll
     for (int c = 0; c < 3; ++c) vm[4 * r + c] = R[c][r];
-    vm[4 * r + 3] = -(R[0][r] * t[0] + R[1][r] * t[1] + R[2][r] * t[2]);
+    vm[4 * r + 3] = -((R[0][r] * t[0] + R[1][r] * t[1]) + R[2][r] * t[2]);
   }
   if (i == 0 && viewmat_out)
 #pragma unroll
@@ -332,22 +343,22 @@ __global__ void render_prep_project_kernel(int n, int num_bases, const float* __
   const float* qp = quats_raw + i * ld.quats;
   const float* dcp = dc + i * ld.dc;
   const float px = mp[0], py = mp[1], pz = mp[2];
-  const float sc0 = expf(sp[0]), sc1 = expf(sp[1]), sc2 = expf(sp[2]);
+  const float sc0 = (float)exp((double)sp[0]), sc1 = (float)exp((double)sp[1]), sc2 = (float)exp((double)sp[2]);
   float q0 = qp[0], q1 = qp[1], q2 = qp[2], q3 = qp[3];
-  const float qn = sqrtf(q0 * q0 + q1 * q1 + q2 * q2 + q3 * q3);
+  const float qn = sqrtf(((q0 * q0 + q1 * q1) + q2 * q2) + q3 * q3);
   q0 /= qn; q1 /= qn; q2 /= qn; q3 /= qn;
   if (isnan(q0) || isnan(q1) || isnan(q2) || isnan(q3)) {
     q0 = 0.f; q1 = 0.f; q2 = 0.f; q3 = 1.f;
   }
-  opac[i] = 1.f / (1.f + expf(-opac_logit[i * ld.opac]));
+  opac[i] = (float)(1.0 / (1.0 + exp(-(double)opac_logit[i * ld.opac])));
   // colours
   const int degree = num_bases >= 25 ? 4 : num_bases >= 16 ? 3 : num_bases >= 9 ? 2 : num_bases >= 4 ? 1 : 0;
   if (degree == 0) {
 #pragma unroll
-    for (int ch = 0; ch < 3; ++ch) rgbs[3 * i + ch] = 1.f / (1.f + expf(-dcp[ch]));
+    for (int ch = 0; ch < 3; ++ch) rgbs[3 * i + ch] = (float)(1.0 / (1.0 + exp(-(double)dcp[ch])));
   } else {
     float vx = px - t[0], vy = py - t[1], vz = pz - t[2];
-    const float vn = sqrtf(vx * vx + vy * vy + vz * vz);
+    const float vn = sqrtf((vx * vx + vy * vy) + vz * vz);
     if (vn == 0.f) {  // reference draws a random direction here (gs_utils.py:72-76); we use +z
       vx = 0.f; vy = 0.f; vz = 1.f;
     } else {

@@ -85,10 +85,19 @@ def voxel_downsample_map_logits_to_original(points: Tensor, downsampled_points: 
     return logits.index_select(0, inverse.long())
 
 
-def furthest_point_sampling(xyz: Tensor, npoint: int) -> Tensor:
+def furthest_point_sampling(xyz: Tensor, npoint: int, start: int = None) -> Tensor:
+    """Indices of `npoint` furthest-point picks; `start` (the first pick) is drawn as the reference draws it
+    when None (tests pass the golden's first pick to pin the deterministic part)."""
     _lib.require_gpu(xyz)
     N = xyz.shape[0]
-    start = int(torch.randint(0, N, (1,)).item())  # the reference's draw (device-independent CPU generator)
+    if N == 0 or npoint <= 0:
+        raise ValueError(f"furthest_point_sampling: need N > 0 and npoint > 0 (got N={N}, npoint={npoint})")
+    # the reference's draw on the points' device (pcd_downsampling_methods.py:17): the device generator, as the
+    # reference's GPU run does; parity of this device draw against a CUDA run is unpinned (the goldens are CPU)
+    if start is None:
+        start = int(torch.randint(0, N, (1,), device=xyz.device).item())
+    if not 0 <= start < N:
+        raise ValueError(f"furthest_point_sampling: start {start} out of range [0, {N})")
     pts = _xyz(xyz)
     out = torch.empty(npoint, device=xyz.device, dtype=torch.int32)
     ws = torch.empty(N, device=xyz.device, dtype=torch.float32)
@@ -99,16 +108,20 @@ def furthest_point_sampling(xyz: Tensor, npoint: int) -> Tensor:
 def nn1(queries: Tensor, refs: Tensor) -> Tensor:
     """Index of the nearest reference point for every query (the sklearn 1-NN query of the reference)."""
     q, r = _xyz(queries), _xyz(refs)
+    if r.shape[0] == 0 and q.shape[0] > 0:
+        raise ValueError("nn1: empty reference set (a downsampling ratio that keeps no point)")
     out = torch.empty(q.shape[0], device=q.device, dtype=torch.int32)
     call("sfx_nn1", q.shape[0], r.shape[0], ptr(q), ptr(r), ptr(out), stream())
     return out
 
 
-def fps_knn_downsample(points: Tensor, features: Tensor, grid_coords: Tensor, ratio: float):
+def fps_knn_downsample(points: Tensor, features: Tensor, grid_coords: Tensor, ratio: float, start: int = None):
     """-> (points [M,3], features [M,C], grid coords [M,3] long, assignments [N] long)."""
     N = points.shape[0]
     M = int(N * ratio)
-    centroid_idx = furthest_point_sampling(points, M)
+    if M <= 0:
+        raise ValueError(f"fps_knn_downsample: int(N * ratio) = {M} keeps no point (N={N}, ratio={ratio})")
+    centroid_idx = furthest_point_sampling(points, M, start)
     centroids = points[centroid_idx]
     assignments = nn1(points, centroids)
     keys = assignments.to(torch.int64)
@@ -126,6 +139,8 @@ def map_to_original_from_centroids(downsampled_features: Tensor, assignments: Te
 def random_downsample(points: Tensor, features: Tensor, grid_coord: Tensor, ratio: float):
     N = points.shape[0]
     M = int(N * ratio)
+    if M <= 0:
+        raise ValueError(f"random_downsample: int(N * ratio) = {M} keeps no point (N={N}, ratio={ratio})")
     indices = torch.randperm(N)[:M].to(points.device)  # the reference's host draw
     return points[indices], features[indices], grid_coord[indices], indices
 

@@ -124,7 +124,17 @@ def _render_fused(gs, c2w, cx, cy, fx, fy, W, H, background):
     return rgb, alpha.unsqueeze(-1)
 
 
-def _render_fused_views(gs, c2ws, cameras):
+def render_views_meta(gs_params: Dict[str, Tensor], cameras: Dict):
+    """The batched eval path of rasterize_gaussians_to_multiimgs, also returning its intermediate device buffers
+    (per-view projection records, intersection keys / ids after the sort, tile bins) for parity checks and
+    tools.  -> (rgbs, alphas, meta)."""
+    gp = {k: v.float() if v.dtype == torch.half else v for k, v in gs_params.items()}
+    meta: Dict = {}
+    rgbs, alphas = _render_fused_views(gp, cameras["camera_to_worlds"], cameras, meta=meta)
+    return rgbs, alphas, meta
+
+
+def _render_fused_views(gs, c2ws, cameras, meta=None):
     means = gs["means"]
     _lib.require_gpu(means)
     dev = means.device
@@ -180,6 +190,12 @@ def _render_fused_views(gs, c2ws, cameras):
         if per_view[v] < 1:
             out[v] = torch.clamp(bg, max=1.0).expand(H, W, 3)
             alpha[v] = 1.0
+    if meta is not None:
+        meta.update(rgbs=rgbs, opacities=opac, xys=xys, depths=depths, radii=radii, conics=conics,
+                    num_tiles_hit=tiles.view(V, n), per_view=per_view, tiles_x=tiles_x, tiles_y=tiles_y)
+        if total > 0:
+            meta.update(isect_sorted=isect_s, gids_sorted=gids_s, tile_bins=bins.view(V, T, 2), final_Ts=final_Ts,
+                        final_idx=final_idx)
     return list(out.unbind(0)), list(alpha.unsqueeze(-1).unbind(0))
 
 
@@ -232,5 +248,5 @@ def _render_autograd(gs_params, camera_to_world, cx, cy, fx, fy, W, H, backgroun
     return rgb, alpha
 
 
-__all__ = ["rasterize_gaussians_to_multiimgs", "rasterize_gaussians_to_singleimg", "BLOCK_WIDTH", "SH2RGB", "RGB2SH",
+__all__ = ["rasterize_gaussians_to_multiimgs", "rasterize_gaussians_to_singleimg", "render_views_meta", "BLOCK_WIDTH", "SH2RGB", "RGB2SH",
            "bin_and_sort_gaussians", "compute_cumulative_intersects"]

@@ -72,28 +72,36 @@ def new_amax(device) -> Tuple[int, int]:
     return buf.data_ptr() + 8 * AMAX_SUB * st[1], st[2]
 
 
+def _own_slot(device) -> Tuple[Tensor, Tuple[int, int]]:
+    """A dedicated, never-recycled amax slot (its own zeroed 64-u64 buffer, tag 1) for a cached bound: the ring
+    of `new_amax` wraps every _AMAX_RING launches, after which a later producer would overwrite a cached slot."""
+    buf = torch.zeros(AMAX_SUB, dtype=torch.int64, device=device)
+    return buf, (buf.data_ptr(), 1)
+
+
 def weight_amax(w: Tensor) -> Tuple[int, int]:
-    """max |W| of a weight matrix (2-D view), cached on the tensor until its storage or version changes."""
+    """max |W| of a weight matrix (2-D view), cached on the tensor (in its own slot) until its storage or version
+    changes."""
     key = (w.data_ptr(), w._version, tuple(w.shape))
     c = getattr(w, "_sfx_wamax", None)
     if c is not None and c[0] == key:
-        return c[1]
+        return c[2]
     w2 = w.reshape(w.shape[0], -1)
-    slot = new_amax(w.device)
+    buf, slot = _own_slot(w.device)
     call("sfx_amax_f32", w2.shape[0], w2.shape[1], ptr(w2), w2.stride(0), slot[0], slot[1], stream())
-    w._sfx_wamax = (key, slot)
+    w._sfx_wamax = (key, buf, slot)
     return slot
 
 
 def ln_amax(gamma: Tensor, beta: Tensor) -> Tuple[int, int]:
-    """Bound sqrt(C-1) max|gamma| + max|beta| of a LayerNorm's outputs, cached on gamma."""
+    """Bound sqrt(C-1) max|gamma| + max|beta| of a LayerNorm's outputs, cached on gamma (in its own slot)."""
     key = (gamma.data_ptr(), gamma._version, beta.data_ptr(), beta._version)
     c = getattr(gamma, "_sfx_lnamax", None)
     if c is not None and c[0] == key:
-        return c[1]
-    slot = new_amax(gamma.device)
+        return c[2]
+    buf, slot = _own_slot(gamma.device)
     call("sfx_ln_amax_bound", gamma.shape[0], ptr(gamma), ptr(beta), slot[0], slot[1], stream())
-    gamma._sfx_lnamax = (key, slot)
+    gamma._sfx_lnamax = (key, buf, slot)
     return slot
 
 

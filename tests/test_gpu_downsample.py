@@ -42,11 +42,10 @@ def test_random_downsample_golden(device):
 
 def test_fps_knn_golden(device):
     pts, feat, grid = dev_(G["points"], device), dev_(G["feat"], device), dev_(G["grid"], device)
-    torch.manual_seed(int(G["fps_seed"]))
-    cidx = ds.furthest_point_sampling(pts, 300)
+    start = int(G["fps_centroids"][0])  # the reference's CPU draw; the product draws on the device generator
+    cidx = ds.furthest_point_sampling(pts, 300, start)
     assert np.array_equal(cidx.cpu().numpy(), G["fps_centroids"])
-    torch.manual_seed(int(G["fps_seed"]))
-    p, f, g, a = ds.fps_knn_downsample(pts, feat, grid, float(G["fps_ratio"]))
+    p, f, g, a = ds.fps_knn_downsample(pts, feat, grid, float(G["fps_ratio"]), start=start)
     assert np.array_equal(a.cpu().numpy(), G["fps_assign"])
     assert np.array_equal(p.cpu().numpy(), G["fps_points"]) and np.array_equal(f.cpu().numpy(), G["fps_feat"])
     assert np.array_equal(g.cpu().numpy(), G["fps_grid"])
@@ -65,9 +64,9 @@ def test_fps_vs_oracle_larger(device):
     from splatformer_amd.scenes import make_scene
     pts = make_scene(20000, 1, seed=3)["means"].float()
     torch.manual_seed(5)
-    got = ds.furthest_point_sampling(pts.to(device), 1000).cpu().numpy()
-    torch.manual_seed(5)
-    ref = D.furthest_point_sampling(pts.numpy(), 1000, D.fps_start(20000))
+    st = D.fps_start(20000)
+    got = ds.furthest_point_sampling(pts.to(device), 1000, st).cpu().numpy()
+    ref = D.furthest_point_sampling(pts.numpy(), 1000, st)
     assert np.array_equal(got, ref)
 
 
@@ -89,3 +88,17 @@ def test_refine_with_downsampling(device, method, info):
         outs.append(model.refine_packed(scene, perms=[[0, 1, 2, 3]] * 5).clone())
     assert outs[0].shape[0] == 3000 and torch.isfinite(outs[0]).all()
     assert float((outs[0] - outs[1]).norm() / outs[1].norm()) < 1e-5
+
+
+def test_empty_samples_rejected(device):
+    """A ratio with int(N * ratio) == 0 keeps no point: rejected on the host (the 1-NN map-back would index an
+    empty tensor)."""
+    pts = torch.rand(100, 3, device=device)
+    feat = torch.rand(100, 4, device=device)
+    grid = (pts * 384).int()
+    with pytest.raises(ValueError):
+        ds.fps_knn_downsample(pts, feat, grid, 0.001)
+    with pytest.raises(ValueError):
+        ds.random_downsample(pts, feat, grid, 0.001)
+    with pytest.raises(ValueError):
+        ds.nn1(pts, pts[:0])

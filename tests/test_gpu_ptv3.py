@@ -42,9 +42,9 @@ def test_linear_vs_torch(device, M, N, K, act):
 
 @pytest.mark.parametrize("scale", [1.0, 1e-30, 1e30])
 def test_linear_split_precision_is_fp32(device, scale):
-    """The 3-term bf16 split GEMM (default for K >= 64) is as accurate as fp32 arithmetic: its error against
-    an fp64 product is at most that of torch's fp32 CPU GEMM (x1.5), at any magnitude bf16 shares with fp32
-    (no scaling, no overflow: operands at 1e+-30)."""
+    """The fp16x2 split GEMM (default for K >= 64: power-of-two operand scales, two fp16 terms per operand,
+    three term products) is as accurate as fp32 arithmetic: its error against an fp64 product is at most that
+    of torch's fp32 CPU GEMM (x1.5), at operand magnitudes 1e+-30 (the scales absorb them)."""
     g = torch.Generator().manual_seed(7)
     M, N, K = 2000, 384, 1024
     x = torch.randn(M, K, generator=g) * scale
@@ -55,6 +55,26 @@ def test_linear_split_precision_is_fp32(device, scale):
     e_f32 = rel_l2(x @ w.T, ref)
     assert torch.isfinite(y).all()
     assert e_hip <= 1.5 * e_f32, (e_hip, e_f32)
+
+
+@pytest.mark.parametrize("span", [10, 20])
+def test_linear_split_rows_wide_dynamic_range(device, span):
+    """Rows whose magnitudes span 2^-span .. 2^span (of each other) keep fp32 accuracy row by row: every row's
+    error against fp64 is within 2x (+ fp32 rounding of the row's own scale) of torch's fp32 CPU GEMM's."""
+    g = torch.Generator().manual_seed(span)
+    M, N, K = 1024, 256, 512
+    e = torch.linspace(-span, span, M)
+    x = torch.randn(M, K, generator=g) * torch.exp2(e)[:, None]
+    w = torch.randn(N, K, generator=g) / K ** 0.5
+    ref = x.double() @ w.double().T
+    y = ops.linear(x.to(device), w.to(device), None).cpu().double()
+    f32 = (x @ w.T).double()
+    rn = ref.norm(dim=1)
+    e_hip = (y - ref).norm(dim=1) / rn
+    e_f32 = (f32 - ref).norm(dim=1) / rn
+    worst = int(torch.argmax(e_hip / (e_f32 + 1e-7)))
+    assert bool((e_hip <= 2 * e_f32 + 1e-7).all()), \
+        f"row {worst} (2^{float(e[worst]):.1f}): rel err {float(e_hip[worst]):.3e} vs fp32 {float(e_f32[worst]):.3e}"
 
 
 def test_linear_gather_is_subm_conv(device):
@@ -326,3 +346,20 @@ def test_gemm_every_tile_config(device, cfg):
                 assert rel_l2(y3.cpu(), ref2) < 2e-6, (cfg, sk, cin, "conv")
     finally:
         ops.gemm_force_config(-1, -1)
+
+
+def test_cached_bounds_survive_amax_ring_wrap(device):
+    """Cached weight / LayerNorm bounds live in their own slots: after more than the ring's worth of producer
+    slots (each filled with a larger tag and a huge value, as later producers would) a second forward of the
+    same model gives the same outputs (a recycled cached slot read 0 or a too-small bound)."""
+    model = _model(9).to(device)
+    s = to_device(make_scene(3000, 1, seed=4, unique_voxels=True), device)
+    perms = [[0, 1, 2, 3]] * 5
+    out1 = {k: v.clone() for k, v in model([s], [0], perms=perms)[0].items()}
+    for _ in range(ops._AMAX_RING + 8):
+        ops.new_amax(device)
+    huge = (0x7FFFFFF0 << 32) | int(np.float32(1e30).view(np.uint32))
+    ops._amax_state[device][0].fill_(huge)  # every ring slot now carries a newer tag than any cached one
+    out2 = model([s], [0], perms=perms)[0]
+    for k in out1:
+        assert torch.equal(out1[k], out2[k]), k

@@ -1,9 +1,11 @@
 """HIP render path (libsfx) vs the gsplat v0.1.11 CPU oracle on identical inputs.
 
-Tolerances: fp32 kernels vs fp32 oracle -- 1e-5 relative on per-Gaussian
-projections, 1e-4 absolute on images, |dPSNR| <= 1e-4 dB on uint8-quantised
-renders (BASELINE.json north_star); integer/index outputs (radii, tile
-counts, sorted intersection ids, tile bins) bit-exact.
+Tolerances: the projection follows the oracle's canonical arithmetic (no
+contraction, left-to-right sums, correctly rounded division/sqrt), so every
+projection output -- integer and float -- is bit-exact; integer/index outputs
+(radii, tile counts, sorted intersection ids, tile bins) bit-exact; images
+within 2e-4 absolute and |dPSNR| <= 1e-4 dB on uint8-quantised renders
+(BASELINE.json north_star).  Full-size workloads: tests/test_gpu_full.py.
 """
 import math
 
@@ -46,9 +48,12 @@ def _proj_inputs(n, seed, W=160, H=120):
     return a, cams, W, H
 
 
-@pytest.mark.parametrize("seed", [0, 4, 8])
-def test_project_fwd(device, seed):
-    a, cams, W, H = _proj_inputs(5000, seed)
+@pytest.mark.parametrize("seed,n,W,H", [(0, 5000, 160, 120), (4, 5000, 160, 120), (8, 5000, 160, 120),
+                                         (2, 100_000, 800, 800)])
+def test_project_fwd(device, seed, n, W, H):
+    """Every output bit-exact (round 1 tolerated max(2, n/2000) integer mismatches; 0 measured at 100k x 9
+    views 800x800 before the canonical-arithmetic change, profiles/r02_proj_mismatch_before.json)."""
+    a, cams, W, H = _proj_inputs(n, seed, W, H)
     args = (a["means"], a["scales"], 1.0, a["quats"], a["viewmat"], cams["fx"], cams["fy"], cams["cx"], cams["cy"], H,
             W, 16)
     ref = gsplat_ref.project_gaussians(*args)
@@ -57,11 +62,9 @@ def test_project_fwd(device, seed):
     names = ["xys", "depths", "radii", "conics", "comp", "num_tiles_hit", "cov3d"]
     for nm, r, o in zip(names, ref, out):
         o = o.cpu()
-        if r.dtype == torch.int32:
-            mism = (r != o).sum().item()
-            assert mism <= max(2, r.numel() // 2000), f"{nm}: {mism} integer mismatches"
-        else:
-            torch.testing.assert_close(o, r, rtol=2e-5, atol=1e-5, msg=nm)
+        assert r.dtype == o.dtype and r.shape == o.shape, nm
+        mism = (r != o).sum().item()
+        assert mism == 0, f"{nm}: {mism} mismatches (max |d| {(r.double() - o.double()).abs().max().item():.3e})"
 
 
 def test_scan_and_sort_exact(device):

@@ -8,7 +8,7 @@ mkdir -p build/exp_$name
 for f in splatformer_amd/csrc/*.hip; do
   b=$(basename $f .hip)
   if [ $b = gemm ]; then
-    /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -ffp-contract=fast -munsafe-fp-atomics \
+    /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -ffp-contract=fast-honor-pragmas -munsafe-fp-atomics \
       -Wno-unused-result -Isplatformer_amd/csrc -Iinclude "$@" -c $f -o build/exp_$name/gemm.o
   else
     cp build/sfx/$b.o build/exp_$name/
