@@ -39,7 +39,7 @@ def glue_args(gs_params, camera_to_world, canonical=False):
     this CPU; torch's vectorised exp / norm / 3x3 matmul round in implementation-defined ways).
     canonical=True: the same math in the machine-independent arithmetic the fused HIP prep kernel reproduces
     bit for bit -- exp / sigmoid in float64 rounded once, norms as left-to-right sums of rounded squares with
-    a correctly rounded sqrt, the viewmat's -R^T t as a left-to-right sum; within 1-2 ulp of the torch form
+    a correctly rounded sqrt (gsplat_ref.sqrt_rn: torch's CPU float32 sqrt is not correctly rounded), the viewmat's -R^T t as a left-to-right sum; within 1-2 ulp of the torch form
     (tests/test_golden_glue.py)."""
     gs_params = {k: v.float() if v.dtype == torch.half else v for k, v in gs_params.items()}
     if canonical:
@@ -58,7 +58,7 @@ def glue_args(gs_params, camera_to_world, canonical=False):
     q = gs_params["quats"]
     if canonical:
         scales = _exp_c(gs_params["scales"])
-        qn = torch.sqrt(((q[:, 0] * q[:, 0] + q[:, 1] * q[:, 1]) + q[:, 2] * q[:, 2]) + q[:, 3] * q[:, 3])[:, None]
+        qn = gsplat_ref.sqrt_rn(((q[:, 0] * q[:, 0] + q[:, 1] * q[:, 1]) + q[:, 2] * q[:, 2]) + q[:, 3] * q[:, 3])[:, None]
         quats = q / qn
     else:
         scales = torch.exp(gs_params["scales"])                               # :45
@@ -84,7 +84,7 @@ def glue_args(gs_params, camera_to_world, canonical=False):
     else:
         vd = means - camera_to_world[:3, 3]                               # :67
         if canonical:
-            nrm = torch.sqrt((vd[:, 0] * vd[:, 0] + vd[:, 1] * vd[:, 1]) + vd[:, 2] * vd[:, 2])[:, None]
+            nrm = gsplat_ref.sqrt_rn((vd[:, 0] * vd[:, 0] + vd[:, 1] * vd[:, 1]) + vd[:, 2] * vd[:, 2])[:, None]
         else:
             nrm = vd.norm(dim=-1, keepdim=True)
         viewdirs = vd / nrm

