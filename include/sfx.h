@@ -120,7 +120,16 @@ int sfx_linear(int M, int N, int K, const float* A, long long lda, const int* ga
                long long group_stride_bias, long long group_stride_Y, const int* out_row_idx, const float* rowscale,
                int pre_before_act, const unsigned long long* a_amax, unsigned a_tag,
                const unsigned long long* w_amax, unsigned w_tag, unsigned long long* y_amax, unsigned y_tag,
-               void* stream);
+               const float* w_split, const float* w_inv, void* stream);
+
+/* Pre-split weight for the fp16x2 GEMMs (ABI v5): dst has W's [rows x cols] shape in 4-byte units, contiguous;
+ * every group of 4 consecutive elements of a row holds 4 fp16 h terms then 4 fp16 l terms of
+ * W[n, k..k+3] * 2^e_n, where 2^e_n puts the row's largest magnitude in [2^14, 2^15); w_inv[n] = 2^-e_n.
+ * cols and ld multiples of 4, buffers 16-byte aligned.  Passing (w_split, w_inv) of a weight to sfx_linear /
+ * sfx_subm_conv / sfx_linear_bwd_data / sfx_subm_conv_bwd_data (split of the matrix passed as W / weight / Wt)
+ * selects the warp-specialised kernel, which also scales every row of A' by its own power of two (chosen
+ * online from the row's values), so no operand maxima are needed; NULL keeps the amax-slot form. */
+int sfx_weight_split(int rows, int cols, const float* w, long long ld, float* w_split, float* w_inv, void* stream);
 
 /* fp16x2 operand maxima ("amax slots").  The GEMMs run K >= 64 products on split operands: fp16x2 by default
  * (a power-of-two scale per operand from an upper bound of its largest magnitude; SFX_GEMM_PREC=bf16x3 or fp32
@@ -147,7 +156,8 @@ int sfx_gemm_force_config(int cfg, int stream_k);
  * feeds it (reference models run under train.py:240-289 `total_loss.backward()`). */
 int sfx_linear_bwd_data(int M, int N, int K, const float* dY, long long ldy, const float* Wt, long long ldwt,
                         const float* rowscale, int dact, int dact_ncols, const float* dact_pre, long long ld_pre,
-                        float* dX, long long lddx, int accumulate, void* stream);
+                        float* dX, long long lddx, int accumulate, const float* wt_split, const float* wt_inv,
+                        void* stream);
 /* dW[N,K] += dY[M,N]^T X[M,K]; db[N] += sum_m dY[m,:] (db may be NULL).  Accumulates (float atomics). */
 int sfx_linear_wgrad(int M, int N, int K, const float* dY, long long ldy, const float* X, long long ldx, float* dW,
                      long long ldw, float* db, void* stream);
@@ -161,7 +171,8 @@ int sfx_transpose(int rows, int cols, const float* src, long long lds, float* ds
  * transposed to [27*Cin, Cout]; centre_ws = 2n ints scratch; dX accumulates (float atomics). */
 int sfx_subm_conv_bwd_data(int n, int cin, int cout, const float* dy, long long ldy, const int* nbr,
                            const float* weight_t, const int* pair_in, const int* pair_out, const int* pair_off_host,
-                           int* centre_ws, float* dx, long long lddx, void* stream);
+                           int* centre_ws, float* dx, long long lddx, const float* wt_split, const float* wt_inv,
+                           void* stream);
 /* non-flash SerializedAttention backward (visualize.py:140-179 math): dout [N, C] = grad of the attention
  * output rows; dqkv [N, 3C] must be zero-filled (dK/dV accumulate across overlapping windows). */
 int sfx_window_attention_bwd(int num_windows, int window, int heads, int head_dim, int channels, const float* qkv,
@@ -272,7 +283,8 @@ int sfx_subm_pairs(int n, const int* nbr, void* ws, size_t ws_bytes, int* pair_i
 int sfx_subm_conv(int n, int cin, int cout, const float* x, long long ldx, const int* nbr, const float* weight,
                   const float* bias, const int* pair_in, const int* pair_out, const int* pair_off_host, float* out,
                   long long ldo, const unsigned long long* x_amax, unsigned x_tag,
-                  const unsigned long long* w_amax, unsigned w_tag, void* stream);
+                  const unsigned long long* w_amax, unsigned w_tag, const float* w_split, const float* w_inv,
+                  void* stream);
 
 /* FeaturePredictor batchify (feature_predictor.py:134-156): strided attribute rows -> feat rows
  * [means,scales,opacities,quats,dc,rest], grid_coord = floor(means*res), optional atomic grid max. */

@@ -23,147 +23,23 @@
 // the descriptor's extent, so loads return 0 and stores are dropped by the
 // hardware -- no per-element branches, which hipcc would otherwise turn into
 // one `s_waitcnt vmcnt(0)` per load and serialise the prefetch.
+#include <climits>
 #include <cstdlib>
 #include <cstring>
 #include <type_traits>
 
-#include "common.h"
+#include "gemm_common.h"
 
 namespace {
 
-typedef float floatx16 __attribute__((ext_vector_type(16)));
-typedef float floatx4 __attribute__((ext_vector_type(4)));
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+using namespace sfxg;
 
-constexpr int BK = 32;
-// residency: persistent workgroups per CU for the four- and eight-wave tiles, LDS buffers of the eight-wave ones
-#ifndef SFX_PERCU4
-#define SFX_PERCU4 2
-#endif
-#ifndef SFX_PERCU8
-#define SFX_PERCU8 1
-#endif
-#ifndef SFX_NBUF8
-#define SFX_NBUF8 2
-#endif
-constexpr int kPerCu4 = SFX_PERCU4, kPerCu8 = SFX_PERCU8;
-constexpr int LDS_STRIDE = BK + 4;
-constexpr int THREADS = 256;
-constexpr unsigned OOB = 0x7ffffff0u;        // byte offset past every descriptor extent
-constexpr int RSRC_FLAGS = 0x00020000;       // gfx950 raw buffer, 32-bit data
-
-enum Act { ACT_NONE = 0, ACT_GELU = 1, ACT_RELU = 2, ACT_TANH = 3 };
-
-struct GemmArgs {
-  int M, N, K;         // K = S * Kseg when gathering
-  const float* A;
-  long long lda;
-  const int* gidx;     // gather index, row stride gstride, or null
-  int S, Kseg, gstride;
-  const float* W;      // [N, K] (row stride ldw)
-  long long ldw;
-  const float* bias;   // [N] or null
-  const float* scale;  // [N] or null  (folded BatchNorm)
-  const float* shift;  // [N] or null
-  int act, act_ncols;  // act applies to columns < act_ncols
-  const float* R;      // residual [*, ldr] or null
-  long long ldr;
-  const int* ridx;     // residual row index (by output row) or null
-  float* Y;
-  long long ldy;
-  float* Ypre;         // optional copy of the pre-residual value
-  long long ldypre;
-  long long gA, gW, gB, gY;  // grouped GEMM (blockIdx.z): per-group element strides
-  const int* out_rows;       // tile row -> output row (or null)
-  // offset-major sparse conv ("pair mode"): blockIdx.x walks a flat tile list over up to 27 slices;
-  // slice k gathers A rows pair_in[pair_off[k] ..] and atomically adds into rows pair_out[...] with the
-  // weight slice W + k * slice_w_stride.
-  int pair_mode;
-  const int* pair_in;
-  const int* pair_out;
-  int slice_tile_off[28];
-  int slice_pair_off[28];
-  int num_slices;
-  long long slice_w_stride;
-  // backward-pass epilogue terms (applied after the activation): v *= rowscale[row] (drop-path masks),
-  // v *= act'(dact_pre[row, col]) for cols < act_ncols (GELU / ReLU on the pre-activation, tanh on its output)
-  const float* rowscale;
-  int pre_before_act;  // Ypre receives the pre-activation value (training forward saves it for act')
-  const float* dact_pre;
-  long long ld_dact;
-  int dact;
-  // Stream-K: the tiles x K-slabs iteration space is split evenly over the workgroups; a tile cut by a range
-  // boundary gets partial sums (atomic add into a zero-filled output; the k-slab-0 owner adds the linear
-  // epilogue terms).  Only for linear epilogues (no activation, no pre-residual copy, no in-place residual).
-  int sk;
-  int split;  // operand precision (see gemm_kernel): 0 exact fp32 MFMA, 2 fp16x2, 3 bf16x3; chosen in pick_cfg
-  // fp16x2 operand maxima, as "amax slots": 64 sub-slots of (tag << 32 | float bits) written with atomicMax
-  // by the producer of the tensor (one sub-slot per producing workgroup); a reader takes the max over the
-  // sub-slots carrying the expected tag, so slots are reused without clearing.  Upper bounds are enough
-  // (a looser bound only lowers the scale).
-  const unsigned long long* a_amax;
-  const unsigned long long* w_amax;
-  unsigned a_tag, w_tag;
-  unsigned long long* y_amax;  // optional: max |Y| of this launch's outputs -> slot, tag y_tag
-  unsigned y_tag;
-};
-
-__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
-// d/dx of the erf GELU (torch GeluBackward, approximate='none')
-__device__ __forceinline__ float gelu_erf_grad(float x) {
-  const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
-  const float pdf = 0.39894228040143268f * expf(-0.5f * x * x);
-  return cdf + x * pdf;
-}
-enum DAct { DACT_NONE = 0, DACT_GELU = 1, DACT_RELU = 2, DACT_TANH_OUT = 3 };
-__device__ __forceinline__ float dact_grad(int dact, float pre) {
-  if (dact == DACT_GELU) return gelu_erf_grad(pre);
-  if (dact == DACT_RELU) return pre > 0.f ? 1.f : 0.f;
-  return 1.f - pre * pre;  // DACT_TANH_OUT: pre holds tanh(z)
-}
-
-// descriptor from a pointer that is wave-uniform by construction; readfirstlane makes that provable to
-// hipcc, which otherwise wraps every buffer op in a waterfall loop (cdna_hip_programming.md T20)
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p) {
-  const unsigned long long a = reinterpret_cast<unsigned long long>(p);
-  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a);
-  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
-  void* u = reinterpret_cast<void*>(((unsigned long long)hi << 32) | lo);
-  return __builtin_amdgcn_make_buffer_rsrc(u, (short)0, (int)OOB, RSRC_FLAGS);
-}
-
-// descriptor with an explicit extent (bytes): accesses at or past it are dropped / read 0
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_ext(const void* p, unsigned bytes) {
-  const unsigned long long a = reinterpret_cast<unsigned long long>(p);
-  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a);
-  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
-  void* u = reinterpret_cast<void*>(((unsigned long long)hi << 32) | lo);
-  return __builtin_amdgcn_make_buffer_rsrc(u, (short)0, (int)__builtin_amdgcn_readfirstlane(bytes), RSRC_FLAGS);
-}
-
-__device__ __forceinline__ float4 bload4(__amdgpu_buffer_rsrc_t r, unsigned off) {
-  const floatx4 v = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
-  return make_float4(v.x, v.y, v.z, v.w);
-}
-__device__ __forceinline__ float bload1(__amdgpu_buffer_rsrc_t r, unsigned off) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
-}
-__device__ __forceinline__ int bload1i(__amdgpu_buffer_rsrc_t r, unsigned off) {
-  return (int)__builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
-}
-__device__ __forceinline__ void bstore1(__amdgpu_buffer_rsrc_t r, unsigned off, float v) {
-  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, off, 0, 0);
-}
-
-using sfx::split3;   // fp32 -> three bf16 terms (common.h)
-using sfx::split2h;  // fp32 -> two fp16 terms of the scaled value (common.h)
 
 // Persistent tile loop: each workgroup walks output tiles blockIdx.x, +gridDim.x, ... and prefetches
 // the first K-slab of its NEXT tile while it computes the last slab and runs the epilogue of the
 // current one, so the global-load latency of a tile start and the epilogue stores overlap (short-K
 // GEMMs -- K = 64..256 on most PTv3 layers -- are otherwise latency-bound).
 // MODE: how the A rows of a tile are found (compile-time so the load path has no runtime branches)
-enum Mode { MODE_DENSE = 0, MODE_GATHER1 = 1, MODE_GATHERS = 2, MODE_PAIR = 3 };
 
 // SPLIT: the fp32 operands are split into three bf16 terms on the LDS store and every 32x32x16 block
 // product is formed from the six leading term products (t0t0, t0t1, t1t0, t0t2, t1t1, t2t0; the dropped
@@ -177,10 +53,15 @@ enum Mode { MODE_DENSE = 0, MODE_GATHER1 = 1, MODE_GATHERS = 2, MODE_PAIR = 3 };
 // 16-byte chunk c of row r sits at chunk c ^ ((r >> 2) & 3), which makes the fragment reads (16 rows x one
 // chunk per quarter-wave) and the staging writes (4 rows x 64 B per half-wave) bank-conflict free.
 //
-// SPL = 2 (the default for K >= 64): fp16x2 -- each operand is scaled by a power of two that puts its largest
-// magnitude in [2^14, 2^15) and split into two fp16 terms (split2h); a block is h*h + h*l + l*h on
-// v_mfma_f32_32x32x16_f16 (three products, two LDS term images) and the accumulators are unscaled once before
-// the epilogue.  Error: that of fp32 arithmetic (dropped l*l <= 2^-22 relative, products exact in fp32).
+// SPL = 2 (the default for K >= 64): fp16x2 -- every operand row is scaled by its own power of two and split
+// into two fp16 terms (split2h); a block is h*h + h*l + l*h on v_mfma_f32_32x32x16_f16 (three products, two
+// LDS term images).  W arrives pre-split (sfx_weight_split: per-row scale, 1/s per output column applied in the
+// epilogue).  A' rows are scaled online by the staging threads: a row's first non-zero slab puts its maximum in
+// [2^12, 2^13); a later slab that would leave the fp16 range (|x s| > 65504) lowers the row's scale, and the
+// staging waves post the factor (a power of two) with the slab (s_fac, any-change flag s_flag) so the compute
+// waves rescale that row's accumulators before adding it.  The epilogue unscales each row by its final 1/s.
+// Error: that of fp32 arithmetic (dropped l*l <= 2^-22 relative, products exact in fp32) for every row,
+// whatever the other rows' magnitudes.
 template <int BM, int BN, int WGM, int NW, bool VEC, int MODE, int SPL>
 __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs p, int tiles_n, int total_tiles) {
   constexpr bool SPLIT = SPL != 0;
@@ -198,7 +79,10 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs
   constexpr int W_ITERS = BN * BK / 4 / NT;
   constexpr int NBUF = SPLIT ? (NW == 8 ? SFX_NBUF8 : 1) : 2;
   // fp32: double-buffered [row][k] images (row stride 36); SPLIT: NBUF x 3 swizzled bf16 term images
-  constexpr int A_FLOATS = SPLIT ? NBUF * NTERM * BM * BK / 2 : 2 * BM * LDS_STRIDE;
+  // (SPL == 2 appends the per-row scale state: [NBUF][BM] factors, [BM] 1/s, [NBUF] flags -- in the same LDS
+  // object: a further __shared__ object can make hipcc wait vmcnt(0) before ds_reads)
+  constexpr int AUX_FLOATS = SPL == 2 ? NBUF * BM + BM + 4 : 0;
+  constexpr int A_FLOATS = (SPLIT ? NBUF * NTERM * BM * BK / 2 : 2 * BM * LDS_STRIDE) + AUX_FLOATS;
   constexpr int W_FLOATS = SPLIT ? NBUF * NTERM * BN * BK / 2 : 2 * BN * LDS_STRIDE;
   __shared__ __attribute__((aligned(16))) float sAraw[A_FLOATS];
   __shared__ __attribute__((aligned(16))) float sWraw[W_FLOATS];
@@ -208,6 +92,9 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs
   char* sWs = reinterpret_cast<char*>(sWraw);  // [NBUF][NTERM][BN][64 B]
   // byte offset of the 4-element group at k = c4 * 4 (c4 = 0..7) of row r in a swizzled term image
   auto swz = [](int r, int c4) -> int { return r * 64 + ((((c4 >> 1) ^ (r >> 2)) & 3) << 4) + ((c4 & 1) << 3); };
+  float* s_fac = sAraw + (A_FLOATS - AUX_FLOATS);   // [NBUF][BM]
+  float* s_inv = s_fac + NBUF * BM;                  // [BM]
+  int* s_flag = reinterpret_cast<int*>(s_inv + BM);  // [NBUF]
 
   const int g = blockIdx.z;
   const float* A = p.A + g * p.gA;
@@ -223,24 +110,11 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs
   const int h = lane >> 5, l32 = lane & 31;
   const int K = p.K;
   const int nk = (K + BK - 1) / BK;
-  // fp16x2 operand scales (powers of two) and their inverses, from the tagged maxima
-  float scA = 1.f, scW = 1.f, invA = 1.f, invW = 1.f;
   if constexpr (SPL == 2) {
-    auto scale_of = [](float m, float& s, float& inv) {
-      int e = 0;
-      if (m > 0.f && m <= 3.4028235e38f) {  // finite, non-zero (inf / NaN: unscaled; the result is inf / NaN)
-        (void)frexpf(m, &e);
-        e = 15 - e;
-        e = e > 126 ? 126 : (e < -126 ? -126 : e);
-      }
-      s = ldexpf(1.f, e);
-      inv = ldexpf(1.f, -e);
-    };
-    scale_of(sfx::read_amax(p.a_amax, p.a_tag), scA, invA);
-    scale_of(sfx::read_amax(p.w_amax, p.w_tag), scW, invW);
+    if (tid < NBUF) s_flag[tid] = 0;  // (published by the first barrier)
   }
   // byte offsets fit 31 bits (host checks every operand against the 2 GiB buffer range)
-  const unsigned lda32 = (unsigned)p.lda, ldw32 = (unsigned)p.ldw, ldy32 = (unsigned)p.ldy;
+  const unsigned lda32 = (unsigned)p.lda, ldw32 = (unsigned)p.ldw, ldy32 = (unsigned)p.ldy, ldws32 = (unsigned)p.ldws;
   const unsigned ldr32 = (unsigned)p.ldr, ldp32 = (unsigned)p.ldypre;
   const int lrow = tid >> 3, lcol = (tid & 7) * 4;  // staging coordinates: rows lrow + RPP i, cols lcol..+3
 
@@ -250,7 +124,8 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs
     const int* gidx;
     int gstride;
     const int* out_rows;
-    const float* W;
+    const float* W;       // W, or its pre-split image (SPL == 2)
+    const float* winv;    // 1/s per W row (SPL == 2)
   };
   auto tile_info = [&](int t) -> Tile {
     Tile ti;
@@ -261,7 +136,8 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs
     ti.gidx = MODE == MODE_DENSE ? nullptr : p.gidx;
     ti.gstride = p.gstride;
     ti.out_rows = p.out_rows;
-    ti.W = p.W + g * p.gW;
+    ti.W = (SPL == 2 ? p.Wsp : p.W) + g * p.gW;
+    ti.winv = p.winv ? p.winv + g * p.gWinv : nullptr;
     if constexpr (MODE == MODE_PAIR) {
       int sl = 0;
       for (int q = 1; q < p.num_slices; ++q)
@@ -272,7 +148,8 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs
       ti.gidx = p.pair_in + base;
       ti.gstride = 1;
       ti.out_rows = p.pair_out + base;
-      ti.W = p.W + sl * p.slice_w_stride;
+      ti.W = (SPL == 2 ? p.Wsp : p.W) + sl * p.slice_w_stride;
+      if (p.winv) ti.winv = p.winv + sl * p.slice_winv_stride;
     }
     return ti;
   };
@@ -330,7 +207,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs
 #pragma unroll
     for (int i = 0; i < W_ITERS; ++i) {
       const int n = ti.n0 + lrow + RPP * i;
-      const unsigned off = (n < p.N && kin) ? ((unsigned)n * ldw32 + (unsigned)k) * 4u : OOB;
+      const unsigned off = (n < p.N && kin) ? ((unsigned)n * (SPL == 2 ? ldws32 : ldw32) + (unsigned)k) * 4u : OOB;
       if (VEC) {
         rw[i] = bload4(rW, off);
       } else {
@@ -343,13 +220,86 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs
       }
     }
   };
-  auto store_tiles = [&](int buf) {
+  // SPL == 2 per-row scale state of the staged rows lrow + RPP i (exponent, scale, overflow threshold) and the
+  // stamp of the last stored slab (the flag that asks the compute waves to rescale carries it)
+  int erow[A_ITERS];
+  float srow[A_ITERS], thr[A_ITERS];
+#pragma unroll
+  for (int i = 0; i < A_ITERS; ++i) { erow[i] = INT_MIN; srow[i] = 1.f; thr[i] = 0.f; }
+  int sq = 0, cq = 0;
+  auto store_tiles = [&](int buf, bool first) {
     if constexpr (SPLIT) {
       const int b = NBUF == 2 ? buf : 0;
+      if constexpr (SPL == 2) {
+        ++sq;
+        float m[A_ITERS];
+        bool over = false;
+#pragma unroll
+        for (int i = 0; i < A_ITERS; ++i) {
+          m[i] = fmaxf(fmaxf(fabsf(ra[i].x), fabsf(ra[i].y)), fmaxf(fabsf(ra[i].z), fabsf(ra[i].w)));
+          over |= m[i] > thr[i];
+        }
+        bool dec = false;
+        if (first || __builtin_amdgcn_ballot_w64(over) != 0) {
+          // slow path (a segment's first slab, a row's first non-zero slab, or a slab that would overflow fp16):
+          // row maxima over the row's 8 staging lanes, new exponents, rescale factors and 1/s
+#pragma unroll
+          for (int i = 0; i < A_ITERS; ++i) {
+            float mr = m[i];
+            mr = fmaxf(mr, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(mr), 0xB1, 0xF, 0xF, false)));
+            mr = fmaxf(mr, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(mr), 0x4E, 0xF, 0xF, false)));
+            mr = fmaxf(mr, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(mr), 0x141, 0xF, 0xF, false)));
+            int e = first ? INT_MIN : erow[i];
+            float fac = 1.f;
+            bool chg = first;
+            if (mr > 0.f && mr <= 3.4028235e38f) {
+              int e2 = 13 - __builtin_amdgcn_frexp_expf(mr);  // row max in [2^12, 2^13)
+              e2 = e2 > 126 ? 126 : (e2 < -126 ? -126 : e2);
+              if (e == INT_MIN) {  // the row's accumulators are still zero: no rescale
+                e = e2;
+                chg = true;
+              } else if (mr * srow[i] > 65504.f) {
+                fac = ldexpf(1.f, e2 - e);
+                e = e2;
+                chg = true;
+                dec = true;
+              }
+            }
+            erow[i] = e;
+            const bool set = e != INT_MIN;
+            srow[i] = set ? ldexpf(1.f, e) : 1.f;
+            thr[i] = set ? ldexpf(65504.f, -e) : 0.f;
+            if ((tid & 7) == 0) {
+              s_fac[b * BM + lrow + RPP * i] = fac;
+              if (chg) s_inv[lrow + RPP * i] = set ? ldexpf(1.f, -e) : 1.f;
+            }
+          }
+        } else if ((tid & 7) == 0) {
+#pragma unroll
+          for (int i = 0; i < A_ITERS; ++i) s_fac[b * BM + lrow + RPP * i] = 1.f;
+        }
+        if (__builtin_amdgcn_ballot_w64(dec) != 0 && lane == 0) s_flag[b] = sq;
+#pragma unroll
+        for (int i = 0; i < A_ITERS; ++i) {
+          uint2 t[2];
+          split2h(ra[i], srow[i], t);
+          const int o = swz(lrow + RPP * i, lcol >> 2);
+          *reinterpret_cast<uint2*>(sAs + ((b * 2 + 0) * BM) * 64 + o) = t[0];
+          *reinterpret_cast<uint2*>(sAs + ((b * 2 + 1) * BM) * 64 + o) = t[1];
+        }
+#pragma unroll
+        for (int i = 0; i < W_ITERS; ++i) {  // pre-split: h terms in .x/.y, l terms in .z/.w
+          const uint4 w = __builtin_bit_cast(uint4, rw[i]);
+          const int o = swz(lrow + RPP * i, lcol >> 2);
+          *reinterpret_cast<uint2*>(sWs + ((b * 2 + 0) * BN) * 64 + o) = make_uint2(w.x, w.y);
+          *reinterpret_cast<uint2*>(sWs + ((b * 2 + 1) * BN) * 64 + o) = make_uint2(w.z, w.w);
+        }
+        return;
+      } else {
 #pragma unroll
       for (int i = 0; i < A_ITERS; ++i) {
         uint2 t[NTERM];
-        if constexpr (SPL == 2) split2h(ra[i], scA, t); else split3(ra[i], t);
+        split3(ra[i], t);
         const int o = swz(lrow + RPP * i, lcol >> 2);
 #pragma unroll
         for (int q = 0; q < NTERM; ++q) *reinterpret_cast<uint2*>(sAs + ((b * NTERM + q) * BM) * 64 + o) = t[q];
@@ -357,12 +307,13 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs
 #pragma unroll
       for (int i = 0; i < W_ITERS; ++i) {
         uint2 t[NTERM];
-        if constexpr (SPL == 2) split2h(rw[i], scW, t); else split3(rw[i], t);
+        split3(rw[i], t);
         const int o = swz(lrow + RPP * i, lcol >> 2);
 #pragma unroll
         for (int q = 0; q < NTERM; ++q) *reinterpret_cast<uint2*>(sWs + ((b * NTERM + q) * BN) * 64 + o) = t[q];
       }
       return;
+      }
     }
 #pragma unroll
     for (int i = 0; i < A_ITERS; ++i)
@@ -384,7 +335,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs
 
   // Epilogue operands of the current tile (bias/scale/shift per column, output row per accumulator row)
   // are fetched BEFORE the next tile's prefetch is issued, so the epilogue never waits on the prefetch.
-  float ebias[NB], escale[NB], eshift[NB];
+  float ebias[NB], escale[NB], eshift[NB], ewinv[NB];
   int mrow[MB][16];
   float ymax = 0.f;  // running max |Y| of this workgroup's outputs (p.y_amax)
   auto load_mrow = [&](const Tile& ti, __amdgpu_buffer_rsrc_t rO) {
@@ -412,6 +363,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs
       ebias[b] = bv;
       escale[b] = sv;  // raw loads; the defaults for absent operands are selected in the epilogue, so
       eshift[b] = hv;  // nothing here waits on them
+      if constexpr (SPL == 2) ewinv[b] = bload1(rsrc(ti.winv), off);
     }
     // output-row remaps (pair mode's pair_out; an out_rows argument of the other modes) are loaded in the
     // epilogue, keeping 16 * MB registers free across the MFMAs
@@ -532,13 +484,20 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs
   };
 
   auto epilogue = [&](const Tile& ti, bool partial, bool owner0) {
-    if constexpr (SPL == 2) {  // undo the operand scales (powers of two: exact)
+    if constexpr (SPL == 2) {  // undo the row scales of A' and W (powers of two: exact)
 #pragma unroll
       for (int a = 0; a < MB; ++a)
 #pragma unroll
-        for (int b = 0; b < NB; ++b)
+        for (int gq = 0; gq < 4; ++gq) {
+          const float4 f = *reinterpret_cast<const float4*>(s_inv + wm * WM + a * 32 + 8 * gq + 4 * h);
 #pragma unroll
-          for (int r = 0; r < 16; ++r) acc[a][b][r] = acc[a][b][r] * invA * invW;
+          for (int b = 0; b < NB; ++b) {
+            acc[a][b][4 * gq + 0] *= f.x * ewinv[b];
+            acc[a][b][4 * gq + 1] *= f.y * ewinv[b];
+            acc[a][b][4 * gq + 2] *= f.z * ewinv[b];
+            acc[a][b][4 * gq + 3] *= f.w * ewinv[b];
+          }
+        }
     }
     if constexpr (MODE != MODE_PAIR) {
       if (!ti.out_rows) {
@@ -717,6 +676,25 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs
     }
   };
   auto compute = [&](int buf) {
+    if constexpr (SPL == 2) {  // a later slab lowered some rows' scales: rescale their accumulators first
+      ++cq;
+      const int b = NBUF == 2 ? buf : 0;
+      if (__builtin_amdgcn_readfirstlane(s_flag[b]) == cq) {
+#pragma unroll
+        for (int a = 0; a < MB; ++a)
+#pragma unroll
+          for (int gq = 0; gq < 4; ++gq) {
+            const float4 f = *reinterpret_cast<const float4*>(s_fac + b * BM + wm * WM + a * 32 + 8 * gq + 4 * h);
+#pragma unroll
+            for (int bb = 0; bb < NB; ++bb) {
+              acc[a][bb][4 * gq + 0] *= f.x;
+              acc[a][bb][4 * gq + 1] *= f.y;
+              acc[a][bb][4 * gq + 2] *= f.z;
+              acc[a][bb][4 * gq + 3] *= f.w;
+            }
+          }
+      }
+    }
     if constexpr (SPLIT) {
       compute_split(buf, 0, BK / 16);
       return;
@@ -767,7 +745,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs
   Tile ti = tile_info(t);
   load_rows(ti, kb, grow);
   load_tiles(ti, kb);
-  store_tiles(0);
+  store_tiles(0, true);
   __syncthreads();
   int buf = 0;
   while (true) {
@@ -791,7 +769,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs
       __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of the MFMAs it overlaps
       compute(buf);
       if constexpr (NBUF == 1) __syncthreads();  // single LDS buffer: every wave is done reading it
-      store_tiles(buf ^ 1);
+      store_tiles(buf ^ 1, false);
       __syncthreads();
       if constexpr (NBUF == 2) buf ^= 1;
     }
@@ -812,7 +790,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs
     epilogue(ti, kb != 0 || ke != nk, kb == 0);
     if (!has_next) break;
     if constexpr (NBUF == 1) __syncthreads();
-    store_tiles(buf ^ 1);
+    store_tiles(buf ^ 1, true);
     __syncthreads();
     if constexpr (NBUF == 2) buf ^= 1;
     t = nt;
@@ -1144,15 +1122,10 @@ void dispatch_mode(GemmArgs a, int groups, bool vec, hipStream_t st) {
 void dispatch(const GemmArgs& a0, int groups, bool vec, hipStream_t st) {
   GemmArgs a = a0;
   a.split = vec ? split_mode(a.K) : 0;
-  if (a.split == 2 && (!a.a_amax || !a.w_amax)) {
-    if (a.pair_mode) {
-      a.split = 3;  // (callers of pair launches pass the maxima; bf16x3 needs none)
-    } else {
-      AmaxJob ja, jw;
-      gemm_amax_jobs(a, groups, ja, jw);
-      if (!prepare_amax(a, ja, jw, st)) a.split = 3;
-    }
-  }
+  // fp16x2 needs the pre-split W (per-row scales of A' are chosen in the kernel); without one the launch runs the
+  // range-safe bf16x3 form.  SFX_GEMM_WS=1 routes fp16x2 launches to the warp-specialised kernel (gemm_ws.hip).
+  if (a.split == 2 && !a.Wsp) a.split = 3;
+  if (a.split == 2 && launch_ws(a, groups, st)) return;
   if (a.pair_mode)
     dispatch_mode<MODE_PAIR>(a, groups, vec, st);
   else if (!a.gidx)
@@ -1305,7 +1278,7 @@ int sfx_linear(int M, int N, int K, const float* A, long long lda, const int* ga
                long long group_stride_bias, long long group_stride_Y, const int* out_row_idx, const float* rowscale,
                int pre_before_act, const unsigned long long* a_amax, unsigned a_tag,
                const unsigned long long* w_amax, unsigned w_tag, unsigned long long* y_amax, unsigned y_tag,
-               void* stream) {
+               const float* w_split, const float* w_inv, void* stream) {
   SFX_REQUIRE(M >= 0 && N > 0 && K > 0, "sfx_linear: bad sizes M=%d N=%d K=%d", M, N, K);
   SFX_REQUIRE(act >= 0 && act <= 3, "sfx_linear: bad activation %d", act);
   SFX_REQUIRE(groups >= 1, "sfx_linear: groups < 1");
@@ -1329,6 +1302,11 @@ int sfx_linear(int M, int N, int K, const float* A, long long lda, const int* ga
   a.a_amax = a_amax; a.a_tag = a_tag; a.w_amax = w_amax; a.w_tag = w_tag; a.y_amax = y_amax; a.y_tag = y_tag;
   const bool vec = (K % 4 == 0) && (lda % 4 == 0) && (ldw % 4 == 0) && aligned16(A) && aligned16(W) &&
                    (group_stride_A % 4 == 0) && (group_stride_W % 4 == 0);
+  SFX_REQUIRE(!w_split == !w_inv, "sfx_linear: w_split and w_inv go together");
+  if (w_split && vec && aligned16(w_split)) {  // split layout: contiguous [groups * N][K], group stride N * K
+    SFX_REQUIRE(groups == 1 || group_stride_W == (long long)N * K, "sfx_linear: w_split needs contiguous groups");
+    a.Wsp = w_split; a.ldws = K; a.winv = w_inv; a.gWinv = N;
+  }
   dispatch(a, groups, vec, sfx::as_stream(stream));
   return sfx::check_launch("sfx_linear");
 }
@@ -1340,7 +1318,8 @@ int sfx_linear(int M, int N, int K, const float* A, long long lda, const int* ga
 int sfx_subm_conv(int n, int cin, int cout, const float* x, long long ldx, const int* nbr, const float* weight,
                   const float* bias, const int* pair_in, const int* pair_out, const int* pair_off_host, float* out,
                   long long ldo, const unsigned long long* x_amax, unsigned x_tag,
-                  const unsigned long long* w_amax, unsigned w_tag, void* stream) {
+                  const unsigned long long* w_amax, unsigned w_tag, const float* w_split, const float* w_inv,
+                  void* stream) {
   SFX_REQUIRE(n >= 0 && cin > 0 && cout > 0, "sfx_subm_conv: bad sizes");
   if (n == 0) return SFX_OK;
   SFX_REQUIRE(x && nbr && weight && out && pair_off_host, "sfx_subm_conv: null buffer");
@@ -1353,9 +1332,13 @@ int sfx_subm_conv(int n, int cin, int cout, const float* x, long long ldx, const
   GemmArgs a{};
   a.M = n; a.N = cout; a.K = cin; a.A = x; a.lda = ldx; a.gidx = nbr + 13; a.S = 1; a.Kseg = cin; a.gstride = 27;
   a.W = weight + 13ll * cin; a.ldw = 27ll * cin; a.bias = bias; a.act = 0; a.act_ncols = cout; a.Y = out; a.ldy = ldo;
-  // fp16x2: one pair of maxima (all of x, all 27 weight slices) for both launches
+  // fp16x2: one pair of maxima (all of x, all 27 weight slices) for both launches, or the pre-split weight
   a.a_amax = x_amax; a.a_tag = x_tag; a.w_amax = w_amax; a.w_tag = w_tag;
-  if (vec && split_mode(cin) == 2 &&
+  SFX_REQUIRE(!w_split == !w_inv, "sfx_subm_conv: w_split and w_inv go together");
+  if (w_split && vec && aligned16(w_split)) {  // split of the [Cout, 27 * Cin] weight
+    a.Wsp = w_split + 13ll * cin; a.ldws = 27ll * cin; a.winv = w_inv;
+  }
+  if (!a.Wsp && vec && split_mode(cin) == 2 &&
       !prepare_amax(a, AmaxJob{x, ldx, 0, n, cin, 1, nullptr, 0, 1},
                     AmaxJob{weight, 27ll * cin, 0, cout, 27 * cin, 1, nullptr, 0, 1}, st)) {
     a.a_amax = a.w_amax = nullptr;  // (dispatch falls back to bf16x3 for the pair launch)
@@ -1368,6 +1351,7 @@ int sfx_subm_conv(int n, int cin, int cout, const float* x, long long ldx, const
   GemmArgs b = a;
   b.gidx = nullptr; b.bias = nullptr; b.gstride = 1; b.pair_mode = 1; b.pair_in = pair_in; b.pair_out = pair_out;
   b.W = weight; b.slice_w_stride = cin; b.num_slices = 27;
+  if (a.Wsp) b.Wsp = w_split;
   for (int k = 0; k <= 27; ++k) b.slice_pair_off[k] = pair_off_host[k];
   b.M = pair_off_host[27];
   dispatch(b, 1, vec, st);
@@ -1380,7 +1364,8 @@ int sfx_subm_conv(int n, int cin, int cout, const float* x, long long ldx, const
 // gradient it should be added to.
 int sfx_subm_conv_bwd_data(int n, int cin, int cout, const float* dy, long long ldy, const int* nbr,
                            const float* weight_t, const int* pair_in, const int* pair_out, const int* pair_off_host,
-                           int* centre_ws, float* dx, long long lddx, void* stream) {
+                           int* centre_ws, float* dx, long long lddx, const float* wt_split, const float* wt_inv,
+                           void* stream) {
   SFX_REQUIRE(n >= 0 && cin > 0 && cout > 0, "sfx_subm_conv_bwd_data: bad sizes");
   if (n == 0) return SFX_OK;
   SFX_REQUIRE(dy && nbr && weight_t && dx && pair_off_host && centre_ws, "sfx_subm_conv_bwd_data: null buffer");
@@ -1389,8 +1374,10 @@ int sfx_subm_conv_bwd_data(int n, int cin, int cout, const float* dy, long long 
               "sfx_subm_conv_bwd_data: operand exceeds the 2 GiB buffer-descriptor range");
   hipStream_t st = sfx::as_stream(stream);
   const bool vec = (cout % 4 == 0) && (ldy % 4 == 0) && aligned16(dy) && aligned16(weight_t);
+  SFX_REQUIRE(!wt_split == !wt_inv, "sfx_subm_conv_bwd_data: wt_split and wt_inv go together");
+  const bool presplit = wt_split && vec && aligned16(wt_split);
   GemmArgs am{};
-  if (vec && split_mode(cout) == 2)
+  if (!presplit && vec && split_mode(cout) == 2)
     (void)prepare_amax(am, AmaxJob{dy, ldy, 0, n, cout, 1, nullptr, 0, 1},
                        AmaxJob{weight_t, (long long)cout, 0, 27 * cin, cout, 1, nullptr, 0, 1}, st);
   int* cg = centre_ws;
@@ -1401,9 +1388,11 @@ int sfx_subm_conv_bwd_data(int n, int cin, int cout, const float* dy, long long 
   a.ldw = cout; a.act = 0; a.act_ncols = cin; a.Y = dx; a.ldy = lddx;
   a.pair_mode = 1; a.slice_w_stride = (long long)cin * cout;
   a.a_amax = am.a_amax; a.a_tag = am.a_tag; a.w_amax = am.w_amax; a.w_tag = am.w_tag;
+  if (presplit) { a.ldws = cout; a.winv = wt_inv; a.slice_winv_stride = cin; }
   // centre offset (k = 13) as a one-slice pair launch
   GemmArgs c = a;
   c.pair_in = cg; c.pair_out = cs; c.W = weight_t + 13ll * cin * cout; c.num_slices = 1;
+  if (presplit) { c.Wsp = wt_split + 13ll * cin * cout; c.winv = wt_inv + 13ll * cin; }
   c.slice_pair_off[0] = 0; c.slice_pair_off[1] = n; c.M = n;
   dispatch(c, 1, vec, st);
   int rc = sfx::check_launch("sfx_subm_conv_bwd_data(centre)");
@@ -1411,6 +1400,7 @@ int sfx_subm_conv_bwd_data(int n, int cin, int cout, const float* dy, long long 
   // the 26 other offsets: roles of the forward pair lists swapped
   GemmArgs b = a;
   b.pair_in = pair_out; b.pair_out = pair_in; b.W = weight_t; b.num_slices = 27;
+  if (presplit) b.Wsp = wt_split;
   for (int k = 0; k <= 27; ++k) b.slice_pair_off[k] = pair_off_host[k];
   b.M = pair_off_host[27];
   dispatch(b, 1, vec, st);
@@ -1419,7 +1409,8 @@ int sfx_subm_conv_bwd_data(int n, int cin, int cout, const float* dy, long long 
 
 int sfx_linear_bwd_data(int M, int N, int K, const float* dY, long long ldy, const float* Wt, long long ldwt,
                         const float* rowscale, int dact, int dact_ncols, const float* dact_pre, long long ld_pre,
-                        float* dX, long long lddx, int accumulate, void* stream) {
+                        float* dX, long long lddx, int accumulate, const float* wt_split, const float* wt_inv,
+                        void* stream) {
   SFX_REQUIRE(M >= 0 && N > 0 && K > 0, "sfx_linear_bwd_data: bad sizes M=%d N=%d K=%d", M, N, K);
   SFX_REQUIRE(dact >= 0 && dact <= 3, "sfx_linear_bwd_data: bad dact %d", dact);
   if (M == 0) return SFX_OK;
@@ -1434,6 +1425,10 @@ int sfx_linear_bwd_data(int M, int N, int K, const float* dY, long long ldy, con
   if (accumulate) { a.R = dX; a.ldr = lddx; }
   a.rowscale = rowscale; a.dact = dact; a.dact_pre = dact_pre; a.ld_dact = ld_pre;
   const bool vec = (N % 4 == 0) && (ldy % 4 == 0) && (ldwt % 4 == 0) && aligned16(dY) && aligned16(Wt);
+  SFX_REQUIRE(!wt_split == !wt_inv, "sfx_linear_bwd_data: wt_split and wt_inv go together");
+  if (wt_split && vec && aligned16(wt_split)) {  // split of Wt [K, N]
+    a.Wsp = wt_split; a.ldws = N; a.winv = wt_inv;
+  }
   dispatch(a, 1, vec, sfx::as_stream(stream));
   return sfx::check_launch("sfx_linear_bwd_data");
 }

@@ -1,0 +1,154 @@
+// Shared declarations of the fp32-accurate GEMM kernels (gemm.hip: the general tile kernel; gemm_ws.hip: the
+// warp-specialised fp16x2 kernel): launch arguments, epilogue helpers and raw-buffer access.
+#pragma once
+
+#include <type_traits>
+
+#include "common.h"
+
+namespace sfxg {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+constexpr int BK = 32;
+// residency: persistent workgroups per CU for the four- and eight-wave tiles, LDS buffers of the eight-wave ones
+#ifndef SFX_PERCU4
+#define SFX_PERCU4 2
+#endif
+#ifndef SFX_PERCU8
+#define SFX_PERCU8 1
+#endif
+#ifndef SFX_NBUF8
+#define SFX_NBUF8 2
+#endif
+constexpr int kPerCu4 = SFX_PERCU4, kPerCu8 = SFX_PERCU8;
+constexpr int LDS_STRIDE = BK + 4;
+constexpr int THREADS = 256;
+constexpr unsigned OOB = 0x7ffffff0u;        // byte offset past every descriptor extent
+constexpr int RSRC_FLAGS = 0x00020000;       // gfx950 raw buffer, 32-bit data
+
+enum Act { ACT_NONE = 0, ACT_GELU = 1, ACT_RELU = 2, ACT_TANH = 3 };
+
+struct GemmArgs {
+  int M, N, K;         // K = S * Kseg when gathering
+  const float* A;
+  long long lda;
+  const int* gidx;     // gather index, row stride gstride, or null
+  int S, Kseg, gstride;
+  const float* W;      // [N, K] (row stride ldw)
+  long long ldw;
+  const float* bias;   // [N] or null
+  const float* scale;  // [N] or null  (folded BatchNorm)
+  const float* shift;  // [N] or null
+  int act, act_ncols;  // act applies to columns < act_ncols
+  const float* R;      // residual [*, ldr] or null
+  long long ldr;
+  const int* ridx;     // residual row index (by output row) or null
+  float* Y;
+  long long ldy;
+  float* Ypre;         // optional copy of the pre-residual value
+  long long ldypre;
+  long long gA, gW, gB, gY;  // grouped GEMM (blockIdx.z): per-group element strides
+  const int* out_rows;       // tile row -> output row (or null)
+  // offset-major sparse conv ("pair mode"): blockIdx.x walks a flat tile list over up to 27 slices;
+  // slice k gathers A rows pair_in[pair_off[k] ..] and atomically adds into rows pair_out[...] with the
+  // weight slice W + k * slice_w_stride.
+  int pair_mode;
+  const int* pair_in;
+  const int* pair_out;
+  int slice_tile_off[28];
+  int slice_pair_off[28];
+  int num_slices;
+  long long slice_w_stride;
+  // backward-pass epilogue terms (applied after the activation): v *= rowscale[row] (drop-path masks),
+  // v *= act'(dact_pre[row, col]) for cols < act_ncols (GELU / ReLU on the pre-activation, tanh on its output)
+  const float* rowscale;
+  int pre_before_act;  // Ypre receives the pre-activation value (training forward saves it for act')
+  const float* dact_pre;
+  long long ld_dact;
+  int dact;
+  // Stream-K: the tiles x K-slabs iteration space is split evenly over the workgroups; a tile cut by a range
+  // boundary gets partial sums (atomic add into a zero-filled output; the k-slab-0 owner adds the linear
+  // epilogue terms).  Only for linear epilogues (no activation, no pre-residual copy, no in-place residual).
+  int sk;
+  int split;  // operand precision (see gemm_kernel): 0 exact fp32 MFMA, 2 fp16x2, 3 bf16x3; chosen in pick_cfg
+  // fp16x2 operand maxima, as "amax slots": 64 sub-slots of (tag << 32 | float bits) written with atomicMax
+  // by the producer of the tensor (one sub-slot per producing workgroup); a reader takes the max over the
+  // sub-slots carrying the expected tag, so slots are reused without clearing.  Upper bounds are enough
+  // (a looser bound only lowers the scale).
+  const unsigned long long* a_amax;
+  const unsigned long long* w_amax;
+  unsigned a_tag, w_tag;
+  unsigned long long* y_amax;  // optional: max |Y| of this launch's outputs -> slot, tag y_tag
+  unsigned y_tag;
+  // pre-split W (sfx_weight_split; the warp-specialised kernel): W's element layout in 4-byte units, every group
+  // of 4 consecutive elements held as 4 fp16 h terms then 4 fp16 l terms of W[n, k] * 2^e_n; winv[n] = 2^-e_n.
+  // Slices / groups use the same element offsets as W (slice_w_stride, gW); winv is grouped by gWinv.
+  const float* Wsp;
+  long long ldws;
+  const float* winv;
+  long long gWinv;
+  long long slice_winv_stride;  // pair mode: winv offset per slice (row-sliced weights, e.g. the conv backward)
+  int epi_vec;  // epilogue operands allow 16-byte accesses (set by launch_ws)
+};
+
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+// d/dx of the erf GELU (torch GeluBackward, approximate='none')
+__device__ __forceinline__ float gelu_erf_grad(float x) {
+  const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
+  const float pdf = 0.39894228040143268f * expf(-0.5f * x * x);
+  return cdf + x * pdf;
+}
+enum DAct { DACT_NONE = 0, DACT_GELU = 1, DACT_RELU = 2, DACT_TANH_OUT = 3 };
+__device__ __forceinline__ float dact_grad(int dact, float pre) {
+  if (dact == DACT_GELU) return gelu_erf_grad(pre);
+  if (dact == DACT_RELU) return pre > 0.f ? 1.f : 0.f;
+  return 1.f - pre * pre;  // DACT_TANH_OUT: pre holds tanh(z)
+}
+
+// descriptor from a pointer that is wave-uniform by construction; readfirstlane makes that provable to
+// hipcc, which otherwise wraps every buffer op in a waterfall loop (cdna_hip_programming.md T20)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p) {
+  const unsigned long long a = reinterpret_cast<unsigned long long>(p);
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+  void* u = reinterpret_cast<void*>(((unsigned long long)hi << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(u, (short)0, (int)OOB, RSRC_FLAGS);
+}
+
+// descriptor with an explicit extent (bytes): accesses at or past it are dropped / read 0
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_ext(const void* p, unsigned bytes) {
+  const unsigned long long a = reinterpret_cast<unsigned long long>(p);
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+  void* u = reinterpret_cast<void*>(((unsigned long long)hi << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(u, (short)0, (int)__builtin_amdgcn_readfirstlane(bytes), RSRC_FLAGS);
+}
+
+__device__ __forceinline__ float4 bload4(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  const floatx4 v = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ float bload1(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+}
+__device__ __forceinline__ int bload1i(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return (int)__builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
+}
+__device__ __forceinline__ void bstore1(__amdgpu_buffer_rsrc_t r, unsigned off, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, off, 0, 0);
+}
+
+using sfx::split3;   // fp32 -> three bf16 terms (common.h)
+using sfx::split2h;  // fp32 -> two fp16 terms of the scaled value (common.h)
+
+enum Mode { MODE_DENSE = 0, MODE_GATHER1 = 1, MODE_GATHERS = 2, MODE_PAIR = 3 };
+
+// Warp-specialised fp16x2 launcher (gemm_ws.hip): false when the launch is not eligible (the caller then runs
+// the general kernel).  Needs vec operands, split == 2, a pre-split W (Wsp / winv) and no Stream-K.
+bool launch_ws(const GemmArgs& a, int groups, hipStream_t st);
+bool ws_enabled();
+
+}  // namespace sfxg

@@ -10,11 +10,12 @@ submodule names and therefore the same state-dict keys
 feature the FeaturePredictor reads (feature_predictor.py:184-188).
 
 The nn modules only hold parameters; forward runs entirely on libsfx HIP
-kernels (serialization radix sort, 27-neighbour hash map, fp32 MFMA GEMMs
-with fused gather/BN/GELU/residual, windowed attention, pooling runs).
-Eval/inference only in this build (the reference's eval path runs under
-torch.no_grad(), train.py:81); the training backward of the refiner is not
-implemented yet and calling forward with autograd-tracked parameters raises.
+kernels (serialization radix sort, 27-neighbour hash map, fp32-accurate MFMA
+GEMMs with fused gather/BN/GELU/residual, windowed attention, pooling runs).
+This module is the eval forward (the reference's eval path runs under
+torch.no_grad(), train.py:81); the training forward/backward of the same
+module tree (train-mode BN, DropPath, hand-written tape backward to the qkv
+parameters) is `ptv3_train.py`, driven by `train.Trainer`.
 """
 from __future__ import annotations
 

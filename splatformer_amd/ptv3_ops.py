@@ -16,7 +16,8 @@ from . import _lib
 from ._lib import I, L, P, F, Z, call, ptr, stream
 
 _lib.register("sfx_linear", [I, I, I, P, L, P, I, P, L, P, P, P, I, I, P, L, P, P, L, P, L, I, L, L, L, L, P, P, I,
-                              P, I, P, I, P, I, P])
+                              P, I, P, I, P, I, P, P, P])
+_lib.register("sfx_weight_split", [I, I, P, L, P, P, P])
 _lib.register("sfx_amax_f32", [I, I, P, L, P, I, P])
 _lib.register("sfx_ln_amax_bound", [I, P, P, P, I, P])
 _lib.register("sfx_layernorm", [I, I, P, L, P, P, F, P, L, P])
@@ -35,7 +36,7 @@ _lib.register("sfx_subm_neighbors", [I, P, P, I, P, P, P, P, P, P])
 _lib.register("sfx_subm_permute", [I, P, P, P, P, P, P])
 _lib.register("sfx_subm_pairs_workspace_bytes", [I], Z)
 _lib.register("sfx_subm_pairs", [I, P, P, Z, P, P, P, P])
-_lib.register("sfx_subm_conv", [I, I, I, P, L, P, P, P, P, P, P, P, L, P, I, P, I, P])
+_lib.register("sfx_subm_conv", [I, I, I, P, L, P, P, P, P, P, P, P, L, P, I, P, I, P, P, P])
 _lib.register("sfx_gs_pack", [I, P, L, P, L, P, L, P, L, P, L, P, L, I, F, P, L, P, P, P])
 _lib.register("sfx_offsets_to_batch", [I, I, P, P, P])
 _lib.register("sfx_gemm_force_config", [I, I])
@@ -105,6 +106,31 @@ def ln_amax(gamma: Tensor, beta: Tensor) -> Tuple[int, int]:
     return slot
 
 
+SPLIT_MIN_K = 64  # K below which the GEMM runs exact fp32 MFMA (gemm.hip split_mode)
+
+
+def weight_split(w: Tensor, rows: Optional[int] = None) -> Tuple[Optional[int], Optional[int]]:
+    """(split, 1/scale) device pointers of the fp16x2 pre-split of a weight viewed as [rows, cols] (default
+    rows = w.shape[0]; sfx_weight_split, include/sfx.h), cached on the tensor until its storage or version
+    changes.  (None, None) when the GEMM would not use it (cols < 64 or not a multiple of 4)."""
+    rows = w.shape[0] if rows is None else rows
+    cols = w.numel() // rows
+    if cols < SPLIT_MIN_K or cols % 4:
+        return None, None
+    key = (w.data_ptr(), w._version, tuple(w.shape), rows)
+    c = getattr(w, "_sfx_wsplit", None)
+    if c is not None and c[0] == key:
+        return c[1].data_ptr(), c[2].data_ptr()
+    w2 = w.reshape(rows, cols)
+    if w2.stride(1) != 1 or w2.stride(0) % 4 or w2.data_ptr() % 16:
+        w2 = w2.contiguous()
+    sp = torch.empty(rows, cols, device=w.device, dtype=torch.float32)
+    inv = torch.empty(rows, device=w.device, dtype=torch.float32)
+    call("sfx_weight_split", rows, cols, ptr(w2), w2.stride(0), ptr(sp), ptr(inv), stream())
+    w._sfx_wsplit = (key, sp, inv)
+    return sp.data_ptr(), inv.data_ptr()
+
+
 def _slot_args(slot: Optional[Tuple[int, int]]):
     return (None, 0) if slot is None else slot
 
@@ -158,7 +184,8 @@ def linear(x: Tensor, weight: Tensor, bias: Optional[Tensor] = None, *, act: int
     ys = new_amax(out.device) if y_amax else None
     call("sfx_linear", M, N, K, pa, lda, ptr(gather_idx), S, pw, ldw, ptr(bias), ptr(scale), ptr(shift), act,
          act_ncols, pr, ldr, ptr(residual_idx), py, ldy, pp, ldp, 1, 0, 0, 0, 0, ptr(out_rows), ptr(rowscale),
-         1 if pre_before_act else 0, *_slot_args(a_amax), *_slot_args(w_amax), *_slot_args(ys), stream())
+         1 if pre_before_act else 0, *_slot_args(a_amax), *_slot_args(w_amax), *_slot_args(ys),
+         *weight_split(weight), stream())
     return (out, ys) if y_amax else out
 
 
@@ -176,7 +203,7 @@ def grouped_linear(x: Tensor, weight: Tensor, bias: Tensor, groups: int, *, act:
     ys = new_amax(out.device) if y_amax else None
     call("sfx_linear", M, N, K, pa, lda, None, 1, ptr(weight), K, ptr(bias), None, None, act, -1, None, 0, None, py,
          ldy, None, 0, G, K, N * K, N, N, None, None, 0, *_slot_args(a_amax), *_slot_args(w_amax),
-         *_slot_args(ys), stream())
+         *_slot_args(ys), *weight_split(weight, G * N), stream())
     return (out, ys) if y_amax else out
 
 
@@ -418,7 +445,8 @@ def subm_conv(x: Tensor, smap: "SubmMap", weight: Tensor, bias: Optional[Tensor]
     px, ldx = _rows(x)
     po, ldo = _rows(out)
     call("sfx_subm_conv", n, cin, cout, px, ldx, ptr(smap.nbr), ptr(weight), ptr(bias), ptr(smap.pair_in),
-         ptr(smap.pair_out), smap._off_host, po, ldo, *_slot_args(x_amax), *_slot_args(w_amax), stream())
+         ptr(smap.pair_out), smap._off_host, po, ldo, *_slot_args(x_amax), *_slot_args(w_amax),
+         *weight_split(weight), stream())
     return out
 
 

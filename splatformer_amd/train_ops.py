@@ -14,14 +14,14 @@ from torch import Tensor
 
 from . import _lib
 from ._lib import F, I, L, P, Z, call, ptr, stream
-from .ptv3_ops import _rows
+from .ptv3_ops import _rows, weight_split
 
 D = C.c_double
 
-_lib.register("sfx_linear_bwd_data", [I, I, I, P, L, P, L, P, I, I, P, L, P, L, I, P])
+_lib.register("sfx_linear_bwd_data", [I, I, I, P, L, P, L, P, I, I, P, L, P, L, I, P, P, P])
 _lib.register("sfx_linear_wgrad", [I, I, I, P, L, P, L, P, L, P, P])
 _lib.register("sfx_transpose", [I, I, P, L, P, L, P])
-_lib.register("sfx_subm_conv_bwd_data", [I, I, I, P, L, P, P, P, P, P, P, P, L, P])
+_lib.register("sfx_subm_conv_bwd_data", [I, I, I, P, L, P, P, P, P, P, P, P, L, P, P, P])
 _lib.register("sfx_window_attention_bwd", [I, I, I, I, I, P, P, P, F, P, P, P])
 _lib.register("sfx_layernorm_bwd", [I, I, P, L, P, P, L, P, L, F, P, L, P])
 _lib.register("sfx_cpe_ln_bwd", [I, I, P, P, P, P, P, P, F, P, P, P])
@@ -65,7 +65,7 @@ def linear_bwd_data(dy: Tensor, weight_t: Tensor, *, rowscale: Optional[Tensor] 
     po, ldo = _rows(out)
     pp, ldp = (None, 0) if dact_pre is None else _rows(dact_pre)
     call("sfx_linear_bwd_data", M, N, K, pd, ldd, pw, ldw, ptr(rowscale), dact, dact_ncols, pp, ldp, po, ldo,
-         1 if accumulate else 0, stream())
+         1 if accumulate else 0, *weight_split(weight_t), stream())
     return out
 
 
@@ -87,7 +87,7 @@ def subm_conv_bwd_data(dy: Tensor, smap, weight_t: Tensor, dx: Tensor) -> Tensor
     px, ldx = _rows(dx)
     ws = torch.empty(2 * max(n, 1), device=dy.device, dtype=torch.int32)
     call("sfx_subm_conv_bwd_data", n, cin, cout, pd, ldd, ptr(smap.nbr), ptr(weight_t), ptr(smap.pair_in),
-         ptr(smap.pair_out), smap._off_host, ws.data_ptr(), px, ldx, stream())
+         ptr(smap.pair_out), smap._off_host, ws.data_ptr(), px, ldx, *weight_split(weight_t), stream())
     return dx
 
 

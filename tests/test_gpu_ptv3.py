@@ -42,9 +42,10 @@ def test_linear_vs_torch(device, M, N, K, act):
 
 @pytest.mark.parametrize("scale", [1.0, 1e-30, 1e30])
 def test_linear_split_precision_is_fp32(device, scale):
-    """The fp16x2 split GEMM (default for K >= 64: power-of-two operand scales, two fp16 terms per operand,
-    three term products) is as accurate as fp32 arithmetic: its error against an fp64 product is at most that
-    of torch's fp32 CPU GEMM (x1.5), at operand magnitudes 1e+-30 (the scales absorb them)."""
+    """The fp16x2 split GEMM (default for K >= 64: a power-of-two scale per operand row -- A' rows chosen online
+    by the kernel, W rows by the cached pre-split --, two fp16 terms per operand, three term products) is as
+    accurate as fp32 arithmetic: its error against an fp64 product is at most that of torch's fp32 CPU GEMM
+    (x1.5), at operand magnitudes 1e+-30 (the scales absorb them)."""
     g = torch.Generator().manual_seed(7)
     M, N, K = 2000, 384, 1024
     x = torch.randn(M, K, generator=g) * scale

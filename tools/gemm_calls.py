@@ -1,5 +1,7 @@
-"""Per-call GEMM breakdown of one refine pass of the bench workload (config B), aggregated by
-(op, M, N, K): calls, ms per scene, TFLOP/s.  GPU only: python tools/gemm_calls.py"""
+"""Per-call GEMM breakdown of one refine (config B workload, or --config E / A): every GEMM-family launch timed
+in context (bench.GemmTimer: HIP events around each launch, real launch sequence), aggregated by
+(op, M, N, K): calls, ms per scene, TFLOP/s.  GPU only: python tools/gemm_calls.py [--config B]"""
+import argparse
 import collections
 import os
 import sys
@@ -15,32 +17,36 @@ from splatformer_amd.scenes import make_scene, to_device  # noqa: E402
 
 
 def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="B")
+    ap.add_argument("--passes", type=int, default=3)
+    a = ap.parse_args()
+    n, _, _, sh, _ = bench.DEFAULTS[a.config]
     dev = torch.device("cuda")
     torch.manual_seed(0)
-    model = FeaturePredictor(sh_degree=1, zeroinit=False).eval().to(dev)
-    scene = to_device(make_scene(100_000, sh_degree=1, seed=0), dev)
+    bk = bench.DEPTH1 if a.config == "A" else {}
+    model = FeaturePredictor(sh_degree=sh, zeroinit=False, backbone_kwargs=bk).eval().to(dev)
+    scene = to_device(make_scene(n, sh_degree=sh, seed=0), dev)
     model.refine_packed(scene)
-    with bench.GemmRecorder() as rec:
-        model.refine_packed(scene)
-    torch.cuda.synchronize()
-    agg = collections.defaultdict(lambda: [0, 0.0, 0.0])
-    for kind, fl, fn, shape in rec.calls:
-        fn()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(5):
-            fn()
-        e1.record()
+    runs = []
+    for _ in range(a.passes):
         torch.cuda.synchronize()
-        ms = e0.elapsed_time(e1) / 5
-        a = agg[(kind,) + tuple(shape)]
-        a[0] += 1
-        a[1] += ms
-        a[2] += fl
+        with bench.GemmTimer() as t:
+            model.refine_packed(scene)
+        runs.append(t.summary())
+    runs.sort(key=lambda r: sum(p[0] for p in r))
+    per = runs[len(runs) // 2]
+    agg = collections.defaultdict(lambda: [0, 0.0, 0.0])
+    for ms, kind, shape, fl, by in per:
+        k = agg[(kind,) + tuple(shape)]
+        k[0] += 1
+        k[1] += ms
+        k[2] += fl
     tot = sum(v[1] for v in agg.values())
     for k, (c, ms, fl) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
         print(f"{k[0]:15s} M={k[1]:6d} N={k[2]:5d} K={k[3]:5d} calls={c:3d} {ms:7.3f} ms {fl / ms / 1e9:6.1f} TF/s")
-    print(f"total {tot:.2f} ms / scene")
+    fl = sum(p[3] for p in per)
+    print(f"total {tot:.2f} ms / scene, {fl / tot / 1e9:.1f} TF/s")
 
 
 if __name__ == "__main__":
