@@ -292,8 +292,12 @@ def batchify(gs: Dict[str, torch.Tensor], grid_resolution: int = 384):
 
 
 def heads_forward(sd, y: torch.Tensor, feat: torch.Tensor, in_gs: Dict[str, torch.Tensor], sh_degree: int = 1,
-                  nlayer: int = 4, prefix: str = "features_outputhead."):
-    """cat(y, feat) -> per-feature MLP(ReLU) -> tanh(means) -> residual add."""
+                  nlayer: int = 4, prefix: str = "features_outputhead.", relu_masks=None):
+    """cat(y, feat) -> per-feature MLP(ReLU) -> tanh(means) -> residual add.
+
+    relu_masks (test replay only): {feature: [active mask of hidden layer li]} -- each ReLU then keeps exactly
+    the given active set (z * mask), so a gradient comparison is not decided by ReLU inputs that lie within
+    rounding of 0 (whose sign differs between two fp32 evaluation orders)."""
     h0 = torch.cat([y, feat], 1)
     out = {}
     for f in INPUT_FEATURES:
@@ -301,7 +305,8 @@ def heads_forward(sd, y: torch.Tensor, feat: torch.Tensor, in_gs: Dict[str, torc
             continue
         h = h0
         for li in range(nlayer - 1):
-            h = torch.relu(F.linear(h, sd[f"{prefix}{f}.{2 * li}.weight"], sd[f"{prefix}{f}.{2 * li}.bias"]))
+            z = F.linear(h, sd[f"{prefix}{f}.{2 * li}.weight"], sd[f"{prefix}{f}.{2 * li}.bias"])
+            h = torch.relu(z) if relu_masks is None else z * relu_masks[f][li].to(z.dtype)
         o = F.linear(h, sd[f"{prefix}{f}.{2 * (nlayer - 1)}.weight"], sd[f"{prefix}{f}.{2 * (nlayer - 1)}.bias"])
         if f == "means":
             o = torch.tanh(o)
@@ -312,7 +317,7 @@ def heads_forward(sd, y: torch.Tensor, feat: torch.Tensor, in_gs: Dict[str, torc
 
 
 def feature_predictor_forward(sd, cfg: PTv3Config, gs: Dict[str, torch.Tensor], perms, sh_degree=1,
-                              grid_resolution=384, train=False, masks=None):
+                              grid_resolution=384, train=False, masks=None, relu_masks=None):
     data = batchify(gs, grid_resolution)
     point = ptv3_forward(sd, cfg, data, perms, prefix="backbone.backbone.", train=train, masks=masks)
-    return heads_forward(sd, point.feat, data["feat"], gs, sh_degree), point
+    return heads_forward(sd, point.feat, data["feat"], gs, sh_degree, relu_masks=relu_masks), point

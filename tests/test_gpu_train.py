@@ -1,12 +1,12 @@
 """Training step (configs C/D) on HIP vs torch autograd of the CPU oracle in train mode.
 
-Two levels:
-- the PTv3 backbone alone (GELU/LayerNorm/BatchNorm/softmax: smooth almost everywhere) -- the qkv
-  gradients must be as close to the fp64 oracle as the fp32 oracle is (2x + 1e-5);
-- the whole refiner incl. the ReLU heads: a ReLU whose input lies within fp32 rounding of 0 flips its mask
+Two levels, both held to the same bar -- the qkv gradients must be as close to the fp64 oracle as the fp32
+oracle is (2x + 1e-5):
+- the PTv3 backbone alone (GELU/LayerNorm/BatchNorm/softmax: smooth almost everywhere);
+- the whole refiner incl. the ReLU heads.  A ReLU whose input lies within fp32 rounding of 0 flips its mask
   between any two fp32 evaluations (the HIP forward sums in another order than torch), and a single flip
-  moves the qkv gradients by ~1e-3 relative, so the bar there is 1e-2 (documented, not a tolerance on a
-  rounding-order-free quantity) with the forward itself held to 1e-5.
+  moves the qkv gradients by ~1e-3 relative; so HIP's active sets are replayed into the oracle (both its
+  fp32 and fp64 runs), which makes the comparison free of that discontinuity.
 
 Same inputs on both sides: state dict, scene, the 5 order shuffles and the DropPath masks (recorded from
 the HIP run and replayed into the oracle).  Checked: the train-mode forward (batch-statistics BatchNorm,
@@ -67,6 +67,10 @@ def test_refiner_train_grads_match_oracle(device, n, unique, bk):
     perms = model.backbone.backbone.last_perms
     d_packed = torch.randn(packed.shape, generator=torch.Generator().manual_seed(9))
     strain.refine_backward(model, tape, d_packed.to(device))
+    # HIP's ReLU active sets of the three hidden head layers, per feature (columns g*W .. (g+1)*W)
+    fpm = model
+    W = fpm.width
+    relu = {f: [(h[:, g * W:(g + 1) * W] > 0).cpu() for h in tape["hs"]] for g, f in enumerate(fpm.output_features)}
 
     # oracle: same weights, perms, masks; autograd w.r.t. the qkv parameters, in fp32 and in fp64
     def oracle(dtype):
@@ -76,7 +80,7 @@ def test_refiner_train_grads_match_oracle(device, n, unique, bk):
                 v.requires_grad_()
         sc = {k: v.to(dtype) for k, v in s.items()}
         mk = {k: m.to(dtype) for k, m in masks.masks.items()}
-        ref, _ = ptv3_ref.feature_predictor_forward(sdd, cfg, sc, perms, train=True, masks=mk)
+        ref, _ = ptv3_ref.feature_predictor_forward(sdd, cfg, sc, perms, train=True, masks=mk, relu_masks=relu)
         rp = torch.cat([ref[f].reshape(n, -1) for f in FEATS], 1)
         (rp * d_packed.to(dtype)).sum().backward()
         return sdd, rp.detach()
@@ -103,7 +107,7 @@ def test_refiner_train_grads_match_oracle(device, n, unique, bk):
     r64 = torch.cat([sd64[k].grad.reshape(-1) for k in names])
     e_hip, e_ref = rel_l2(hip, r64), rel_l2(r32, r64)
     print(f"\n[refiner {n} {bk}] qkv grads to fp64: HIP {e_hip:.2e}, fp32 oracle {e_ref:.2e}")
-    assert e_hip < 1e-2, f"HIP {e_hip:.2e} vs fp32-oracle {e_ref:.2e} (to fp64)"
+    assert e_hip <= 2.0 * e_ref + 1e-5, f"HIP {e_hip:.2e} vs fp32-oracle {e_ref:.2e} (to fp64)"
 
 
 @pytest.mark.parametrize("n,unique,bk", [
