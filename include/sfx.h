@@ -103,6 +103,17 @@ int sfx_rasterize_bwd(int tiles_x, int tiles_y, int block_width, int img_h, int 
                       const float* v_out, const float* v_out_alpha, float* v_xy, float* v_xy_abs, float* v_conic,
                       float* v_rgb, float* v_opacity, void* stream);
 
+/* Eval-path rasterizer over packed records (round 2): sfx_pack_raster_records writes one 48-byte record per
+ * projected Gaussian, r0 = (x, y, opacity, conic.a), r1 = (conic.b, conic.c, r, g), r2 = (b, 0, 0, 0)
+ * (records 16-byte aligned, 12 floats each); sfx_rasterize_fwd_views_packed is sfx_rasterize_fwd_views over
+ * them (same outputs, bit for bit). */
+int sfx_pack_raster_records(int n, const float* xys, const float* conics, const float* colors, const float* opacity,
+                            float* records, void* stream);
+int sfx_rasterize_fwd_views_packed(int views, int tiles_x, int tiles_y, int block_width, int img_h, int img_w,
+                                   const int32_t* gids_sorted, const int* tile_bins, const float* records,
+                                   const float* background, int clamp_max1, float* final_Ts, int* final_idx,
+                                   float* out_img, float* out_alpha, void* stream);
+
 /* ---- refiner: Pointcept PTv3 m1 + FeaturePredictor (models/pointtransformer_v3.py, feature_predictor.py) -- */
 /* fp32 MFMA GEMM, Y = act((A' W^T + bias) * scale + shift) + R[ridx]; A' = A or, with gather_idx [M][S],
  * the concatenation of S gathered rows (SubMConv3d implicit GEMM).  act: 0 none, 1 GELU(erf), 2 ReLU,

@@ -44,6 +44,8 @@ _lib.register("sfx_render_prep_project_views", [I, I, I, P, L, P, L, P, L, P, L,
                                                  P, P, P, P, P, P, P, P])
 _lib.register("sfx_isect_emit_views", [I, I, P, P, P, P, I, I, I, P, P, P])
 _lib.register("sfx_rasterize_fwd_views", [I, I, I, I, I, I, P, P, P, P, P, P, P, I, P, P, P, P, P])
+_lib.register("sfx_pack_raster_records", [I, P, P, P, P, P, P])
+_lib.register("sfx_rasterize_fwd_views_packed", [I, I, I, I, I, I, P, P, P, P, I, P, P, P, P, P])
 
 
 def rasterize_gaussians_to_multiimgs(gs_params: Dict[str, Tensor], cameras: Dict) -> Tuple[List[Tensor], List[Tensor]]:
@@ -184,8 +186,10 @@ def _render_fused_views(gs, c2ws, cameras, meta=None):
         bins = f(V * T, 2, dt=torch.int32)
         call("sfx_tile_bins", total, ptr(isect_s), V * T, ptr(bins), stream())
         final_Ts, final_idx = f(V, H, W), f(V, H, W, dt=torch.int32)
-        call("sfx_rasterize_fwd_views", V, tiles_x, tiles_y, bw, H, W, ptr(gids_s), ptr(bins), ptr(xys), ptr(conics),
-             ptr(rgbs), ptr(opac), ptr(bg), 1, ptr(final_Ts), ptr(final_idx), ptr(out), ptr(alpha), stream())
+        rec = f(V * n, 12)  # packed 48-byte records: one gather per Gaussian in the rasterizer's batch fetch
+        call("sfx_pack_raster_records", V * n, ptr(xys), ptr(conics), ptr(rgbs), ptr(opac), ptr(rec), stream())
+        call("sfx_rasterize_fwd_views_packed", V, tiles_x, tiles_y, bw, H, W, ptr(gids_s), ptr(bins), ptr(rec),
+             ptr(bg), 1, ptr(final_Ts), ptr(final_idx), ptr(out), ptr(alpha), stream())
     for v in range(V):
         if per_view[v] < 1:
             out[v] = torch.clamp(bg, max=1.0).expand(H, W, 3)

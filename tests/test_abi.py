@@ -34,6 +34,7 @@ def test_python_signatures_cover_header():
     import splatformer_amd.train_ops  # noqa: F401  (training entry points)
     import splatformer_amd.metrics  # noqa: F401  (evaluation entry points)
     import splatformer_amd.gs_render  # noqa: F401  (batched-view render entry points)
+    import splatformer_amd.downsample  # noqa: F401  (point-downsampling entry points)
     missing = [s for s in declared_symbols() if s not in _lib.SIGNATURES]
     assert not missing, f"no ctypes signature for: {missing}"
 
