@@ -157,14 +157,11 @@ class FeaturePredictor(nn.Module):
             h0[:, :cb] = mapper(y)
         w1, b1, mids, wl, bl, out_dim = self._packed_heads()
         x = h0[:, :w1.shape[1]]  # [y | feat | 0-pad]
-        # fp16x2 operand bounds: each head layer's epilogue publishes max |output| for the next layer
-        h, h_amax = ops.linear(x, w1, b1, act=ops.ACT_RELU, w_amax=ops.weight_amax(w1), y_amax=True)
+        h = ops.linear(x, w1, b1, act=ops.ACT_RELU)
         for wm, bm in mids:
-            h, h_amax = ops.grouped_linear(h, wm, bm, len(self.output_features), act=ops.ACT_RELU, a_amax=h_amax,
-                                           w_amax=ops.weight_amax(wm), y_amax=True)
+            h = ops.grouped_linear(h, wm, bm, len(self.output_features), act=ops.ACT_RELU)
         n_tanh = self.ch["means"] if self.output_features[0] == "means" else 0
-        return ops.linear(h, wl, bl, act=ops.ACT_TANH, act_ncols=n_tanh, residual=feat, a_amax=h_amax,
-                          w_amax=ops.weight_amax(wl))
+        return ops.linear(h, wl, bl, act=ops.ACT_TANH, act_ncols=n_tanh, residual=feat)
 
     def unpack(self, packed: Tensor) -> Dict[str, Tensor]:
         out = OrderedDict()

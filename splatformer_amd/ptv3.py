@@ -128,30 +128,21 @@ class Block(nn.Module):
         C = self.channels
         ln_c = self.cpe[2]
         wf, bf = self.cpe_fused()
-        # fp16x2 operand bounds (ptv3_ops.new_amax): the conv input's from the producer of x (previous Block's
-        # fc2 epilogue) when it is the conv input; LayerNorm outputs by their weight bound; the attention
-        # output by max|qkv| (a convex combination of v rows); fc1 / fc2 / qkv outputs from their epilogues
-        x_amax = point.get("feat_amax") if conv_in is None else None
-        t = ops.subm_conv(x if conv_in is None else conv_in, point.nbr, wf, bf, x_amax=x_amax,
-                          w_amax=ops.weight_amax(wf))
+        # The GEMMs scale their fp16x2 operands per row themselves (no operand bounds needed); the qkv GEMM
+        # publishes max |qkv| for the attention's fp16x2 q / k / v terms (ptv3_ops.new_amax)
+        t = ops.subm_conv(x if conv_in is None else conv_in, point.nbr, wf, bf)
         ln1 = self.norm1[0]
         x1, h = ops.cpe_residual_ln(t, x, ln_c.weight, ln_c.bias, ln1.weight, ln1.bias, ln1.eps)
-        qkv, q_amax = ops.linear(h, self.attn.qkv.weight, self.attn.qkv.bias, a_amax=ops.ln_amax(ln1.weight, ln1.bias),
-                                 w_amax=ops.weight_amax(self.attn.qkv.weight), y_amax=True)
+        qkv, q_amax = ops.linear(h, self.attn.qkv.weight, self.attn.qkv.bias, y_amax=True)
         K, win, nw = point_windows(point, self.attn.patch_size_max)
         oi = point.order_type[self.attn.order_index]
         a = ops.window_attention(qkv, point.order_phys[oi], win, nw, K, self.attn.num_heads, C, qkv_amax=q_amax)
-        x2 = ops.linear(a, self.attn.proj.weight, self.attn.proj.bias, residual=x1, a_amax=q_amax,
-                        w_amax=ops.weight_amax(self.attn.proj.weight))
+        x2 = ops.linear(a, self.attn.proj.weight, self.attn.proj.bias, residual=x1)
         ln2 = self.norm2[0]
         h2 = ops.layernorm(x2, ln2.weight, ln2.bias, ln2.eps)
         mlp = self.mlp[0]
-        m, m_amax = ops.linear(h2, mlp.fc1.weight, mlp.fc1.bias, act=ops.ACT_GELU,
-                               a_amax=ops.ln_amax(ln2.weight, ln2.bias), w_amax=ops.weight_amax(mlp.fc1.weight),
-                               y_amax=True)
-        point.feat, point.feat_amax = ops.linear(m, mlp.fc2.weight, mlp.fc2.bias, residual=x2, out=out,
-                                                 a_amax=m_amax, w_amax=ops.weight_amax(mlp.fc2.weight),
-                                                 y_amax=True)
+        m = ops.linear(h2, mlp.fc1.weight, mlp.fc1.bias, act=ops.ACT_GELU)
+        point.feat = ops.linear(m, mlp.fc2.weight, mlp.fc2.bias, residual=x2, out=out)
         return point
 
 
@@ -213,8 +204,7 @@ class SerializedPooling(nn.Module):
     def run(self, point: Point, perm: Sequence[int]) -> Point:
         st = self.geometry_begin(point)
         # the projection does not depend on the clusters: enqueued while the host waits for the pooled count
-        pf = ops.linear(point.feat, self.proj.weight, self.proj.bias, a_amax=point.get("feat_amax"),
-                        w_amax=ops.weight_amax(self.proj.weight))
+        pf = ops.linear(point.feat, self.proj.weight, self.proj.bias)
         new, sidx, idx_ptr, m = self.geometry_end(point, perm, st)
         sc, sh = bn_affine(self.norm[0])
         new.feat = ops.segment_max_affine_act(pf, idx_ptr, sidx, m, sc, sh, ops.ACT_GELU)
@@ -232,14 +222,12 @@ class SerializedUnpooling(nn.Module):
         parent = point.pop("pooling_parent")
         inverse = point.pop("pooling_inverse")
         sc, sh = bn_affine(self.proj[1])
-        coarse = ops.linear(point.feat, self.proj[0].weight, self.proj[0].bias, scale=sc, shift=sh, act=ops.ACT_GELU,
-                            a_amax=point.get("feat_amax"), w_amax=ops.weight_amax(self.proj[0].weight))
+        coarse = ops.linear(point.feat, self.proj[0].weight, self.proj[0].bias, scale=sc, shift=sh, act=ops.ACT_GELU)
         sc2, sh2 = bn_affine(self.proj_skip[1])
         skip = torch.empty(parent.feat.shape[0], coarse.shape[1], device=coarse.device)
-        parent.feat, parent.feat_amax = ops.linear(
+        parent.feat = ops.linear(
             parent.feat, self.proj_skip[0].weight, self.proj_skip[0].bias, scale=sc2, shift=sh2, act=ops.ACT_GELU,
-            residual=coarse, residual_idx=inverse, pre_out=skip, a_amax=parent.get("feat_amax"),
-            w_amax=ops.weight_amax(self.proj_skip[0].weight), y_amax=True)
+            residual=coarse, residual_idx=inverse, pre_out=skip)
         # Pointcept quirk: SerializedUnpooling does not refresh sparse_conv_feat, so the next Block's
         # SubMConv3d sees proj_skip(parent) only (PointSequential semantics, pointtransformer_v3.py:52-79)
         parent.stale_conv_feat = skip
@@ -368,10 +356,9 @@ class PointTransformerV3(nn.Module):
         emb, bnm = self.embedding[0], self.embedding[1]
         sc, sh = bn_affine(bnm)
         # the embedding needs no geometry: enqueued first, it runs while prepare() waits for the grid depth
-        emb_feat, emb_amax = ops.linear(feat, emb.weight, emb.bias, scale=sc, shift=sh, act=ops.ACT_GELU,
-                                        y_amax=True)
+        emb_feat = ops.linear(feat, emb.weight, emb.bias, scale=sc, shift=sh, act=ops.ACT_GELU)
         point = self.prepare(data_dict, perms)
-        point.feat, point.feat_amax = emb_feat, emb_amax
+        point.feat = emb_feat
         k = 1
         for s in range(self.num_stages):
             stage = getattr(self.enc, f"enc{s}")
