@@ -1016,28 +1016,41 @@ void gemm_amax_jobs(const GemmArgs& a, int groups, AmaxJob& ja, AmaxJob& jw) {
 }
 
 // Measured per-launch best (tile configuration, Stream-K) for the config-B refine's dense linears under fp16x2
-// operands (tools/gemm_tune.py, profiles/r01_gemm_tune_f16x2.jsonl) where it beats the cost model by > 2 us;
+// operands (tools/gemm_tune.py; profiles/r01_gemm_tune_f16x2.jsonl, re-swept with the per-row scales in
+// profiles/r02_gemm_tune.jsonl) where it beats the cost model by > 2 us;
 // applied when N and K match and M is within 0.8-1.25x of the tuned M (stage point counts vary per scene).
 struct TunedLaunch {
   int M, N, K, cfg, sk;
 };
 constexpr TunedLaunch kTuned[] = {
-    {100000, 64, 23, 2, 1},
+    {100000, 64, 23, 2, 0},
     {100000, 256, 64, 1, 1},
-    {90434, 128, 96, 2, 1},
+    {90434, 128, 96, 3, 1},
     {70349, 384, 128, 1, 0},
-    {70349, 128, 128, 2, 1},
-    {70349, 512, 128, 2, 0},
-    {70349, 128, 512, 2, 0},
-    {70349, 256, 128, 2, 1},
+    {70349, 128, 128, 3, 0},
+    {70349, 512, 128, 3, 1},
+    {70349, 128, 512, 3, 0},
+    {70349, 256, 128, 3, 1},
     {37759, 768, 256, 6, 0},
     {37759, 256, 256, 1, 1},
     {37759, 256, 1024, 1, 0},
     {37759, 512, 256, 6, 1},
     {14764, 1536, 512, 6, 0},
     {14764, 2048, 512, 6, 1},
-    {14764, 512, 2048, 6, 1},
-    {100000, 768, 120, 1, 0}};
+    {14764, 512, 2048, 6, 0},
+    {100000, 768, 120, 6, 0},
+    {37759, 1024, 256, 6, 1},
+    {14764, 512, 512, 6, 0},
+    {70349, 96, 128, 1, 0},
+    {100000, 384, 96, 1, 1}};
+
+// The same for the SubM conv launches of config B's stages (sfx_subm_conv: n, Cout, Cin -> the tile shape /
+// Stream-K of its centre and pair launches; profiles/r02_gemm_tune.jsonl)
+constexpr TunedLaunch kTunedConv[] = {
+    {90434, 96, 96, 3, 1},
+    {70349, 128, 128, 3, 1},
+    {37759, 256, 256, 6, 1},
+    {100000, 96, 96, 3, 0}};
 
 // tuning / test hooks: SFX_GEMM_CFG=<index into kCfgs>, SFX_GEMM_SK=0|1, or sfx_gemm_force_config()
 int forced = -2, forced_sk = -2;
@@ -1063,6 +1076,12 @@ int pick_cfg(GemmArgs& a, int groups, bool vec) {
                      !a.y_amax &&
                      !(a.R && a.R == a.Y) && a.M > 0 && forced_sk != 0;
   const double sk_overhead = a.pair_mode ? 2.5 : 4.0;  // slab-equivalents: partial epilogues (+ memset)
+  if (force < 0 && forced_sk < 0 && a.tuned > 0 && !((kCfgs[a.tuned - 1].nw == 8) && !split)) {
+    const int c = a.tuned - 1;
+    a.sk = (a.tuned_sk && sk_ok && kCfgs[c].bm >= 128) ? 1 : 0;
+    tiles_m_of(a, kCfgs[c].bm);
+    return c;
+  }
   if (force < 0 && forced_sk < 0 && !a.pair_mode && !a.gidx && groups == 1) {
     for (const TunedLaunch& t : kTuned) {
       if (t.N == a.N && t.K == a.K && 5ll * a.M >= 4ll * t.M && 4ll * a.M <= 5ll * t.M &&
@@ -1331,6 +1350,12 @@ int sfx_subm_conv(int n, int cin, int cout, const float* x, long long ldx, const
   // 1) centre offset: dense gathered GEMM with bias, plain stores
   GemmArgs a{};
   a.M = n; a.N = cout; a.K = cin; a.A = x; a.lda = ldx; a.gidx = nbr + 13; a.S = 1; a.Kseg = cin; a.gstride = 27;
+  for (const TunedLaunch& t : kTunedConv)  // measured tile shape for both launches of this conv
+    if (t.N == cout && t.K == cin && 5ll * n >= 4ll * t.M && 4ll * n <= 5ll * t.M) {
+      a.tuned = t.cfg + 1;
+      a.tuned_sk = t.sk;
+      break;
+    }
   a.W = weight + 13ll * cin; a.ldw = 27ll * cin; a.bias = bias; a.act = 0; a.act_ncols = cout; a.Y = out; a.ldy = ldo;
   // fp16x2: one pair of maxima (all of x, all 27 weight slices) for both launches, or the pre-split weight
   a.a_amax = x_amax; a.a_tag = x_tag; a.w_amax = w_amax; a.w_tag = w_tag;

@@ -92,6 +92,7 @@ struct GemmArgs {
   long long gWinv;
   long long slice_winv_stride;  // pair mode: winv offset per slice (row-sliced weights, e.g. the conv backward)
   int epi_vec;  // epilogue operands allow 16-byte accesses (set by launch_ws)
+  int tuned, tuned_sk;  // measured tile configuration + 1 (0: cost model / table) and its Stream-K flag
 };
 
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }

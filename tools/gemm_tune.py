@@ -16,6 +16,50 @@ from splatformer_amd.feature_predictor import FeaturePredictor  # noqa: E402
 from splatformer_amd.scenes import make_scene, to_device  # noqa: E402
 
 
+class GemmRecorder:
+    """Records the GEMM launches (ptv3_ops.linear / subm_conv / grouped_linear) of one refine pass as
+    re-runnable closures writing into scratch outputs."""
+
+    def __enter__(self):
+        self.calls = []
+        self._lin, self._conv, self._grp = ops.linear, ops.subm_conv, ops.grouped_linear
+        rec = self
+
+        def lin(x, weight, bias=None, **kw):
+            res = rec._lin(x, weight, bias, **kw)
+            out = res[0] if isinstance(res, tuple) else res
+            M, (N, K) = out.shape[0], weight.shape
+            kw2 = dict(kw, out=torch.empty_like(out))
+            if kw.get("pre_out") is not None:
+                kw2["pre_out"] = torch.empty_like(kw["pre_out"])
+            rec.calls.append(("linear", 2.0 * M * N * K, lambda: rec._lin(x, weight, bias, **kw2), (M, N, K)))
+            return res
+
+        def conv(x, smap, weight, bias, out=None, **kw):
+            o = rec._conv(x, smap, weight, bias, out=out, **kw)
+            n, cin = x.shape
+            cout = weight.shape[0]
+            scratch = torch.empty_like(o)
+            rec.calls.append(("subm_conv", 2.0 * (n + smap.num_pairs) * cin * cout,
+                              lambda: rec._conv(x, smap, weight, bias, out=scratch, **kw), (n, cout, cin)))
+            return o
+
+        def grp(x, weight, bias, groups, **kw):
+            res = rec._grp(x, weight, bias, groups, **kw)
+            out = res[0] if isinstance(res, tuple) else res
+            G, N, K = weight.shape
+            scratch = torch.empty_like(out)
+            rec.calls.append(("grouped_linear", 2.0 * x.shape[0] * G * N * K,
+                              lambda: rec._grp(x, weight, bias, groups, **dict(kw, out=scratch)), (x.shape[0], G * N, K)))
+            return res
+
+        ops.linear, ops.subm_conv, ops.grouped_linear = lin, conv, grp
+        return self
+
+    def __exit__(self, *a):
+        ops.linear, ops.subm_conv, ops.grouped_linear = self._lin, self._conv, self._grp
+
+
 def timeit(fn, reps=8):
     fn()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -34,7 +78,7 @@ def main():
     model = FeaturePredictor(sh_degree=1, zeroinit=False).eval().to(dev)
     scene = to_device(make_scene(n, sh_degree=1, seed=0), dev)
     model.refine_packed(scene)
-    with bench.GemmRecorder() as rec:
+    with GemmRecorder() as rec:
         model.refine_packed(scene)
     torch.cuda.synchronize()
     seen = {}
