@@ -44,3 +44,35 @@ def test_load_checkpoint_strict_reports_missing():
     else:
         raise AssertionError("strict load accepted a missing key")
     assert convert_state_dict({}, {}) == {}
+
+
+def test_pretrained_backbone_checkpoint(tmp_path):
+    """pointtransformer_v3.py:164-178: a Pointcept segmentor checkpoint ({'state_dict': {'module.backbone.*',
+    'module.seg_head.*'}}, e.g. a ScanNet PTv3 with 6 input channels) feeds the backbone -- keys matched by name
+    after stripping 'module.backbone.', shape mismatches (the embedding) and non-backbone keys skipped, nothing
+    else touched.  The checkpoint is built from a module of a different configuration (in_channels 6), not from
+    the module that loads it."""
+    from splatformer_amd.ptv3 import PointTransformerV3Model
+    torch.manual_seed(3)
+    scannet = PointTransformerV3Model(in_channels=6)
+    sd = {"module.backbone." + k: v.clone() for k, v in scannet.backbone.state_dict().items()}
+    sd["module.seg_head.weight"] = torch.randn(20, 64)
+    sd["module.seg_head.bias"] = torch.randn(20)
+    path = os.path.join(str(tmp_path), "scannet-semseg-pt-v3m1-0-base.pth")
+    torch.save({"state_dict": sd, "epoch": 100}, path)
+    torch.manual_seed(4)
+    fresh = PointTransformerV3Model(in_channels=23)
+    before = {k: v.clone() for k, v in fresh.backbone.state_dict().items()}
+    torch.manual_seed(4)
+    loaded = PointTransformerV3Model(in_channels=23, pretrained_ckpt=path)
+    src = scannet.backbone.state_dict()
+    n_loaded = n_skipped = 0
+    for k, v in loaded.backbone.state_dict().items():
+        if src[k].shape == v.shape:
+            assert torch.equal(v, src[k]), k
+            n_loaded += 1
+        else:  # the embedding's input width differs (6 vs 23): left at its own initialisation
+            assert torch.equal(v, before[k]), k
+            n_skipped += 1
+    assert n_skipped >= 1 and n_loaded > 100
+    assert all(k.startswith("embedding") for k, v in loaded.backbone.state_dict().items() if src[k].shape != v.shape)
