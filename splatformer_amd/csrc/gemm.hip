@@ -62,11 +62,15 @@ using namespace sfxg;
 // waves rescale that row's accumulators before adding it.  The epilogue unscales each row by its final 1/s.
 // Error: that of fp32 arithmetic (dropped l*l <= 2^-22 relative, products exact in fp32) for every row,
 // whatever the other rows' magnitudes.
+//
+// SPL = 4: fp16x2 with A pre-split as well (sfx_split_rows layout, one scale per source row over the whole
+// row): the staging threads only copy both operands' term images, no split, no overflow check, no rescale.
 template <int BM, int BN, int WGM, int NW, bool VEC, int MODE, int SPL>
 __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs p, int tiles_n, int total_tiles) {
   constexpr bool SPLIT = SPL != 0;
-  constexpr int NTERM = SPL == 2 ? 2 : 3;  // LDS term images per operand
-  static_assert(SPL == 0 || SPL == 2 || SPL == 3, "operand precision");
+  constexpr bool F16 = SPL == 2 || SPL == 4;  // fp16x2 terms (A split in-kernel / pre-split)
+  constexpr int NTERM = F16 ? 2 : 3;          // LDS term images per operand
+  static_assert(SPL == 0 || SPL == 2 || SPL == 3 || SPL == 4, "operand precision");
   constexpr int NT = NW * 64;                  // threads
   constexpr int WGN = NW / WGM;                // waves along N
   constexpr int WM = BM / WGM, WN = BN / WGN;  // wave sub-tile
@@ -79,9 +83,9 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs
   constexpr int W_ITERS = BN * BK / 4 / NT;
   constexpr int NBUF = SPLIT ? (NW == 8 ? SFX_NBUF8 : 1) : 2;
   // fp32: double-buffered [row][k] images (row stride 36); SPLIT: NBUF x 3 swizzled bf16 term images
-  // (SPL == 2 appends the per-row scale state: [NBUF][BM] factors, [BM] 1/s, [NBUF] flags -- in the same LDS
-  // object: a further __shared__ object can make hipcc wait vmcnt(0) before ds_reads)
-  constexpr int AUX_FLOATS = SPL == 2 ? NBUF * BM + BM + 4 : 0;
+  // (fp16x2 appends the per-row scale state: [NBUF][BM] factors, [2][BM] 1/s by segment parity, [NBUF] flags --
+  // in the same LDS object: a further __shared__ object can make hipcc wait vmcnt(0) before ds_reads)
+  constexpr int AUX_FLOATS = F16 ? NBUF * BM + 2 * BM + 4 : 0;
   constexpr int A_FLOATS = (SPLIT ? NBUF * NTERM * BM * BK / 2 : 2 * BM * LDS_STRIDE) + AUX_FLOATS;
   constexpr int W_FLOATS = SPLIT ? NBUF * NTERM * BN * BK / 2 : 2 * BN * LDS_STRIDE;
   __shared__ __attribute__((aligned(16))) float sAraw[A_FLOATS];
@@ -93,11 +97,12 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs
   // byte offset of the 4-element group at k = c4 * 4 (c4 = 0..7) of row r in a swizzled term image
   auto swz = [](int r, int c4) -> int { return r * 64 + ((((c4 >> 1) ^ (r >> 2)) & 3) << 4) + ((c4 & 1) << 3); };
   float* s_fac = sAraw + (A_FLOATS - AUX_FLOATS);   // [NBUF][BM]
-  float* s_inv = s_fac + NBUF * BM;                  // [BM]
-  int* s_flag = reinterpret_cast<int*>(s_inv + BM);  // [NBUF]
+  float* s_inv = s_fac + NBUF * BM;                  // [2][BM]: a segment's epilogue reads its own copy while the
+                                                     // next segment's first slab is staged into the other
+  int* s_flag = reinterpret_cast<int*>(s_inv + 2 * BM);  // [NBUF]
 
   const int g = blockIdx.z;
-  const float* A = p.A + g * p.gA;
+  const float* A = (SPL == 4 ? p.Asp : p.A) + g * p.gA;
   const float* bias = p.bias ? p.bias + g * p.gB : nullptr;
   float* Y = p.Y + g * p.gY;
   const __amdgpu_buffer_rsrc_t rA = rsrc(A);
@@ -114,7 +119,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs
     if (tid < NBUF) s_flag[tid] = 0;  // (published by the first barrier)
   }
   // byte offsets fit 31 bits (host checks every operand against the 2 GiB buffer range)
-  const unsigned lda32 = (unsigned)p.lda, ldw32 = (unsigned)p.ldw, ldy32 = (unsigned)p.ldy, ldws32 = (unsigned)p.ldws;
+  const unsigned lda32 = (unsigned)(SPL == 4 ? p.ldas : p.lda), ldw32 = (unsigned)p.ldw, ldy32 = (unsigned)p.ldy, ldws32 = (unsigned)p.ldws;
   const unsigned ldr32 = (unsigned)p.ldr, ldp32 = (unsigned)p.ldypre;
   const int lrow = tid >> 3, lcol = (tid & 7) * 4;  // staging coordinates: rows lrow + RPP i, cols lcol..+3
 
@@ -136,7 +141,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs
     ti.gidx = MODE == MODE_DENSE ? nullptr : p.gidx;
     ti.gstride = p.gstride;
     ti.out_rows = p.out_rows;
-    ti.W = (SPL == 2 ? p.Wsp : p.W) + g * p.gW;
+    ti.W = (F16 ? p.Wsp : p.W) + g * p.gW;
     ti.winv = p.winv ? p.winv + g * p.gWinv : nullptr;
     if constexpr (MODE == MODE_PAIR) {
       int sl = 0;
@@ -148,7 +153,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs
       ti.gidx = p.pair_in + base;
       ti.gstride = 1;
       ti.out_rows = p.pair_out + base;
-      ti.W = (SPL == 2 ? p.Wsp : p.W) + sl * p.slice_w_stride;
+      ti.W = (F16 ? p.Wsp : p.W) + sl * p.slice_w_stride;
       if (p.winv) ti.winv = p.winv + sl * p.slice_winv_stride;
     }
     return ti;
@@ -173,7 +178,8 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs
   };
 
   float4 ra[A_ITERS], rw[W_ITERS];
-  auto load_tiles = [&](const Tile& ti, int kt) {
+  float rinv[A_ITERS];  // SPL == 4: 1/s of the staged source rows (loaded with a segment's first slab)
+  auto load_tiles = [&](const Tile& ti, int kt, bool first) {
     const __amdgpu_buffer_rsrc_t rW = rsrc(ti.W);
     const int k = kt * BK + lcol;
     const bool kin = k < K;
@@ -193,6 +199,14 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs
       } else {
         off = (mok && kin) ? ((unsigned)m * lda32 + (unsigned)kk) * 4u : OOB;
       }
+      if constexpr (SPL == 4) {
+        if (first) {
+          unsigned ioff;
+          if constexpr (MODE != MODE_DENSE) ioff = (mok && grow[i] >= 0) ? (unsigned)grow[i] * 4u : OOB;
+          else ioff = mok ? (unsigned)m * 4u : OOB;
+          rinv[i] = bload1(rsrc(p.ainv), ioff);
+        }
+      }
       if (VEC) {
         ra[i] = bload4(rA, off);
       } else {
@@ -207,7 +221,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs
 #pragma unroll
     for (int i = 0; i < W_ITERS; ++i) {
       const int n = ti.n0 + lrow + RPP * i;
-      const unsigned off = (n < p.N && kin) ? ((unsigned)n * (SPL == 2 ? ldws32 : ldw32) + (unsigned)k) * 4u : OOB;
+      const unsigned off = (n < p.N && kin) ? ((unsigned)n * (F16 ? ldws32 : ldw32) + (unsigned)k) * 4u : OOB;
       if (VEC) {
         rw[i] = bload4(rW, off);
       } else {
@@ -227,10 +241,32 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs
 #pragma unroll
   for (int i = 0; i < A_ITERS; ++i) { erow[i] = INT_MIN; srow[i] = 1.f; thr[i] = 0.f; }
   int sq = 0, cq = 0;
-  auto store_tiles = [&](int buf, bool first) {
+  int sp = 0;  // segment parity (the s_inv copy of the current segment)
+  // par: parity of the segment whose rows are staged (selects its s_inv copy)
+  auto store_tiles = [&](int buf, bool first, int par) {
     if constexpr (SPLIT) {
       const int b = NBUF == 2 ? buf : 0;
-      if constexpr (SPL == 2) {
+      if constexpr (SPL == 4) {  // both operands pre-split: copy the h / l halves into the term images
+        if (first && (tid & 7) == 0) {
+#pragma unroll
+          for (int i = 0; i < A_ITERS; ++i) s_inv[par * BM + lrow + RPP * i] = rinv[i];
+        }
+#pragma unroll
+        for (int i = 0; i < A_ITERS; ++i) {
+          const uint4 w = __builtin_bit_cast(uint4, ra[i]);
+          const int o = swz(lrow + RPP * i, lcol >> 2);
+          *reinterpret_cast<uint2*>(sAs + ((b * 2 + 0) * BM) * 64 + o) = make_uint2(w.x, w.y);
+          *reinterpret_cast<uint2*>(sAs + ((b * 2 + 1) * BM) * 64 + o) = make_uint2(w.z, w.w);
+        }
+#pragma unroll
+        for (int i = 0; i < W_ITERS; ++i) {
+          const uint4 w = __builtin_bit_cast(uint4, rw[i]);
+          const int o = swz(lrow + RPP * i, lcol >> 2);
+          *reinterpret_cast<uint2*>(sWs + ((b * 2 + 0) * BN) * 64 + o) = make_uint2(w.x, w.y);
+          *reinterpret_cast<uint2*>(sWs + ((b * 2 + 1) * BN) * 64 + o) = make_uint2(w.z, w.w);
+        }
+        return;
+      } else if constexpr (SPL == 2) {
         ++sq;
         float m[A_ITERS];
         bool over = false;
@@ -271,7 +307,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs
             thr[i] = set ? ldexpf(65504.f, -e) : 0.f;
             if ((tid & 7) == 0) {
               s_fac[b * BM + lrow + RPP * i] = fac;
-              if (chg) s_inv[lrow + RPP * i] = set ? ldexpf(1.f, -e) : 1.f;
+              if (chg) s_inv[par * BM + lrow + RPP * i] = set ? ldexpf(1.f, -e) : 1.f;
             }
           }
         } else if ((tid & 7) == 0) {
@@ -363,7 +399,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs
       ebias[b] = bv;
       escale[b] = sv;  // raw loads; the defaults for absent operands are selected in the epilogue, so
       eshift[b] = hv;  // nothing here waits on them
-      if constexpr (SPL == 2) ewinv[b] = bload1(rsrc(ti.winv), off);
+      if constexpr (F16) ewinv[b] = bload1(rsrc(ti.winv), off);
     }
     // output-row remaps (pair mode's pair_out; an out_rows argument of the other modes) are loaded in the
     // epilogue, keeping 16 * MB registers free across the MFMAs
@@ -484,12 +520,12 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs
   };
 
   auto epilogue = [&](const Tile& ti, bool partial, bool owner0) {
-    if constexpr (SPL == 2) {  // undo the row scales of A' and W (powers of two: exact)
+    if constexpr (F16) {  // undo the row scales of A' and W (powers of two: exact)
 #pragma unroll
       for (int a = 0; a < MB; ++a)
 #pragma unroll
         for (int gq = 0; gq < 4; ++gq) {
-          const float4 f = *reinterpret_cast<const float4*>(s_inv + wm * WM + a * 32 + 8 * gq + 4 * h);
+          const float4 f = *reinterpret_cast<const float4*>(s_inv + sp * BM + wm * WM + a * 32 + 8 * gq + 4 * h);
 #pragma unroll
           for (int b = 0; b < NB; ++b) {
             acc[a][b][4 * gq + 0] *= f.x * ewinv[b];
@@ -634,7 +670,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs
   auto compute_split = [&](int buf, int s0, int s1) {
     const int bb = NBUF == 2 ? buf : 0;
     typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
-    typedef typename std::conditional<SPL == 2, f16x8, bf16x8>::type frag_t;
+    typedef typename std::conditional<F16, f16x8, bf16x8>::type frag_t;
 #pragma unroll
     for (int s = s0; s < s1; ++s) {
       frag_t af[MB][NTERM], wf[NB][NTERM];
@@ -654,7 +690,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs
         }
       }
       // smallest terms first; the (a, b) blocks interleave so consecutive MFMAs are independent
-      if constexpr (SPL == 2) {
+      if constexpr (F16) {
         constexpr int QA[3] = {1, 0, 0}, QW[3] = {0, 1, 0};
 #pragma unroll
         for (int j = 0; j < 3; ++j)
@@ -744,8 +780,8 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs
   constexpr bool per_tile_rows = MODE == MODE_GATHER1 || MODE == MODE_PAIR;
   Tile ti = tile_info(t);
   load_rows(ti, kb, grow);
-  load_tiles(ti, kb);
-  store_tiles(0, true);
+  load_tiles(ti, kb, true);
+  store_tiles(0, true, sp);
   __syncthreads();
   int buf = 0;
   while (true) {
@@ -765,11 +801,11 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs
     zero_acc();
     for (int kt = kb; kt + 1 < ke; ++kt) {
       if constexpr (MODE == MODE_GATHERS) load_rows(ti, kt + 1, grow);
-      load_tiles(ti, kt + 1);
+      load_tiles(ti, kt + 1, false);
       __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of the MFMAs it overlaps
       compute(buf);
       if constexpr (NBUF == 1) __syncthreads();  // single LDS buffer: every wave is done reading it
-      store_tiles(buf ^ 1, false);
+      store_tiles(buf ^ 1, false, sp);
       __syncthreads();
       if constexpr (NBUF == 2) buf ^= 1;
     }
@@ -783,16 +819,17 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs
       } else {
         load_rows(tn, 0, grow);
       }
-      load_tiles(tn, 0);
+      load_tiles(tn, 0, true);
     }
     __builtin_amdgcn_sched_barrier(0);
     compute(buf);
     epilogue(ti, kb != 0 || ke != nk, kb == 0);
     if (!has_next) break;
     if constexpr (NBUF == 1) __syncthreads();
-    store_tiles(buf ^ 1, true);
+    store_tiles(buf ^ 1, true, sp ^ 1);
     __syncthreads();
     if constexpr (NBUF == 2) buf ^= 1;
+    sp ^= 1;
     t = nt;
     ti = tn;
     kb = 0;
@@ -854,13 +891,18 @@ void launch(GemmArgs a, int groups, bool vec, hipStream_t st) {
     if (grid_x >= 8) grid_x = (grid_x + 7) / 8 * 8;  // whole XCD groups for the XCD-aware numbering
   }
   dim3 grid(grid_x, 1, groups);
+  constexpr bool PRE_A = MODE != MODE_GATHERS;  // pre-split A exists for single-row-source modes
   if constexpr (NW == 8) {  // split-only tiles (vec operands)
-    if (a.split == 2)
+    if (PRE_A && a.split == 4)
+      gemm_kernel<BM, BN, WGM, 8, true, MODE, PRE_A ? 4 : 2><<<grid, 512, 0, st>>>(a, tiles_n, total);
+    else if (a.split == 2)
       gemm_kernel<BM, BN, WGM, 8, true, MODE, 2><<<grid, 512, 0, st>>>(a, tiles_n, total);
     else
       gemm_kernel<BM, BN, WGM, 8, true, MODE, 3><<<grid, 512, 0, st>>>(a, tiles_n, total);
   } else {
-    if (vec && a.split == 2)
+    if (PRE_A && vec && a.split == 4)
+      gemm_kernel<BM, BN, WGM, 4, true, MODE, PRE_A ? 4 : 2><<<grid, 256, 0, st>>>(a, tiles_n, total);
+    else if (vec && a.split == 2)
       gemm_kernel<BM, BN, WGM, 4, true, MODE, 2><<<grid, 256, 0, st>>>(a, tiles_n, total);
     else if (vec && split)
       gemm_kernel<BM, BN, WGM, 4, true, MODE, 3><<<grid, 256, 0, st>>>(a, tiles_n, total);
@@ -1144,6 +1186,7 @@ void dispatch(const GemmArgs& a0, int groups, bool vec, hipStream_t st) {
   // fp16x2 needs the pre-split W (per-row scales of A' are chosen in the kernel); without one the launch runs the
   // range-safe bf16x3 form.  SFX_GEMM_WS=1 routes fp16x2 launches to the warp-specialised kernel (gemm_ws.hip).
   if (a.split == 2 && !a.Wsp) a.split = 3;
+  if (a.split == 2 && a.Asp && groups == 1 && !(a.gidx && a.S != 1)) a.split = 4;  // A pre-split by the caller
   if (a.split == 2 && launch_ws(a, groups, st)) return;
   if (a.pair_mode)
     dispatch_mode<MODE_PAIR>(a, groups, vec, st);
@@ -1155,6 +1198,106 @@ void dispatch(const GemmArgs& a0, int groups, bool vec, hipStream_t st) {
     launch<64, 128, 2, 4, MODE_GATHERS>(a, groups, vec, st);  // multi-segment gather: test/reference path only
 }
 
+// ---- pre-split A rows (split == 4) -------------------------------------------------------------------------
+// Row r of src (cols floats, row stride ld) -> dst row r in the pre-split layout (every 4 elements: 4 fp16 h
+// terms, then 4 fp16 l terms of x * 2^e_r), inv[r] = 2^-e_r with e_r = row_exp(max |row|) + 2 (the maximum in
+// [2^14, 2^15), like sfx_weight_split).  16 lanes per row, rows up to 512 wide held in registers.
+__global__ void __launch_bounds__(256) split_rows_kernel(int rows, int cols, const float* __restrict__ src,
+                                                         long long ld, float* __restrict__ dst,
+                                                         float* __restrict__ inv) {
+  const int row = (int)blockIdx.x * 16 + (int)(threadIdx.x >> 4);
+  const int l = threadIdx.x & 15;
+  if (row >= rows) return;  // whole 16-lane groups leave together
+  const float* s = src + (long long)row * ld;
+  constexpr int CH = 8;  // float4 chunks per lane kept in registers
+  float4 v[CH];
+  float m = 0.f;
+#pragma unroll
+  for (int j = 0; j < CH; ++j) {
+    const int c = (l + 16 * j) * 4;
+    v[j] = c < cols ? *reinterpret_cast<const float4*>(s + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    m = fmaxf(m, fmaxf(fmaxf(fabsf(v[j].x), fabsf(v[j].y)), fmaxf(fabsf(v[j].z), fabsf(v[j].w))));
+  }
+  for (int c = (l + 16 * CH) * 4; c < cols; c += 64) {
+    const float4 u = *reinterpret_cast<const float4*>(s + c);
+    m = fmaxf(m, fmaxf(fmaxf(fabsf(u.x), fabsf(u.y)), fmaxf(fabsf(u.z), fabsf(u.w))));
+  }
+#pragma unroll
+  for (int o = 8; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 16));
+  int e = 0;
+  if (m > 0.f && m <= 3.4028235e38f) e = row_exp(m) + 2;
+  const float sc = ldexpf(1.f, e);
+  uint4* d = reinterpret_cast<uint4*>(dst + (long long)row * cols);
+#pragma unroll
+  for (int j = 0; j < CH; ++j) {
+    const int c = (l + 16 * j) * 4;
+    if (c < cols) {
+      uint2 t[2];
+      split2h(v[j], sc, t);
+      d[c / 4] = make_uint4(t[0].x, t[0].y, t[1].x, t[1].y);
+    }
+  }
+  for (int c = (l + 16 * CH) * 4; c < cols; c += 64) {
+    uint2 t[2];
+    split2h(*reinterpret_cast<const float4*>(s + c), sc, t);
+    d[c / 4] = make_uint4(t[0].x, t[0].y, t[1].x, t[1].y);
+  }
+  if (l == 0) inv[row] = ldexpf(1.f, -e);
+}
+
+// A-split scratch: one grow-only buffer per (device, stream); a stream's launches are ordered, so each split
+// overwrites rows its previous GEMM has finished reading.  SFX_GEMM_ASPLIT=0 keeps the in-kernel split.
+bool asplit_enabled() {
+  static int on = -1;
+  if (on < 0) {
+    const char* e = getenv("SFX_GEMM_ASPLIT");
+    on = (e && *e) ? (atoi(e) != 0) : 0;
+  }
+  return on == 1;
+}
+
+float* asplit_scratch(size_t floats, hipStream_t st) {
+  struct Slot { int dev; hipStream_t st; float* p; size_t cap; };
+  static Slot slots[32] = {};
+  static int used = 0;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  Slot* s = nullptr;
+  for (int i = 0; i < used; ++i)
+    if (slots[i].dev == dev && slots[i].st == st) s = &slots[i];
+  if (!s) {
+    if (used == 32) return nullptr;
+    s = &slots[used++];
+    *s = Slot{dev, st, nullptr, 0};
+  }
+  if (s->cap < floats) {
+    if (s->p) {
+      (void)hipStreamSynchronize(st);
+      (void)hipFree(s->p);
+      s->p = nullptr;
+      s->cap = 0;
+    }
+    const size_t want = floats + floats / 4;  // headroom: stage sizes vary per scene
+    if (hipMalloc(&s->p, want * sizeof(float)) != hipSuccess) return nullptr;
+    s->cap = want;
+  }
+  return s->p;
+}
+
+// Pre-split the `rows` source rows of a fp16x2 launch's A (a.A, a.lda, a.K columns) so the GEMM only copies term
+// images (split == 4).  No-op (the kernel then splits in place) when disabled, ineligible or out of scratch.
+void presplit_a(GemmArgs& a, long long rows, bool vec, hipStream_t st) {
+  if (!asplit_enabled() || !vec || !a.Wsp || rows <= 0 || split_mode(a.K) != 2) return;
+  const long long kp = (a.K + 3) / 4 * 4;
+  if (!fits(rows, kp)) return;
+  float* buf = asplit_scratch((size_t)(rows * kp + rows + 64), st);
+  if (!buf) return;
+  float* inv = buf + rows * kp;
+  split_rows_kernel<<<(unsigned)sfx::ceil_div(rows, 16), 256, 0, st>>>((int)rows, a.K, a.A, a.lda, buf, inv);
+  a.Asp = buf;
+  a.ldas = kp;
+  a.ainv = inv;
+}
 
 // ---- weight gradient: dW[N, K] += dY[M, N]^T X[M, K] (reduction over the point rows) ----------------
 // Output tiles are few (N x K of one layer), the reduction long (M = 10^4..10^5 rows): the M range is
@@ -1326,6 +1469,7 @@ int sfx_linear(int M, int N, int K, const float* A, long long lda, const int* ga
     SFX_REQUIRE(groups == 1 || group_stride_W == (long long)N * K, "sfx_linear: w_split needs contiguous groups");
     a.Wsp = w_split; a.ldws = K; a.winv = w_inv; a.gWinv = N;
   }
+  if (!gather_idx && groups == 1) presplit_a(a, M, vec, sfx::as_stream(stream));
   dispatch(a, groups, vec, sfx::as_stream(stream));
   return sfx::check_launch("sfx_linear");
 }
@@ -1368,6 +1512,7 @@ int sfx_subm_conv(int n, int cin, int cout, const float* x, long long ldx, const
                     AmaxJob{weight, 27ll * cin, 0, cout, 27 * cin, 1, nullptr, 0, 1}, st)) {
     a.a_amax = a.w_amax = nullptr;  // (dispatch falls back to bf16x3 for the pair launch)
   }
+  presplit_a(a, n, vec, st);  // x once, for the centre and the pair launch
   dispatch(a, 1, vec, st);
   int rc = sfx::check_launch("sfx_subm_conv(centre)");
   if (rc) return rc;

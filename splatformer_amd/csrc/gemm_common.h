@@ -93,7 +93,19 @@ struct GemmArgs {
   long long slice_winv_stride;  // pair mode: winv offset per slice (row-sliced weights, e.g. the conv backward)
   int epi_vec;  // epilogue operands allow 16-byte accesses (set by launch_ws)
   int tuned, tuned_sk;  // measured tile configuration + 1 (0: cost model / table) and its Stream-K flag
+  // pre-split A (split == 4): the source rows of A in the Wsp layout (row stride ldas, 4-byte units), ainv[r] =
+  // 1/s of source row r (the row A is gathered from: dense m, gidx[m], pair_in[m])
+  const float* Asp;
+  long long ldas;
+  const float* ainv;
 };
+
+// fp16x2 row exponent: a row with maximum m is scaled by 2^e so that m * 2^e lies in [2^12, 2^13)
+__device__ __forceinline__ int row_exp(float m) {
+  int e = __builtin_amdgcn_frexp_expf(m);  // m in [2^(e-1), 2^e)
+  e = 13 - e;
+  return e > 126 ? 126 : (e < -126 ? -126 : e);
+}
 
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
 // d/dx of the erf GELU (torch GeluBackward, approximate='none')

@@ -104,12 +104,7 @@ __device__ __forceinline__ float max8(float m) {
   return m;
 }
 
-// exponent E with m * 2^E in [2^12, 2^13) (m finite, > 0), clamped to the normal range
-__device__ __forceinline__ int row_exp(float m) {
-  int e = __builtin_amdgcn_frexp_expf(m);  // m in [2^(e-1), 2^e)
-  e = 13 - e;
-  return e > 126 ? 126 : (e < -126 ? -126 : e);
-}
+// (row_exp: the row exponent, gemm_common.h)
 
 // LDS map (one __shared__ array: a second LDS object can make hipcc wait vmcnt(0) before ds_reads):
 //   [NS] stages of { A terms h, l: [BM][64 B] swizzled; W terms h, l: [BN][64 B] }
