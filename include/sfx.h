@@ -234,6 +234,13 @@ int sfx_layernorm(int M, int C, const float* X, long long ldx, const float* gamm
 /* Block tail of cpe + shortcut + norm1: X_out = X + LN_cpe(T); H = LN1(X_out)  (X_out may alias X) */
 int sfx_cpe_residual_ln(int M, int C, const float* T, const float* X, const float* gamma_cpe, const float* beta_cpe,
                         const float* gamma1, const float* beta1, float eps, float* X_out, float* H, void* stream);
+/* (ABI v6) the same with T = the centre output of sfx_subm_conv_partials plus, per row, the SubM pair partials
+ * partials[pair_pos[row][k]] summed in ascending offset order k (pair_pos: sfx_subm_pair_pos; -1 entries skipped):
+ * the conv without float atomics, bitwise reproducible.  C in {64, 96, 128, 256, 512}, 16-byte aligned rows. */
+int sfx_cpe_residual_ln_pairs(int M, int C, const float* T, const float* partials, const int* pair_pos,
+                              long long num_pairs, const float* X, const float* gamma_cpe, const float* beta_cpe,
+                              const float* gamma1, const float* beta1, float eps, float* X_out, float* H,
+                              void* stream);
 
 /* SerializedAttention (non-flash): windows win[w] = (key_start, query_start) over serialized positions,
  * qkv [N,3C] in point order, order [N] serialized->point; out[order[p]] for every query position p. */
@@ -287,6 +294,10 @@ int sfx_subm_permute(int n, const int* perm, const int* nbr, const unsigned* mas
 size_t sfx_subm_pairs_workspace_bytes(int n);
 int sfx_subm_pairs(int n, const int* nbr, void* ws, size_t ws_bytes, int* pair_in, int* pair_out, int* pair_off,
                    void* stream);
+/* (ABI v6) inverted pair index: pair_pos[i][k] = index of pair (k, out = i) in pair_in/pair_out, -1 if none
+ * (always -1 for the centre k = 13); pair_off = the device pair_off of sfx_subm_pairs, num_pairs = pair_off[27]. */
+int sfx_subm_pair_pos(int n, long long num_pairs, const int* pair_out, const int* pair_off, int* pair_pos,
+                      void* stream);
 /* spconv SubMConv3d(Cin, Cout, 3, bias) forward on the pair lists: out = bias + x[nbr[:,13]] W_13^T (dense centre
  * GEMM, plain stores), then one fp32 MFMA launch over the 26 other offsets' gathered rows whose partial products
  * are atomically added into out (float atomics: summation order across offsets is not fixed).
@@ -296,6 +307,13 @@ int sfx_subm_conv(int n, int cin, int cout, const float* x, long long ldx, const
                   long long ldo, const unsigned long long* x_amax, unsigned x_tag,
                   const unsigned long long* w_amax, unsigned w_tag, const float* w_split, const float* w_inv,
                   void* stream);
+/* (ABI v6) atomic-free form: out = bias + the centre offset's product; the 26 other offsets' products are stored
+ * as rows of partials [pair_off[27]][ldp] (row = pair index) for sfx_cpe_residual_ln_pairs to sum per output row
+ * in a fixed offset order. */
+int sfx_subm_conv_partials(int n, int cin, int cout, const float* x, long long ldx, const int* nbr,
+                           const float* weight, const float* bias, const int* pair_in, const int* pair_out,
+                           const int* pair_off_host, float* out, long long ldo, float* partials, long long ldp,
+                           const float* w_split, const float* w_inv, void* stream);
 
 /* FeaturePredictor batchify (feature_predictor.py:134-156): strided attribute rows -> feat rows
  * [means,scales,opacities,quats,dc,rest], grid_coord = floor(means*res), optional atomic grid max. */

@@ -541,8 +541,12 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs
         return;
       }
     }
-    if constexpr (MODE == MODE_PAIR) {  // partial sums of one neighbour offset: accumulate into the output rows
+    if constexpr (MODE == MODE_PAIR) {
+      // partial sums of one neighbour offset: accumulated into the output rows (float atomics), or, with
+      // pair_store, stored as row `pair index` of a partials matrix that the consumer sums per output row in a
+      // fixed offset order (sfx_cpe_residual_ln_pairs: no atomics, bitwise reproducible)
       const __amdgpu_buffer_rsrc_t rO = rsrc(ti.out_rows);
+      const int pbase = (int)(ti.out_rows - p.pair_out);
 #pragma unroll
       for (int a = 0; a < MB; ++a) {
         int orow[16];
@@ -551,12 +555,18 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs
         for (int r = 0; r < 16; ++r) {
           const int mt = ti.m0 + wm * WM + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
           ok[r] = mt < ti.M;
-          orow[r] = bload1i(rO, ok[r] ? (unsigned)mt * 4u : OOB);
+          orow[r] = p.pair_store ? pbase + mt : bload1i(rO, ok[r] ? (unsigned)mt * 4u : OOB);
         }
 #pragma unroll
         for (int b = 0; b < NB; ++b) {
           const int n = ti.n0 + wn * WN + b * 32 + l32;
           const bool nok = n < p.N;
+          if (p.pair_store) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+              bstore1(rY, (nok && ok[r]) ? ((unsigned)orow[r] * ldy32 + (unsigned)n) * 4u : OOB, acc[a][b][r]);
+            continue;
+          }
 #pragma unroll
           for (int r = 0; r < 16; ++r)
             __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(
@@ -1115,6 +1125,7 @@ int pick_cfg(GemmArgs& a, int groups, bool vec) {
   // Stream-K needs a linear epilogue that can be split into atomically added pieces
   // (measured: the memset + atomic partial epilogues only pay off on long K; pair mode needs no memset)
   const bool sk_ok = groups == 1 && nk >= (a.pair_mode ? 8 : 16) && a.act == ACT_NONE && !a.Ypre && !a.out_rows &&
+                     !a.pair_store &&
                      !a.y_amax &&
                      !(a.R && a.R == a.Y) && a.M > 0 && forced_sk != 0;
   const double sk_overhead = a.pair_mode ? 2.5 : 4.0;  // slab-equivalents: partial epilogues (+ memset)
@@ -1476,19 +1487,21 @@ int sfx_linear(int M, int N, int K, const float* A, long long lda, const int* ga
 
 // SubMConv3d, offset-major sparse form.  out = bias + x[nbr[:,13]] W_13^T (dense centre launch, plain
 // stores), then one launch over the 26 other offsets' pair lists (pairs from sfx_subm_pairs) whose
-// partial products are atomically added.  weight: [Cout, 27, Cin] (spconv [Cout,3,3,3,Cin]).
+// partial products are atomically added (or, with `partials`, stored per pair).  weight: [Cout, 27, Cin] (spconv [Cout,3,3,3,Cin]).
 // pair_off_host: 28 host ints (prefix of pair counts per offset, centre slice empty).
-int sfx_subm_conv(int n, int cin, int cout, const float* x, long long ldx, const int* nbr, const float* weight,
-                  const float* bias, const int* pair_in, const int* pair_out, const int* pair_off_host, float* out,
-                  long long ldo, const unsigned long long* x_amax, unsigned x_tag,
-                  const unsigned long long* w_amax, unsigned w_tag, const float* w_split, const float* w_inv,
-                  void* stream) {
+static int subm_conv_impl(int n, int cin, int cout, const float* x, long long ldx, const int* nbr,
+                          const float* weight, const float* bias, const int* pair_in, const int* pair_out,
+                          const int* pair_off_host, float* out, long long ldo, const unsigned long long* x_amax,
+                          unsigned x_tag, const unsigned long long* w_amax, unsigned w_tag, const float* w_split,
+                          const float* w_inv, float* partials, long long ldp, void* stream) {
   SFX_REQUIRE(n >= 0 && cin > 0 && cout > 0, "sfx_subm_conv: bad sizes");
   if (n == 0) return SFX_OK;
   SFX_REQUIRE(x && nbr && weight && out && pair_off_host, "sfx_subm_conv: null buffer");
   SFX_REQUIRE(ldx >= cin && ldo >= cout, "sfx_subm_conv: leading dimension too small");
   SFX_REQUIRE(fits(n, ldx) && fits(n, ldo) && fits(cout, 27ll * cin),
               "sfx_subm_conv: operand exceeds the 2 GiB buffer-descriptor range");
+  SFX_REQUIRE(!partials || (ldp >= cout && fits(pair_off_host[27], ldp)),
+              "sfx_subm_conv_partials: partials leading dimension too small or too large");
   hipStream_t st = sfx::as_stream(stream);
   const bool vec = (cin % 4 == 0) && (ldx % 4 == 0) && aligned16(x) && aligned16(weight);
   // 1) centre offset: dense gathered GEMM with bias, plain stores
@@ -1524,8 +1537,35 @@ int sfx_subm_conv(int n, int cin, int cout, const float* x, long long ldx, const
   if (a.Wsp) b.Wsp = w_split;
   for (int k = 0; k <= 27; ++k) b.slice_pair_off[k] = pair_off_host[k];
   b.M = pair_off_host[27];
+  if (partials) {
+    b.pair_store = 1;
+    b.Y = partials;
+    b.ldy = ldp;
+  }
   dispatch(b, 1, vec, st);
   return sfx::check_launch("sfx_subm_conv(pairs)");
+}
+
+int sfx_subm_conv(int n, int cin, int cout, const float* x, long long ldx, const int* nbr, const float* weight,
+                  const float* bias, const int* pair_in, const int* pair_out, const int* pair_off_host, float* out,
+                  long long ldo, const unsigned long long* x_amax, unsigned x_tag,
+                  const unsigned long long* w_amax, unsigned w_tag, const float* w_split, const float* w_inv,
+                  void* stream) {
+  return subm_conv_impl(n, cin, cout, x, ldx, nbr, weight, bias, pair_in, pair_out, pair_off_host, out, ldo, x_amax,
+                        x_tag, w_amax, w_tag, w_split, w_inv, nullptr, 0, stream);
+}
+
+// Atomic-free form: out = bias + the centre offset's product (plain stores); the 26 other offsets' products are
+// stored as rows of `partials` ([num_pairs][ldp], row = pair index in the sfx_subm_pairs lists) for a consumer that
+// sums them per output row (sfx_cpe_residual_ln_pairs / sfx_pair_reduce).
+int sfx_subm_conv_partials(int n, int cin, int cout, const float* x, long long ldx, const int* nbr,
+                           const float* weight, const float* bias, const int* pair_in, const int* pair_out,
+                           const int* pair_off_host, float* out, long long ldo, float* partials, long long ldp,
+                           const float* w_split, const float* w_inv, void* stream) {
+  SFX_REQUIRE(n == 0 || pair_off_host[27] == 0 || (partials && pair_in && pair_out),
+              "sfx_subm_conv_partials: null partials / pair lists");
+  return subm_conv_impl(n, cin, cout, x, ldx, nbr, weight, bias, pair_in, pair_out, pair_off_host, out, ldo, nullptr,
+                        0, nullptr, 0, w_split, w_inv, partials, ldp, stream);
 }
 
 // SubMConv3d backward w.r.t. its input: dX[in] += dY[out] W_k for every pair (in, out, k), centre included.

@@ -98,6 +98,7 @@ struct GemmArgs {
   const float* Asp;
   long long ldas;
   const float* ainv;
+  int pair_store;  // pair mode: store each pair's row at row `pair index` of Y instead of adding into pair_out
 };
 
 // fp16x2 row exponent: a row with maximum m is scaled by 2^e so that m * 2^e lies in [2^12, 2^13)

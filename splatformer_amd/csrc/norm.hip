@@ -143,14 +143,39 @@ __global__ void __launch_bounds__(256) layernorm4_kernel(int M, const float* __r
   for (int i = 0; i < NV; ++i) *reinterpret_cast<float4*>(Y + (long long)row * ldy + 4 * (sub + G * i)) = o[i];
 }
 
+// t += the row's SubM pair partials (sfx_subm_conv_partials), offsets in ascending order: the conv output
+// without float atomics, identical from run to run.  Absent pairs read through an out-of-range buffer offset (0).
 template <int G, int NV>
+__device__ __forceinline__ void add_pair_partials(float4 (&v)[NV], const float* __restrict__ P,
+                                                  const int* __restrict__ pos, int row, int sub) {
+  constexpr int C = 4 * G * NV;
+  const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(P), (short)0, 0x7ffffff0,
+                                                                      0x00020000);
+  int q[27];
+#pragma unroll
+  for (int k = 0; k < 27; ++k) q[k] = pos[27ll * row + k];
+#pragma unroll
+  for (int k = 0; k < 27; ++k) {
+    if (k == 13) continue;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const unsigned off = q[k] >= 0 ? ((unsigned)q[k] * (unsigned)C + 4u * (unsigned)(sub + G * i)) * 4u : 0x7ffffff0u;
+      const float4 a = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rp, off, 0, 0));
+      v[i] = make_float4(v[i].x + a.x, v[i].y + a.y, v[i].z + a.z, v[i].w + a.w);
+    }
+  }
+}
+
+template <int G, int NV, bool PAIRS>
 __global__ void __launch_bounds__(256) cpe_residual_ln4_kernel(int M, const float* __restrict__ T,
                                                                const float* __restrict__ X,
                                                                const float* __restrict__ g_cpe,
                                                                const float* __restrict__ b_cpe,
                                                                const float* __restrict__ g1,
                                                                const float* __restrict__ b1, float eps,
-                                                               float* __restrict__ Xout, float* __restrict__ H) {
+                                                               float* __restrict__ Xout, float* __restrict__ H,
+                                                               const float* __restrict__ P,
+                                                               const int* __restrict__ pos) {
   constexpr int C = 4 * G * NV;
   const int row = blockIdx.x * (256 / G) + threadIdx.x / G;
   const int sub = threadIdx.x % G;
@@ -162,6 +187,7 @@ __global__ void __launch_bounds__(256) cpe_residual_ln4_kernel(int M, const floa
     v[i] = *reinterpret_cast<const float4*>(T + base + 4 * (sub + G * i));
     x[i] = *reinterpret_cast<const float4*>(X + base + 4 * (sub + G * i));
   }
+  if constexpr (PAIRS) add_pair_partials<G, NV>(v, P, pos, row, sub);
   ln_row4<G, NV>(v, g_cpe, b_cpe, eps, sub, o);
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
@@ -228,9 +254,10 @@ int sfx_cpe_residual_ln(int M, int C, const float* T, const float* X, const floa
   hipStream_t st = sfx::as_stream(stream);
   const bool v4 = al16(T) && al16(X) && al16(X_out) && al16(H) && al16(gamma_cpe) && al16(beta_cpe) && al16(gamma1) &&
                   al16(beta1);
-#define SFX_CPE4(G, NV)                                                                                    \
-  cpe_residual_ln4_kernel<G, NV><<<sfx::ceil_div(M, 256 / G), 256, 0, st>>>(M, T, X, gamma_cpe, beta_cpe, gamma1, \
-                                                                            beta1, eps, X_out, H)
+#define SFX_CPE4(G, NV)                                                                                         \
+  cpe_residual_ln4_kernel<G, NV, false><<<sfx::ceil_div(M, 256 / G), 256, 0, st>>>(M, T, X, gamma_cpe, beta_cpe,   \
+                                                                                   gamma1, beta1, eps, X_out, H,   \
+                                                                                   nullptr, nullptr)
   if (v4 && C == 64) SFX_CPE4(16, 1);
   else if (v4 && C == 96) SFX_CPE4(8, 3);
   else if (v4 && C == 128) SFX_CPE4(32, 1);
@@ -240,6 +267,36 @@ int sfx_cpe_residual_ln(int M, int C, const float* T, const float* X, const floa
                                                                    X_out, H);
 #undef SFX_CPE4
   return sfx::check_launch("sfx_cpe_residual_ln");
+}
+
+// sfx_cpe_residual_ln with T = the centre output of sfx_subm_conv_partials and the pair partials summed per row
+// in ascending offset order (pair_pos: sfx_subm_pair_pos; partials: [num_pairs][C], contiguous).
+int sfx_cpe_residual_ln_pairs(int M, int C, const float* T, const float* partials, const int* pair_pos,
+                              long long num_pairs, const float* X, const float* gamma_cpe, const float* beta_cpe,
+                              const float* gamma1, const float* beta1, float eps, float* X_out, float* H,
+                              void* stream) {
+  SFX_REQUIRE(M >= 0 && num_pairs >= 0, "sfx_cpe_residual_ln_pairs: bad sizes");
+  if (M == 0) return SFX_OK;
+  SFX_REQUIRE(T && X && gamma_cpe && beta_cpe && gamma1 && beta1 && X_out && H && pair_pos &&
+                  (num_pairs == 0 || partials),
+              "sfx_cpe_residual_ln_pairs: null buffer");
+  SFX_REQUIRE(num_pairs * C * 4 + 64 < 0x7ffffff0ll, "sfx_cpe_residual_ln_pairs: partials exceed 2 GiB");
+  const bool v4 = al16(T) && al16(X) && al16(X_out) && al16(H) && al16(gamma_cpe) && al16(beta_cpe) && al16(gamma1) &&
+                  al16(beta1) && (!partials || al16(partials));
+  SFX_REQUIRE(v4 && (C == 64 || C == 96 || C == 128 || C == 256 || C == 512),
+              "sfx_cpe_residual_ln_pairs: needs 16-byte aligned rows and C in {64, 96, 128, 256, 512}");
+  hipStream_t st = sfx::as_stream(stream);
+#define SFX_CPE4P(G, NV)                                                                                        \
+  cpe_residual_ln4_kernel<G, NV, true><<<sfx::ceil_div(M, 256 / G), 256, 0, st>>>(M, T, X, gamma_cpe, beta_cpe,   \
+                                                                                  gamma1, beta1, eps, X_out, H,   \
+                                                                                  partials, pair_pos)
+  if (C == 64) SFX_CPE4P(16, 1);
+  else if (C == 96) SFX_CPE4P(8, 3);
+  else if (C == 128) SFX_CPE4P(32, 1);
+  else if (C == 256) SFX_CPE4P(64, 1);
+  else SFX_CPE4P(64, 2);
+#undef SFX_CPE4P
+  return sfx::check_launch("sfx_cpe_residual_ln_pairs");
 }
 
 }  // extern "C"

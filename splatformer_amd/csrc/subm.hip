@@ -109,6 +109,18 @@ __global__ void subm_pair_fill_kernel(int n, const int* __restrict__ nbr, const 
   }
 }
 
+// inverted pair index: pair_pos[out][k] = index of pair (k, out) in the flat lists (-1: none; centre -1)
+__global__ void subm_pair_pos_kernel(long long num_pairs, const int* __restrict__ pair_out,
+                                     const int* __restrict__ pair_off, int* __restrict__ pair_pos) {
+  const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= num_pairs) return;
+  int k = 0;
+#pragma unroll 1
+  for (int q = 1; q < 27; ++q)
+    if (pair_off[q] <= p) k = q;
+  pair_pos[27ll * pair_out[p] + k] = (int)p;
+}
+
 }  // namespace
 
 extern "C" int sfx_scan_i32(long long n, const int32_t* in, int32_t* out, int inclusive, void* ws, size_t ws_bytes,
@@ -170,6 +182,20 @@ int sfx_subm_pairs(int n, const int* nbr, void* ws, size_t ws_bytes, int* pair_i
   if (rc) return rc;
   subm_pair_fill_kernel<<<sfx::ceil_div(e, 256), 256, 0, st>>>(n, nbr, flags, pos, pair_in, pair_out, pair_off);
   return sfx::check_launch("sfx_subm_pairs");
+}
+
+// pair_pos [n][27]: for output row i and offset k, the index of pair (k, i) in pair_in/pair_out (-1: no pair);
+// pair_off (device, 28 ints) as written by sfx_subm_pairs, num_pairs = pair_off[27]
+int sfx_subm_pair_pos(int n, long long num_pairs, const int* pair_out, const int* pair_off, int* pair_pos,
+                      void* stream) {
+  SFX_REQUIRE(n >= 0 && num_pairs >= 0 && num_pairs <= 26ll * n, "sfx_subm_pair_pos: bad sizes");
+  if (n == 0) return SFX_OK;
+  SFX_REQUIRE(pair_pos && (num_pairs == 0 || (pair_out && pair_off)), "sfx_subm_pair_pos: null buffer");
+  hipStream_t st = sfx::as_stream(stream);
+  hipMemsetAsync(pair_pos, 0xff, 27ll * n * sizeof(int), st);
+  if (num_pairs > 0)
+    subm_pair_pos_kernel<<<sfx::ceil_div(num_pairs, 256), 256, 0, st>>>(num_pairs, pair_out, pair_off, pair_pos);
+  return sfx::check_launch("sfx_subm_pair_pos");
 }
 
 int sfx_subm_permute(int n, const int* perm, const int* nbr, const unsigned* mask, int* nbr_sorted,

@@ -130,7 +130,9 @@ class Block(nn.Module):
         wf, bf = self.cpe_fused()
         # The GEMMs scale their fp16x2 operands per row themselves (no operand bounds needed); the qkv GEMM
         # publishes max |qkv| for the attention's fp16x2 q / k / v terms (ptv3_ops.new_amax)
-        t = ops.subm_conv(x if conv_in is None else conv_in, point.nbr, wf, bf)
+        # the conv's pair products go to per-pair rows that the LN kernel sums in a fixed order (no float atomics,
+        # reproducible); SFX_SUBM_ATOMIC=1 restores the atomic accumulation
+        t = ops.subm_conv(x if conv_in is None else conv_in, point.nbr, wf, bf, partials=ops.SUBM_PARTIALS)
         ln1 = self.norm1[0]
         x1, h = ops.cpe_residual_ln(t, x, ln_c.weight, ln_c.bias, ln1.weight, ln1.bias, ln1.eps)
         qkv, q_amax = ops.linear(h, self.attn.qkv.weight, self.attn.qkv.bias, y_amax=True)

@@ -6,6 +6,7 @@ fallback: a missing library or a CPU tensor raises.
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -22,6 +23,7 @@ _lib.register("sfx_amax_f32", [I, I, P, L, P, I, P])
 _lib.register("sfx_ln_amax_bound", [I, P, P, P, I, P])
 _lib.register("sfx_layernorm", [I, I, P, L, P, P, F, P, L, P])
 _lib.register("sfx_cpe_residual_ln", [I, I, P, P, P, P, P, P, F, P, P, P])
+_lib.register("sfx_cpe_residual_ln_pairs", [I, I, P, P, P, L, P, P, P, P, P, F, P, P, P])
 _lib.register("sfx_window_attention", [I, I, I, I, I, P, P, P, F, P, P, I, P])
 _lib.register("sfx_serialize_keys", [I, P, P, I, I, I, I, I, I, I, P, P, P])
 _lib.register("sfx_serialize_finalize", [I, I, P, P, P, P])
@@ -37,6 +39,8 @@ _lib.register("sfx_subm_permute", [I, P, P, P, P, P, P])
 _lib.register("sfx_subm_pairs_workspace_bytes", [I], Z)
 _lib.register("sfx_subm_pairs", [I, P, P, Z, P, P, P, P])
 _lib.register("sfx_subm_conv", [I, I, I, P, L, P, P, P, P, P, P, P, L, P, I, P, I, P, P, P])
+_lib.register("sfx_subm_conv_partials", [I, I, I, P, L, P, P, P, P, P, P, P, L, P, L, P, P, P])
+_lib.register("sfx_subm_pair_pos", [I, L, P, P, P, P])
 _lib.register("sfx_gs_pack", [I, P, L, P, L, P, L, P, L, P, L, P, L, I, F, P, L, P, P, P])
 _lib.register("sfx_offsets_to_batch", [I, I, P, P, P])
 _lib.register("sfx_gemm_force_config", [I, I])
@@ -217,14 +221,20 @@ def layernorm(x: Tensor, gamma: Tensor, beta: Tensor, eps: float, out: Optional[
     return out
 
 
-def cpe_residual_ln(t: Tensor, x: Tensor, g_cpe: Tensor, b_cpe: Tensor, g1: Tensor, b1: Tensor, eps: float,
+def cpe_residual_ln(t, x: Tensor, g_cpe: Tensor, b_cpe: Tensor, g1: Tensor, b1: Tensor, eps: float,
                     x_out: Optional[Tensor] = None) -> Tuple[Tensor, Tensor]:
-    """x' = x + LN_cpe(t); h = LN_norm1(x')  (Block cpe tail + shortcut + norm1)."""
+    """x' = x + LN_cpe(t); h = LN_norm1(x')  (Block cpe tail + shortcut + norm1).  t is the conv output, or a
+    `SubmPartials` (subm_conv(..., partials=True)): the centre output plus the pair partials, summed here per row in
+    a fixed offset order."""
     M, C = x.shape
     x_out = torch.empty_like(x) if x_out is None else x_out
     h = torch.empty_like(x)
-    call("sfx_cpe_residual_ln", M, C, ptr(t), ptr(x), ptr(g_cpe), ptr(b_cpe), ptr(g1), ptr(b1), float(eps),
-         ptr(x_out), ptr(h), stream())
+    if isinstance(t, SubmPartials):
+        call("sfx_cpe_residual_ln_pairs", M, C, ptr(t.centre), ptr(t.partials), ptr(t.pair_pos), t.num_pairs, ptr(x),
+             ptr(g_cpe), ptr(b_cpe), ptr(g1), ptr(b1), float(eps), ptr(x_out), ptr(h), stream())
+    else:
+        call("sfx_cpe_residual_ln", M, C, ptr(t), ptr(x), ptr(g_cpe), ptr(b_cpe), ptr(g1), ptr(b1), float(eps),
+             ptr(x_out), ptr(h), stream())
     return x_out, h
 
 
@@ -383,11 +393,27 @@ class SubmMap:
     """Per-stage SubMConv3d indice map (indice_key=stage{s}): nbr [n,27] + offset-major pair lists.  The 28 pair
     offsets reach the host asynchronously; the first conv that needs them waits for that copy only."""
 
-    def __init__(self, nbr: Tensor, mask: Tensor, pair_in: Tensor, pair_out: Tensor, pair_off):
+    def __init__(self, nbr: Tensor, mask: Tensor, pair_in: Tensor, pair_out: Tensor, pair_off,
+                 pair_off_dev: Optional[Tensor] = None):
         self.nbr, self.mask, self.pair_in, self.pair_out = nbr, mask, pair_in, pair_out
         self._off_src = pair_off  # list or _lib.HostRead
         self._off = None
         self._off_c = None
+        self._off_dev = pair_off_dev
+        self._pos = None
+
+    @property
+    def pair_pos(self) -> Tensor:
+        """[n, 27] inverted pair index (sfx_subm_pair_pos), built once per map."""
+        if self._pos is None:
+            n = self.nbr.shape[0]
+            off_dev = self._off_dev
+            if off_dev is None:
+                off_dev = torch.tensor(self.pair_off, dtype=torch.int32, device=self.nbr.device)
+            pos = torch.empty(n, 27, device=self.nbr.device, dtype=torch.int32)
+            call("sfx_subm_pair_pos", n, self.num_pairs, ptr(self.pair_out), ptr(off_dev), ptr(pos), stream())
+            self._pos = pos
+        return self._pos
 
     @property
     def pair_off(self) -> List[int]:
@@ -430,20 +456,50 @@ def subm_neighbors(grid_coord: Tensor, batch: Optional[Tensor], with_pairs: bool
     poff = torch.empty(28, device=dev, dtype=torch.int32)
     ws = _lib.workspace(_lib.fn("sfx_subm_pairs_workspace_bytes")(n), dev)
     call("sfx_subm_pairs", n, ptr(nbr), ptr(ws), ws.numel(), ptr(pin), ptr(pout), ptr(poff), stream())
-    return SubmMap(nbr, mask, pin, pout, _lib.HostRead(poff))
+    return SubmMap(nbr, mask, pin, pout, _lib.HostRead(poff), poff)
+
+
+# eval-path SubM convs: store per-pair partials and sum them in the consumer (default), or add them atomically
+SUBM_PARTIALS = os.environ.get("SFX_SUBM_ATOMIC", "0") != "1"
+
+
+class SubmPartials:
+    """Atomic-free SubM conv output: centre [n, Cout] (bias + centre offset) and partials [num_pairs, Cout] (one row
+    per (offset, output) pair), summed per output row by the consumer (cpe_residual_ln) or by `total()`."""
+
+    def __init__(self, centre: Tensor, partials: Tensor, pair_pos: Tensor, num_pairs: int):
+        self.centre, self.partials, self.pair_pos, self.num_pairs = centre, partials, pair_pos, num_pairs
+
+    def total(self) -> Tensor:
+        """The conv output, summed in the consumer's order (ascending offsets after the centre)."""
+        out = self.centre.clone()
+        pos = self.pair_pos.long()
+        for k in range(27):
+            sel = pos[:, k] >= 0
+            if k != 13 and bool(sel.any()):
+                out[sel] += self.partials[pos[sel, k]]
+        return out
 
 
 def subm_conv(x: Tensor, smap: "SubmMap", weight: Tensor, bias: Optional[Tensor],
               out: Optional[Tensor] = None, x_amax: Optional[Tuple[int, int]] = None,
-              w_amax: Optional[Tuple[int, int]] = None) -> Tensor:
+              w_amax: Optional[Tuple[int, int]] = None, partials: bool = False):
     """SubMConv3d(k=3): dense centre GEMM + offset-major pair GEMM with atomic accumulation (x_amax / w_amax:
-    amax slots bounding |x| and the whole weight; None: measured by the library)."""
+    amax slots bounding |x| and the whole weight; None: measured by the library).  partials=True: the pair
+    products are stored per pair instead (no atomics) and a SubmPartials is returned for cpe_residual_ln."""
     n, cin = x.shape
     cout = weight.shape[0]
     if out is None:
         out = torch.empty(n, cout, device=x.device, dtype=torch.float32)
     px, ldx = _rows(x)
     po, ldo = _rows(out)
+    if partials:
+        npairs = smap.num_pairs
+        part = torch.empty(max(1, npairs), cout, device=x.device, dtype=torch.float32)
+        call("sfx_subm_conv_partials", n, cin, cout, px, ldx, ptr(smap.nbr), ptr(weight), ptr(bias),
+             ptr(smap.pair_in), ptr(smap.pair_out), smap._off_host, po, ldo, ptr(part), cout, *weight_split(weight),
+             stream())
+        return SubmPartials(out, part, smap.pair_pos, npairs)
     call("sfx_subm_conv", n, cin, cout, px, ldx, ptr(smap.nbr), ptr(weight), ptr(bias), ptr(smap.pair_in),
          ptr(smap.pair_out), smap._off_host, po, ldo, *_slot_args(x_amax), *_slot_args(w_amax),
          *weight_split(weight), stream())

@@ -111,6 +111,45 @@ def test_linear_gather_is_subm_conv(device):
         assert rel_l2(y2.cpu(), ref2) < 2e-6
 
 
+def test_subm_conv_partials_atomic_free(device):
+    """Atomic-free SubM conv (sfx_subm_conv_partials + sfx_subm_pair_pos + sfx_cpe_residual_ln_pairs): the inverted
+    pair index names every pair, the per-row sum in ascending offset order equals the oracle conv, the fused
+    cpe/residual/LN tail equals the unfused one on that sum bit for bit, and two runs agree bit for bit."""
+    n = 6000
+    s = make_scene(n, 1, seed=5, unique_voxels=True)
+    grid = torch.floor(s["means"] * 320).int()
+    nbr_ref = ptv3_ref.subm_neighbors(grid, torch.zeros(grid.shape[0], dtype=torch.int64))
+    smap = ops.subm_neighbors(grid.to(device), None)
+    off = smap.pair_off
+    pos = smap.pair_pos.cpu().long()
+    pout = smap.pair_out.cpu().long()
+    assert int((pos >= 0).sum()) == off[27] and bool((pos[:, 13] < 0).all())
+    for k in range(27):
+        if k == 13:
+            continue
+        p = torch.arange(off[k], off[k + 1])
+        assert torch.equal(pos[pout[p], k], p)
+        assert torch.equal(pos[:, k] >= 0, nbr_ref[:, k] >= 0)
+    g = torch.Generator().manual_seed(4)
+    for C in (64, 96, 128, 256):
+        x = torch.randn(grid.shape[0], C, generator=g)
+        w = torch.randn(C, 3, 3, 3, C, generator=g) * 0.05
+        b = torch.randn(C, generator=g)
+        ga, be = torch.randn(C, generator=g), torch.randn(C, generator=g)
+        g1, b1 = torch.randn(C, generator=g), torch.randn(C, generator=g)
+        xd, wd, bd = x.to(device), w.to(device), b.to(device)
+        sp = ops.subm_conv(xd, smap, wd, bd, partials=True)
+        t = sp.total()
+        assert rel_l2(t.cpu(), ptv3_ref.subm_conv(x, nbr_ref, w, b)) < 2e-6
+        args = (ga.to(device), be.to(device), g1.to(device), b1.to(device), 1e-5)
+        xo, h = ops.cpe_residual_ln(sp, xd, *args)
+        xo_u, h_u = ops.cpe_residual_ln(t, xd, *args)
+        assert torch.equal(xo, xo_u) and torch.equal(h, h_u)
+        sp2 = ops.subm_conv(xd, smap, wd, bd, partials=True)
+        xo2, h2 = ops.cpe_residual_ln(sp2, xd, *args)
+        assert torch.equal(xo, xo2) and torch.equal(h, h2)
+
+
 def test_subm_neighbors_duplicates_lowest_index(device):
     grid = torch.tensor([[5, 5, 5], [5, 5, 5], [6, 5, 5], [5, 5, 5], [0, 0, 0]], dtype=torch.int32)
     nbr = ops.subm_neighbors(grid.to(device), None, with_pairs=False).cpu()
