@@ -1097,12 +1097,14 @@ constexpr TunedLaunch kTuned[] = {
     {100000, 384, 96, 1, 1}};
 
 // The same for the SubM conv launches of config B's stages (sfx_subm_conv: n, Cout, Cin -> the tile shape /
-// Stream-K of its centre and pair launches; profiles/r02_gemm_tune.jsonl)
+// Stream-K of its centre and pair launches; re-swept for the per-pair-store form,
+// profiles/r02_gemm_tune_conv_partials.jsonl -- Stream-K only applies to the atomic form)
 constexpr TunedLaunch kTunedConv[] = {
-    {90434, 96, 96, 3, 1},
+    {90434, 96, 96, 1, 1},
     {70349, 128, 128, 3, 1},
     {37759, 256, 256, 6, 1},
-    {100000, 96, 96, 3, 0}};
+    {14764, 512, 512, 6, 0},
+    {100000, 96, 96, 1, 0}};
 
 // tuning / test hooks: SFX_GEMM_CFG=<index into kCfgs>, SFX_GEMM_SK=0|1, or sfx_gemm_force_config()
 int forced = -2, forced_sk = -2;

@@ -1,6 +1,6 @@
 """Measure every (tile configuration, Stream-K) for each distinct GEMM launch of one refine pass (config B
 workload) and print the fastest -- the data behind gemm.hip's tuned table.  GPU only:
-python tools/gemm_tune.py [n_gaussians] > table.txt"""
+python tools/gemm_tune.py [n_gaussians] [kind filter, e.g. subm_conv] > table.txt"""
 import json
 import os
 import sys
@@ -39,7 +39,7 @@ class GemmRecorder:
             o = rec._conv(x, smap, weight, bias, out=out, **kw)
             n, cin = x.shape
             cout = weight.shape[0]
-            scratch = torch.empty_like(o)
+            scratch = torch.empty_like(o.centre if isinstance(o, ops.SubmPartials) else o)
             rec.calls.append(("subm_conv", 2.0 * (n + smap.num_pairs) * cin * cout,
                               lambda: rec._conv(x, smap, weight, bias, out=scratch, **kw), (n, cout, cin)))
             return o
@@ -73,6 +73,7 @@ def timeit(fn, reps=8):
 
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 100_000
+    only = sys.argv[2] if len(sys.argv) > 2 else None
     dev = torch.device("cuda")
     torch.manual_seed(0)
     model = FeaturePredictor(sh_degree=1, zeroinit=False).eval().to(dev)
@@ -84,6 +85,8 @@ def main():
     seen = {}
     for kind, fl, fn, shape in rec.calls:
         key = (kind,) + tuple(shape)
+        if only and kind != only:
+            continue
         if key in seen:
             seen[key][0] += 1
             continue
