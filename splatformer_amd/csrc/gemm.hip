@@ -1067,8 +1067,8 @@ void gemm_amax_jobs(const GemmArgs& a, int groups, AmaxJob& ja, AmaxJob& jw) {
   jw = AmaxJob{a.W, a.ldw, a.gW, a.N, a.K, groups, nullptr, 0, 1};
 }
 
-// Measured per-launch best (tile configuration, Stream-K) for the config-B refine's dense linears under fp16x2
-// operands (tools/gemm_tune.py; profiles/r01_gemm_tune_f16x2.jsonl, re-swept with the per-row scales in
+// Measured per-launch best (tile configuration, Stream-K) for the config-B (and config-E) refine's dense linears
+// under fp16x2 operands (tools/gemm_tune.py; profiles/r01_gemm_tune_f16x2.jsonl, re-swept with the per-row scales in
 // profiles/r02_gemm_tune.jsonl) where it beats the cost model by > 2 us;
 // applied when N and K match and M is within 0.8-1.25x of the tuned M (stage point counts vary per scene).
 struct TunedLaunch {
@@ -1094,7 +1094,28 @@ constexpr TunedLaunch kTuned[] = {
     {37759, 1024, 256, 6, 1},
     {14764, 512, 512, 6, 0},
     {70349, 96, 128, 1, 0},
-    {100000, 384, 96, 1, 1}};
+    {100000, 384, 96, 1, 1},
+    // config E (500k SH3) stages: profiles/r02_gemm_tune_configE.jsonl
+    {500000, 256, 64, 1, 1},
+    {329874, 384, 96, 1, 1},
+    {329874, 128, 96, 3, 0},
+    {167925, 128, 128, 3, 0},
+    {167925, 512, 128, 6, 1},
+    {167925, 128, 512, 5, 0},
+    {167925, 256, 128, 6, 1},
+    {66844, 768, 256, 6, 0},
+    {66844, 1024, 256, 6, 0},
+    {66844, 256, 1024, 6, 1},
+    {66844, 512, 256, 6, 1},
+    {31270, 1536, 512, 6, 0},
+    {31270, 512, 512, 6, 0},
+    {31270, 2048, 512, 6, 0},
+    {31270, 512, 2048, 5, 0},
+    {31270, 256, 512, 6, 0},
+    {66844, 128, 256, 3, 1},
+    {500000, 384, 96, 1, 0},
+    {500000, 768, 156, 6, 1},
+    {500000, 59, 768, 2, 0}};
 
 // The same for the SubM conv launches of config B's stages (sfx_subm_conv: n, Cout, Cin -> the tile shape /
 // Stream-K of its centre and pair launches; re-swept for the per-pair-store form,
@@ -1104,7 +1125,14 @@ constexpr TunedLaunch kTunedConv[] = {
     {70349, 128, 128, 3, 1},
     {37759, 256, 256, 6, 1},
     {14764, 512, 512, 6, 0},
-    {100000, 96, 96, 1, 0}};
+    {100000, 96, 96, 1, 0},
+    // config E (500k SH3) stages: profiles/r02_gemm_tune_configE.jsonl
+    {500000, 64, 64, 2, 1},
+    {329874, 96, 96, 1, 0},
+    {167925, 128, 128, 5, 0},
+    {66844, 256, 256, 6, 0},
+    {31270, 512, 512, 6, 0},
+    {500000, 96, 96, 1, 1}};
 
 // tuning / test hooks: SFX_GEMM_CFG=<index into kCfgs>, SFX_GEMM_SK=0|1, or sfx_gemm_force_config()
 int forced = -2, forced_sk = -2;

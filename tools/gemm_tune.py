@@ -1,6 +1,6 @@
 """Measure every (tile configuration, Stream-K) for each distinct GEMM launch of one refine pass (config B
 workload) and print the fastest -- the data behind gemm.hip's tuned table.  GPU only:
-python tools/gemm_tune.py [n_gaussians] [kind filter, e.g. subm_conv] > table.txt"""
+python tools/gemm_tune.py [n_gaussians] [kind filter, e.g. subm_conv, or all] [sh_degree] > table.txt"""
 import json
 import os
 import sys
@@ -73,11 +73,12 @@ def timeit(fn, reps=8):
 
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 100_000
-    only = sys.argv[2] if len(sys.argv) > 2 else None
+    only = sys.argv[2] if len(sys.argv) > 2 and sys.argv[2] != "all" else None
+    sh = int(sys.argv[3]) if len(sys.argv) > 3 else 1
     dev = torch.device("cuda")
     torch.manual_seed(0)
-    model = FeaturePredictor(sh_degree=1, zeroinit=False).eval().to(dev)
-    scene = to_device(make_scene(n, sh_degree=1, seed=0), dev)
+    model = FeaturePredictor(sh_degree=sh, zeroinit=False).eval().to(dev)
+    scene = to_device(make_scene(n, sh_degree=sh, seed=0), dev)
     model.refine_packed(scene)
     with GemmRecorder() as rec:
         model.refine_packed(scene)
