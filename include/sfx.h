@@ -189,6 +189,11 @@ int sfx_subm_conv_bwd_data(int n, int cin, int cout, const float* dy, long long 
 int sfx_window_attention_bwd(int num_windows, int window, int heads, int head_dim, int channels, const float* qkv,
                              const int* order, const int* win, float scale, const float* dout, float* dqkv,
                              void* stream);
+/* (ABI v7) enable_flash=True backward (windows as sfx_window_attention_varlen): dqkv [N, 3C] zero-filled,
+ * stats = workspace of N * heads * 2 floats (per-query log-sum-exp and dO.O). */
+int sfx_window_attention_varlen_bwd(int num_windows, int max_window, int heads, int head_dim, int channels,
+                                    const float* qkv, const int* order, const int* win3, float scale,
+                                    const float* dout, float* dqkv, float* stats, void* stream);
 /* nn.LayerNorm backward w.r.t. the input: dX = LN'(X) dY (+ dR) */
 int sfx_layernorm_bwd(int M, int C, const float* X, long long ldx, const float* gamma, const float* dY,
                       long long ldgy, const float* dR, long long ldr, float eps, float* dX, long long lddx,
@@ -247,6 +252,13 @@ int sfx_cpe_residual_ln_pairs(int M, int C, const float* T, const float* partial
 int sfx_window_attention(int num_windows, int window, int heads, int head_dim, int channels, const float* qkv,
                          const int* order, const int* win, float scale, float* out,
                          const unsigned long long* qkv_amax, unsigned qkv_tag, void* stream);
+/* (ABI v7) SerializedAttention with enable_flash=True (reference models/pointtransformer_v3.py:121-123: patch
+ * 1024; Pointcept's flash branch cuts the padded sequence at cu_seqlens): win3[w] = (key_start, query_start,
+ * key_count), key_count <= max_window <= 2^20 (a batch of n <= K points is one n-key window); online softmax over
+ * 128-key blocks, exact fp32 MFMA.  Same qkv / order / out layout as sfx_window_attention. */
+int sfx_window_attention_varlen(int num_windows, int max_window, int heads, int head_dim, int channels,
+                                const float* qkv, const int* order, const int* win3, float scale, float* out,
+                                void* stream);
 
 /* Point.serialization: codes[R][n] = batch << 3*depth | enc_t(grid) for order types t0..t3 (0 z, 1 z-trans,
  * 2 hilbert, 3 hilbert-trans) and combined sort keys r << code_bits | code; finalize turns the argsort of

@@ -40,6 +40,7 @@ class PTv3Config:
     dec_num_head: Sequence[int] = (4, 4, 8, 16)
     stride: Sequence[int] = (1, 2, 2, 2)
     patch_size: int = 128
+    enable_flash: bool = False  # Pointcept flash branch: fixed K = patch_size (1024 in the reference) windows
     mlp_ratio: int = 4
     bn_eps: float = 1e-3
     ln_eps: float = 1e-5
@@ -148,10 +149,42 @@ def get_padding_and_inverse(offset: torch.Tensor, patch_size: int):
     return pad, unpad
 
 
-def serialized_attention_heads(sd, p, point: Point, C, H, patch_size_max, order_index, feat):
+def cu_seqlens(offset: torch.Tensor, patch_size: int) -> torch.Tensor:
+    """Pointcept get_padding_and_inverse's third output (the flash branch's window starts over the padded
+    sequence + its end): arange(_offset_pad[i], _offset_pad[i+1], step=K) per batch."""
+    bincount = offset2bincount(offset)
+    bincount_pad = torch.div(bincount + patch_size - 1, patch_size, rounding_mode="trunc") * patch_size
+    mask_pad = bincount > patch_size
+    bincount_pad = ~mask_pad * bincount + mask_pad * bincount_pad
+    _offset_pad = F.pad(torch.cumsum(bincount_pad, dim=0), (1, 0))
+    cu = [torch.arange(_offset_pad[i], _offset_pad[i + 1], patch_size) for i in range(len(offset))]
+    return F.pad(torch.cat(cu), (0, 1), value=int(_offset_pad[-1]))
+
+
+def serialized_attention_flash(qkv, point: Point, C, H, K, order_index):
+    """The enable_flash=True branch (reference pointtransformer_v3.py:121-123 -> Pointcept SerializedAttention:
+    patch K fixed, qkv[order] over the padded sequence, flash_attn_varlen_qkvpacked_func over cu_seqlens windows,
+    feat[inverse]).  Pointcept casts qkv to fp16 for flash-attn; this restatement keeps fp32 (fp64 when qkv is).
+    Parity of the varlen window cut against a flash-attn run is unpinned (Pointcept / flash-attn are absent)."""
+    pad, unpad = get_padding_and_inverse(point.offset, K)
+    cu = cu_seqlens(point.offset, K)
+    order = point.serialized_order[order_index][pad]
+    inverse = unpad[point.serialized_inverse[order_index]]
+    q, k, v = qkv[order].reshape(-1, 3, H, C // H).unbind(dim=1)   # [Npad, H, d]
+    scale = (C // H) ** -0.5
+    out = torch.empty(q.shape[0], C, dtype=qkv.dtype)
+    for s, e in zip(cu[:-1].tolist(), cu[1:].tolist()):
+        a = torch.softmax(torch.einsum("qhd,khd->hqk", q[s:e] * scale, k[s:e]), dim=-1)
+        out[s:e] = torch.einsum("hqk,khd->qhd", a, v[s:e]).reshape(e - s, C)
+    return out[inverse]
+
+
+def serialized_attention_heads(sd, p, point: Point, C, H, patch_size_max, order_index, feat, flash=False):
     """SerializedAttention up to (excluding) proj: the per-head softmax(q k^T d^-1/2) v of every point, heads
     concatenated along channels, in the original point order [N, C] (restated visualize.py:140-179; pinned by
-    tests/golden/backbone_pins.npz captured from that hook)."""
+    tests/golden/backbone_pins.npz captured from that hook).  flash=True: serialized_attention_flash."""
+    if flash:
+        return serialized_attention_flash(linear(feat, sd, p + ".qkv"), point, C, H, patch_size_max, order_index)
     K = min(int(offset2bincount(point.offset).min()), patch_size_max)
     key = ("pad", K)
     if key not in point:
@@ -168,8 +201,8 @@ def serialized_attention_heads(sd, p, point: Point, C, H, patch_size_max, order_
     return out[inverse]
 
 
-def serialized_attention(sd, p, point: Point, C, H, patch_size_max, order_index, feat):
-    out = serialized_attention_heads(sd, p, point, C, H, patch_size_max, order_index, feat)
+def serialized_attention(sd, p, point: Point, C, H, patch_size_max, order_index, feat, flash=False):
+    out = serialized_attention_heads(sd, p, point, C, H, patch_size_max, order_index, feat, flash)
     return linear(out, sd, p + ".proj")
 
 
@@ -190,7 +223,7 @@ def block(sd, p, point: Point, C, H, cfg: PTv3Config, order_index, conv_in=None,
     h = ln(feat, sd, p + ".norm1.0", cfg.ln_eps)
     if trace is not None:
         trace["h1"] = h
-    h = serialized_attention(sd, p + ".attn", point, C, H, cfg.patch_size, order_index, h)
+    h = serialized_attention(sd, p + ".attn", point, C, H, cfg.patch_size, order_index, h, cfg.enable_flash)
     if masks.get(p + ".attn") is not None:
         h = h * masks[p + ".attn"][:, None]
     feat = shortcut + h

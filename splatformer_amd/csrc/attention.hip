@@ -156,6 +156,318 @@ window_attn_kernel(const float* __restrict__ qkv, const int* __restrict__ order,
   }
 }
 
+// ---- flash mode: windows of up to 2^20 keys, per-window key count -------------------------------------
+// Reference pointtransformer_v3.py:121-123 (patch 1024 when enable_flash) and Pointcept's SerializedAttention
+// flash branch: the padded serialized sequence is cut at cu_seqlens, so a batch of n <= K points is ONE window
+// of n keys (no padding) and a longer batch has windows of K keys, its ragged last one padded with the points
+// that precede it (the same (key_start, query_start) encoding as above).  Table win3[w] = (key_start,
+// query_start, key_count).
+//
+// One 256-thread workgroup per (window, 128-query block, head): the 128 queries stay in registers as S^T
+// columns while the window's keys stream through LDS in 128-key blocks with an online softmax (running max and
+// sum per query, accumulator rescaled by exp(m_old - m_new)), exact fp32 MFMA (v_mfma_f32_32x32x2_f32) --
+// the same S^T = K Q^T / O^T = V^T P^T register dataflow as window_attn_kernel, K/V LDS images reused per
+// block.  Query blocks past the window's count or wholly before its query_start exit before any barrier.
+template <int D>
+__global__ void __launch_bounds__(256, 2)
+window_attn_flash_kernel(const float* __restrict__ qkv, const int* __restrict__ order, const int* __restrict__ win3,
+                         int qblocks, int C, float scale, float* __restrict__ out) {
+  constexpr int DP = D + 4;
+  constexpr int DPV = 40;
+  constexpr int HALF = D / 2;
+  constexpr int CH = D / 4;
+  __shared__ __attribute__((aligned(16))) float Qs[KMAX * DP];
+  __shared__ __attribute__((aligned(16))) float Ks[KMAX * DP];
+  __shared__ __attribute__((aligned(16))) float Vs[KMAX * DPV];
+  __shared__ int qrows[KMAX];
+  __shared__ int krows[KMAX];
+
+  const int w = blockIdx.x / qblocks, qb = blockIdx.x - w * qblocks, head = blockIdx.y;
+  const int key_start = win3[3 * w], query_start = win3[3 * w + 1], count = win3[3 * w + 2];
+  const int q0 = qb * KMAX;  // window-relative first query of this block
+  if (q0 >= count || key_start + q0 + KMAX <= query_start) return;  // workgroup-uniform, before any barrier
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, h = lane >> 5, l32 = lane & 31;
+  const long long ld = 3ll * C;
+
+  if (tid < KMAX) qrows[tid] = q0 + tid < count ? order[key_start + q0 + tid] : -1;
+  if (D < 32)
+    for (int e = tid; e < KMAX * (32 - D) / 4; e += 256) {
+      const int row = e / ((32 - D) / 4), c4 = e - row * ((32 - D) / 4);
+      *reinterpret_cast<float4*>(&Vs[row * DPV + D + 4 * c4]) = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  __syncthreads();
+  for (int e = tid; e < KMAX * CH; e += 256) {
+    const int row = e / CH, ch = e - row * CH;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    const int src = qrows[row];
+    if (src >= 0) v = *reinterpret_cast<const float4*>(qkv + (long long)src * ld + head * D + 4 * ch);
+    v.x *= scale; v.y *= scale; v.z *= scale; v.w *= scale;
+    *reinterpret_cast<float4*>(&Qs[row * DP + 4 * ch]) = v;
+  }
+  __syncthreads();
+  float4 qv[HALF / 4];
+#pragma unroll
+  for (int c = 0; c < HALF / 4; ++c)
+    qv[c] = *reinterpret_cast<const float4*>(&Qs[(32 * wid + l32) * DP + h * HALF + 4 * c]);
+
+  float m_run = -INFINITY, l_run = 0.f;
+  floatx16 o;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) o[r] = 0.f;
+  const float* vcol = &Vs[4 * h * DPV + l32];
+
+  for (int k0 = 0; k0 < count; k0 += KMAX) {
+    const int nk = min(KMAX, count - k0);
+    __syncthreads();  // the previous block's K/V fragment reads are done
+    if (tid < KMAX) krows[tid] = tid < nk ? order[key_start + k0 + tid] : -1;
+    __syncthreads();
+    for (int e = tid; e < KMAX * 2 * CH; e += 256) {
+      const int row = e / (2 * CH);
+      const int rem = e - row * 2 * CH;
+      const int mat = rem / CH, ch = rem - mat * CH;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      const int src = krows[row];
+      if (src >= 0) v = *reinterpret_cast<const float4*>(qkv + (long long)src * ld + (mat + 1) * C + head * D + 4 * ch);
+      if (mat == 0) *reinterpret_cast<float4*>(&Ks[row * DP + 4 * ch]) = v;
+      else *reinterpret_cast<float4*>(&Vs[row * DPV + 4 * ch]) = v;
+    }
+    __syncthreads();
+
+    floatx16 s[4];
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s[kb][r] = 0.f;
+#pragma unroll
+    for (int c = 0; c < HALF / 4; ++c) {
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) {
+        const float4 kv = *reinterpret_cast<const float4*>(&Ks[(kb * 32 + l32) * DP + h * HALF + 4 * c]);
+        s[kb] = __builtin_amdgcn_mfma_f32_32x32x2f32(kv.x, qv[c].x, s[kb], 0, 0, 0);
+        s[kb] = __builtin_amdgcn_mfma_f32_32x32x2f32(kv.y, qv[c].y, s[kb], 0, 0, 0);
+        s[kb] = __builtin_amdgcn_mfma_f32_32x32x2f32(kv.z, qv[c].z, s[kb], 0, 0, 0);
+        s[kb] = __builtin_amdgcn_mfma_f32_32x32x2f32(kv.w, qv[c].w, s[kb], 0, 0, 0);
+      }
+    }
+    if (nk < KMAX) {
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          if (key >= nk) s[kb][r] = -INFINITY;
+        }
+    }
+    float bm = -INFINITY;
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) bm = fmaxf(bm, s[kb][r]);
+    bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
+    const float m_new = fmaxf(m_run, bm);  // finite: every block holds at least one key
+    const float corr = __expf(m_run - m_new);
+    float sum = 0.f;
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float e = __expf(s[kb][r] - m_new);
+        s[kb][r] = e;
+        sum += e;
+      }
+    sum += __shfl_xor(sum, 32, 64);
+    l_run = l_run * corr + sum;
+    m_run = m_new;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[r] *= corr;
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+      for (int st = 0; st < 16; ++st) {
+        const int key0 = kb * 32 + (st & 3) + 8 * (st >> 2);
+        o = __builtin_amdgcn_mfma_f32_32x32x2f32(vcol[key0 * DPV], s[kb][st], o, 0, 0, 0);
+      }
+  }
+
+  const float rinv = 1.f / l_run;
+  const int qi = q0 + 32 * wid + l32;
+  if (qi < count && key_start + qi >= query_start) {
+    float* dst = out + (long long)qrows[32 * wid + l32] * C + head * D;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int dd = 8 * g + 4 * h;
+      if (dd + 3 < D)
+        *reinterpret_cast<float4*>(dst + dd) = make_float4(o[4 * g + 0] * rinv, o[4 * g + 1] * rinv,
+                                                           o[4 * g + 2] * rinv, o[4 * g + 3] * rinv);
+    }
+  }
+}
+
+// ---- flash mode backward (training with enable_flash=True) ----------------------------------------------
+// Two launches, fp32 VALU (each lane owns one query or one key; the block's other rows stream through LDS as
+// wave-wide broadcasts):
+//   query pass: per query i of window w (i >= query_start): m_i, l_i and O_i (online softmax over the window's
+//     keys), lse_i = m_i + log l_i, delta_i = dO_i . O_i / l_i, then dQ_i = scale sum_j P_ij (dO_i.v_j - delta_i)
+//     k_j (plain store: a point is a query of exactly one window); (lse, delta) saved per (point, head).
+//   key pass: per key j of window w: dV_j += sum_i P_ij dO_i, dK_j += scale sum_i P_ij (dO_i.v_j - delta_i) q_i
+//     over the window's own queries; float atomics into dqkv (the keys of a ragged last window are also keys of
+//     the window before it: two adds onto the zero-filled buffer, order-independent).
+constexpr int FB = 128;  // rows per workgroup and per LDS block
+
+template <int D>
+__global__ void __launch_bounds__(FB)
+flash_bwd_query_kernel(const float* __restrict__ qkv, const int* __restrict__ order, const int* __restrict__ win3,
+                       int qblocks, int C, int H, float scale, const float* __restrict__ dout,
+                       float* __restrict__ dqkv, float* __restrict__ stats) {
+  __shared__ __attribute__((aligned(16))) float Ks[FB * D];
+  __shared__ __attribute__((aligned(16))) float Vs[FB * D];
+  __shared__ int krows[FB];
+  const int w = blockIdx.x / qblocks, qb = blockIdx.x - w * qblocks, head = blockIdx.y;
+  const int ks = win3[3 * w], qs = win3[3 * w + 1], cnt = win3[3 * w + 2];
+  const int q0 = qb * FB;
+  if (q0 >= cnt || ks + q0 + FB <= qs) return;  // workgroup-uniform, before any barrier
+  const int t = threadIdx.x, qi = q0 + t;
+  const bool valid = qi < cnt && ks + qi >= qs;
+  const int row = valid ? order[ks + qi] : 0;
+  const long long ld = 3ll * C;
+  float q[D], g[D], o[D], dq[D];
+#pragma unroll
+  for (int c = 0; c < D; ++c) {
+    q[c] = valid ? qkv[(long long)row * ld + head * D + c] * scale : 0.f;
+    g[c] = valid ? dout[(long long)row * C + head * D + c] : 0.f;
+    o[c] = 0.f;
+    dq[c] = 0.f;
+  }
+  auto stage = [&](int k0, int nk) {
+    __syncthreads();
+    krows[t] = t < nk ? order[ks + k0 + t] : -1;
+    __syncthreads();
+    for (int e = t; e < FB * D / 4; e += FB) {
+      const int r = e / (D / 4), c4 = e - r * (D / 4);
+      float4 kv = make_float4(0.f, 0.f, 0.f, 0.f), vv = kv;
+      if (krows[r] >= 0) {
+        const float* src = qkv + (long long)krows[r] * ld + head * D + 4 * c4;
+        kv = *reinterpret_cast<const float4*>(src + C);
+        vv = *reinterpret_cast<const float4*>(src + 2 * C);
+      }
+      *reinterpret_cast<float4*>(&Ks[r * D + 4 * c4]) = kv;
+      *reinterpret_cast<float4*>(&Vs[r * D + 4 * c4]) = vv;
+    }
+    __syncthreads();
+  };
+  float m = -INFINITY, l = 0.f;
+  for (int k0 = 0; k0 < cnt; k0 += FB) {
+    const int nk = min(FB, cnt - k0);
+    stage(k0, nk);
+    for (int j = 0; j < nk; ++j) {
+      float s = 0.f;
+#pragma unroll
+      for (int c = 0; c < D; ++c) s = fmaf(q[c], Ks[j * D + c], s);
+      const float mn = fmaxf(m, s);
+      const float corr = expf(m - mn), p = expf(s - mn);
+      l = l * corr + p;
+#pragma unroll
+      for (int c = 0; c < D; ++c) o[c] = fmaf(p, Vs[j * D + c], o[c] * corr);
+      m = mn;
+    }
+  }
+  float delta = 0.f;
+#pragma unroll
+  for (int c = 0; c < D; ++c) delta = fmaf(g[c], o[c], delta);
+  delta /= l;
+  const float lse = m + logf(l);
+  for (int k0 = 0; k0 < cnt; k0 += FB) {
+    const int nk = min(FB, cnt - k0);
+    stage(k0, nk);
+    for (int j = 0; j < nk; ++j) {
+      float s = 0.f, dp = 0.f;
+#pragma unroll
+      for (int c = 0; c < D; ++c) {
+        s = fmaf(q[c], Ks[j * D + c], s);
+        dp = fmaf(g[c], Vs[j * D + c], dp);
+      }
+      const float ds = expf(s - lse) * (dp - delta);
+#pragma unroll
+      for (int c = 0; c < D; ++c) dq[c] = fmaf(ds, Ks[j * D + c], dq[c]);
+    }
+  }
+  if (valid) {
+#pragma unroll
+    for (int c = 0; c < D; ++c) dqkv[(long long)row * ld + head * D + c] = dq[c] * scale;
+    stats[((long long)row * H + head) * 2] = lse;
+    stats[((long long)row * H + head) * 2 + 1] = delta;
+  }
+}
+
+template <int D>
+__global__ void __launch_bounds__(FB)
+flash_bwd_key_kernel(const float* __restrict__ qkv, const int* __restrict__ order, const int* __restrict__ win3,
+                     int kblocks, int C, int H, float scale, const float* __restrict__ dout,
+                     float* __restrict__ dqkv, const float* __restrict__ stats) {
+  __shared__ __attribute__((aligned(16))) float Qs[FB * D];
+  __shared__ __attribute__((aligned(16))) float Gs[FB * D];
+  __shared__ float Ls[FB], Ds[FB];
+  __shared__ int qrows[FB];
+  const int w = blockIdx.x / kblocks, kb = blockIdx.x - w * kblocks, head = blockIdx.y;
+  const int ks = win3[3 * w], qs = win3[3 * w + 1], cnt = win3[3 * w + 2];
+  const int k0 = kb * FB;
+  if (k0 >= cnt) return;  // workgroup-uniform
+  const int t = threadIdx.x, kj = k0 + t;
+  const bool valid = kj < cnt;
+  const int row = valid ? order[ks + kj] : 0;
+  const long long ld = 3ll * C;
+  float k[D], v[D], dk[D], dv[D];
+#pragma unroll
+  for (int c = 0; c < D; ++c) {
+    k[c] = valid ? qkv[(long long)row * ld + C + head * D + c] : 0.f;
+    v[c] = valid ? qkv[(long long)row * ld + 2 * C + head * D + c] : 0.f;
+    dk[c] = 0.f;
+    dv[c] = 0.f;
+  }
+  for (int i0 = qs - ks; i0 < cnt; i0 += FB) {  // the window's own queries
+    const int ni = min(FB, cnt - i0);
+    __syncthreads();
+    qrows[t] = t < ni ? order[ks + i0 + t] : -1;
+    __syncthreads();
+    for (int e = t; e < FB * D / 4; e += FB) {
+      const int r = e / (D / 4), c4 = e - r * (D / 4);
+      float4 qv = make_float4(0.f, 0.f, 0.f, 0.f), gv = qv;
+      if (qrows[r] >= 0) {
+        qv = *reinterpret_cast<const float4*>(qkv + (long long)qrows[r] * ld + head * D + 4 * c4);
+        qv.x *= scale; qv.y *= scale; qv.z *= scale; qv.w *= scale;
+        gv = *reinterpret_cast<const float4*>(dout + (long long)qrows[r] * C + head * D + 4 * c4);
+      }
+      *reinterpret_cast<float4*>(&Qs[r * D + 4 * c4]) = qv;
+      *reinterpret_cast<float4*>(&Gs[r * D + 4 * c4]) = gv;
+    }
+    Ls[t] = t < ni ? stats[((long long)qrows[t] * H + head) * 2] : INFINITY;
+    Ds[t] = t < ni ? stats[((long long)qrows[t] * H + head) * 2 + 1] : 0.f;
+    __syncthreads();
+    for (int i = 0; i < ni; ++i) {
+      float s = 0.f, dp = 0.f;
+#pragma unroll
+      for (int c = 0; c < D; ++c) {
+        s = fmaf(Qs[i * D + c], k[c], s);
+        dp = fmaf(Gs[i * D + c], v[c], dp);
+      }
+      const float p = expf(s - Ls[i]);
+      const float ds = p * (dp - Ds[i]);
+#pragma unroll
+      for (int c = 0; c < D; ++c) {
+        dv[c] = fmaf(p, Gs[i * D + c], dv[c]);
+        dk[c] = fmaf(ds, Qs[i * D + c], dk[c]);
+      }
+    }
+  }
+  if (valid) {
+    float* dst = dqkv + (long long)row * ld + head * D;
+#pragma unroll
+    for (int c = 0; c < D; ++c) {
+      atomicAdd(dst + C + c, dk[c]);
+      atomicAdd(dst + 2 * C + c, dv[c]);
+    }
+  }
+}
 
 // ---- split-bf16 forward (default) ---------------------------------------------------------------------
 // The same dataflow on v_mfma_f32_32x32x16_bf16: q, k, v and p enter as three bf16 terms each
@@ -681,6 +993,62 @@ int sfx_window_attention(int num_windows, int window, int heads, int head_dim, i
 #undef SFX_ATTN
   }
   return sfx::check_launch("sfx_window_attention");
+}
+
+// flash mode: win3 [num_windows][3] = (key_start, query_start, key_count), key_count <= max_window
+int sfx_window_attention_varlen(int num_windows, int max_window, int heads, int head_dim, int channels,
+                                const float* qkv, const int* order, const int* win3, float scale, float* out,
+                                void* stream) {
+  SFX_REQUIRE(num_windows >= 0, "sfx_window_attention_varlen: num_windows < 0");
+  SFX_REQUIRE(max_window >= 1 && max_window <= (1 << 20), "sfx_window_attention_varlen: max_window out of [1, 2^20]");
+  SFX_REQUIRE(heads * head_dim == channels, "sfx_window_attention_varlen: heads * head_dim != channels");
+  SFX_REQUIRE(head_dim == 16 || head_dim == 24 || head_dim == 32,
+              "sfx_window_attention_varlen: head_dim %d unsupported (16, 24, 32)", head_dim);
+  if (num_windows == 0) return SFX_OK;
+  SFX_REQUIRE(qkv && order && win3 && out, "sfx_window_attention_varlen: null buffer");
+  const int qblocks = (max_window + KMAX - 1) / KMAX;
+  SFX_REQUIRE((long long)num_windows * qblocks < (1ll << 31) && heads <= 65535,
+              "sfx_window_attention_varlen: grid too large");
+  dim3 grid((unsigned)(num_windows * qblocks), heads);
+  hipStream_t st = sfx::as_stream(stream);
+  if (head_dim == 16)
+    window_attn_flash_kernel<16><<<grid, 256, 0, st>>>(qkv, order, win3, qblocks, channels, scale, out);
+  else if (head_dim == 24)
+    window_attn_flash_kernel<24><<<grid, 256, 0, st>>>(qkv, order, win3, qblocks, channels, scale, out);
+  else
+    window_attn_flash_kernel<32><<<grid, 256, 0, st>>>(qkv, order, win3, qblocks, channels, scale, out);
+  return sfx::check_launch("sfx_window_attention_varlen");
+}
+
+// flash-mode backward: dqkv [N, 3C] zero-filled by the caller, stats [N][heads][2] floats of workspace
+int sfx_window_attention_varlen_bwd(int num_windows, int max_window, int heads, int head_dim, int channels,
+                                    const float* qkv, const int* order, const int* win3, float scale,
+                                    const float* dout, float* dqkv, float* stats, void* stream) {
+  SFX_REQUIRE(num_windows >= 0, "sfx_window_attention_varlen_bwd: num_windows < 0");
+  SFX_REQUIRE(max_window >= 1 && max_window <= (1 << 20),
+              "sfx_window_attention_varlen_bwd: max_window out of [1, 2^20]");
+  SFX_REQUIRE(heads * head_dim == channels, "sfx_window_attention_varlen_bwd: heads * head_dim != channels");
+  SFX_REQUIRE(head_dim == 16 || head_dim == 24 || head_dim == 32,
+              "sfx_window_attention_varlen_bwd: head_dim %d unsupported (16, 24, 32)", head_dim);
+  if (num_windows == 0) return SFX_OK;
+  SFX_REQUIRE(qkv && order && win3 && dout && dqkv && stats, "sfx_window_attention_varlen_bwd: null buffer");
+  const int blocks = (max_window + FB - 1) / FB;
+  SFX_REQUIRE((long long)num_windows * blocks < (1ll << 31) && heads <= 65535,
+              "sfx_window_attention_varlen_bwd: grid too large");
+  dim3 grid((unsigned)(num_windows * blocks), heads);
+  hipStream_t st = sfx::as_stream(stream);
+#define SFX_FBWD(DD)                                                                                           \
+  do {                                                                                                         \
+    flash_bwd_query_kernel<DD><<<grid, FB, 0, st>>>(qkv, order, win3, blocks, channels, heads, scale, dout, dqkv, \
+                                                     stats);                                                   \
+    flash_bwd_key_kernel<DD><<<grid, FB, 0, st>>>(qkv, order, win3, blocks, channels, heads, scale, dout, dqkv, \
+                                                   stats);                                                     \
+  } while (0)
+  if (head_dim == 16) SFX_FBWD(16);
+  else if (head_dim == 24) SFX_FBWD(24);
+  else SFX_FBWD(32);
+#undef SFX_FBWD
+  return sfx::check_launch("sfx_window_attention_varlen_bwd");
 }
 
 // dout [N, C] = d(attention output); dqkv [N, 3C] zero-filled by the caller (dK/dV accumulate)

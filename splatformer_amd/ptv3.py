@@ -75,10 +75,13 @@ class MLP(nn.Module):
 
 
 class SerializedAttention(nn.Module):
-    def __init__(self, channels, num_heads, patch_size, order_index=0):
+    def __init__(self, channels, num_heads, patch_size, order_index=0, enable_flash=False):
         super().__init__()
         assert channels % num_heads == 0
         self.channels, self.num_heads = channels, num_heads
+        # Pointcept's flash branch: fixed K = patch_size windows cut at cu_seqlens (a batch of n <= K points is
+        # one n-key window) instead of K = min(min bincount, patch_size)
+        self.enable_flash = enable_flash
         self.scale = (channels // num_heads) ** -0.5
         self.order_index = order_index
         self.patch_size_max = patch_size
@@ -90,14 +93,15 @@ class SerializedAttention(nn.Module):
 
 
 class Block(nn.Module):
-    def __init__(self, channels, num_heads, patch_size=128, mlp_ratio=4.0, order_index=0, cpe_indice_key=None):
+    def __init__(self, channels, num_heads, patch_size=128, mlp_ratio=4.0, order_index=0, cpe_indice_key=None,
+                 enable_flash=False):
         super().__init__()
         self.channels = channels
         self.pre_norm = True
         self.cpe = PointSequential(SubMConv3d(channels, channels, 3, True, cpe_indice_key),
                                    nn.Linear(channels, channels), nn.LayerNorm(channels))
         self.norm1 = PointSequential(nn.LayerNorm(channels))
-        self.attn = SerializedAttention(channels, num_heads, patch_size, order_index)
+        self.attn = SerializedAttention(channels, num_heads, patch_size, order_index, enable_flash)
         self.norm2 = PointSequential(nn.LayerNorm(channels))
         self.mlp = PointSequential(MLP(channels, int(channels * mlp_ratio), channels))
         self.drop_path = PointSequential(nn.Identity())  # DropPath has no parameters; rate in drop_prob
@@ -136,9 +140,13 @@ class Block(nn.Module):
         ln1 = self.norm1[0]
         x1, h = ops.cpe_residual_ln(t, x, ln_c.weight, ln_c.bias, ln1.weight, ln1.bias, ln1.eps)
         qkv, q_amax = ops.linear(h, self.attn.qkv.weight, self.attn.qkv.bias, y_amax=True)
-        K, win, nw = point_windows(point, self.attn.patch_size_max)
         oi = point.order_type[self.attn.order_index]
-        a = ops.window_attention(qkv, point.order_phys[oi], win, nw, K, self.attn.num_heads, C, qkv_amax=q_amax)
+        if self.attn.enable_flash:
+            K, win3, nw = point_windows_flash(point, self.attn.patch_size_max)
+            a = ops.window_attention_varlen(qkv, point.order_phys[oi], win3, nw, K, self.attn.num_heads, C)
+        else:
+            K, win, nw = point_windows(point, self.attn.patch_size_max)
+            a = ops.window_attention(qkv, point.order_phys[oi], win, nw, K, self.attn.num_heads, C, qkv_amax=q_amax)
         x2 = ops.linear(a, self.attn.proj.weight, self.attn.proj.bias, residual=x1)
         ln2 = self.norm2[0]
         h2 = ops.layernorm(x2, ln2.weight, ln2.bias, ln2.eps)
@@ -248,6 +256,17 @@ def point_windows(point: Point, patch_size_max: int):
     return K, win, nw
 
 
+def point_windows_flash(point: Point, patch_size_max: int):
+    """Flash mode: K = patch_size_max and the (key_start, query_start, key_count) device table (cached per Point)."""
+    K = patch_size_max
+    key = ("winv", K)
+    if key not in point:
+        t = torch.from_numpy(ops.window_table_varlen_np(point.offset, K)).pin_memory()
+        point[key] = (t.to(point.feat.device, non_blocking=True), t.shape[0])
+    win3, nw = point[key]
+    return K, win3, nw
+
+
 class _Container(nn.Module):
     def add(self, module, name):
         self.add_module(name, module)
@@ -258,7 +277,7 @@ class PointTransformerV3(nn.Module):
                  enc_channels=(32, 64, 128, 256, 512), enc_num_head=(2, 4, 8, 16, 32),
                  enc_patch_size=(48, 48, 48, 48, 48), dec_depths=(2, 2, 2, 2), dec_channels=(64, 64, 128, 256),
                  dec_num_head=(4, 4, 8, 16), dec_patch_size=(48, 48, 48, 48), mlp_ratio=4, turn_off_bn=False,
-                 shuffle_orders=True, embedding_type="MLP", drop_path=0.3):
+                 shuffle_orders=True, embedding_type="MLP", drop_path=0.3, enable_flash=False):
         super().__init__()
         if turn_off_bn:
             raise NotImplementedError("turn_off_bn=True is not on the SplatFormer path (ptv3_base.gin:30)")
@@ -280,7 +299,7 @@ class PointTransformerV3(nn.Module):
                         "down")
             for i in range(enc_depths[s]):
                 enc.add(Block(enc_channels[s], enc_num_head[s], enc_patch_size[s], mlp_ratio, i % len(self.order),
-                              f"stage{s}"), f"block{i}")
+                              f"stage{s}", enable_flash), f"block{i}")
             self.enc.add(enc, f"enc{s}")
         # DropPath schedule (reference pointtransformer_v3.py:280-287, :330-339): linspace(0, p) over the
         # encoder blocks in order, and over the decoder blocks with each stage's slice reversed
@@ -296,7 +315,7 @@ class PointTransformerV3(nn.Module):
             dec.add(SerializedUnpooling(dch[s + 1], enc_channels[s], dch[s], bn_layer, nn.GELU), "up")
             for i in range(dec_depths[s]):
                 dec.add(Block(dch[s], dec_num_head[s], dec_patch_size[s], mlp_ratio, i % len(self.order),
-                              f"stage{s}"), f"block{i}")
+                              f"stage{s}", enable_flash), f"block{i}")
             self.dec.add(dec, f"dec{s}")
         dec_dp = torch.linspace(0, drop_path, sum(dec_depths)).tolist()
         for s in range(self.num_stages - 1):
@@ -406,15 +425,16 @@ class PointTransformerV3Model(nn.Module):
             if enc_channels is None:
                 raise ValueError("Unsupported enc_dim")
         self.dec_channels = tuple(dec_channels)
-        # the HIP attention kernel implements both paths with the non-flash math; flash would use K=1024
+        # enable_flash: K = 1024 windows cut at cu_seqlens (sfx_window_attention_varlen), fp32 arithmetic where
+        # Pointcept's flash-attn call runs fp16 (>= the reference's precision)
         patch = 1024 if enable_flash else 128
         self.backbone = PointTransformerV3(
             in_channels=in_channels, order=ORDERS, stride=stride, enc_depths=enc_depths, enc_channels=enc_channels,
             enc_num_head=enc_num_head, enc_patch_size=(patch,) * len(enc_channels), dec_depths=dec_depths,
             dec_channels=dec_channels, dec_num_head=dec_num_head, dec_patch_size=(patch,) * len(dec_channels),
-            mlp_ratio=4, turn_off_bn=turn_off_bn, shuffle_orders=True, embedding_type=embedding_type)
-        if enable_flash:
-            raise NotImplementedError("enable_flash=True (K=1024 windows) exceeds the 128-key window kernel")
+            mlp_ratio=4, turn_off_bn=turn_off_bn, shuffle_orders=True, embedding_type=embedding_type,
+            enable_flash=enable_flash)
+        self.enable_flash = enable_flash
         self.output_dim = self.dec_channels[0]
         if pretrained_ckpt is not None:
             sd = torch.load(pretrained_ckpt, map_location="cpu", weights_only=True)["state_dict"]

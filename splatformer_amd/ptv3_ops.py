@@ -25,6 +25,7 @@ _lib.register("sfx_layernorm", [I, I, P, L, P, P, F, P, L, P])
 _lib.register("sfx_cpe_residual_ln", [I, I, P, P, P, P, P, P, F, P, P, P])
 _lib.register("sfx_cpe_residual_ln_pairs", [I, I, P, P, P, L, P, P, P, P, P, F, P, P, P])
 _lib.register("sfx_window_attention", [I, I, I, I, I, P, P, P, F, P, P, I, P])
+_lib.register("sfx_window_attention_varlen", [I, I, I, I, I, P, P, P, F, P, P])
 _lib.register("sfx_serialize_keys", [I, P, P, I, I, I, I, I, I, I, P, P, P])
 _lib.register("sfx_serialize_finalize", [I, I, P, P, P, P])
 _lib.register("sfx_pool_run_flags", [I, I, P, P, I, P, P])
@@ -268,6 +269,40 @@ def window_table_np(offsets: Sequence[int], K: int) -> np.ndarray:
         start = end
     tab = np.concatenate(parts) if parts else np.zeros((0, 2), np.int64)
     return np.ascontiguousarray(tab, dtype=np.int32)
+
+
+def window_table_varlen_np(offsets: Sequence[int], K: int) -> np.ndarray:
+    """The flash branch's windows (Pointcept get_padding_and_inverse + cu_seqlens, patch K) as an int32
+    [num_windows, 3] array of (key_start, query_start, key_count): a batch of n <= K points is one window of n keys
+    (no padding), a longer one has K-key windows with the ragged last one padded by its preceding points."""
+    parts = []
+    start = 0
+    for end in offsets:
+        n = end - start
+        if 0 < n <= K:
+            parts.append(np.array([[start, start, n]], np.int64))
+        elif n > K:
+            qs = start + K * np.arange((n + K - 1) // K, dtype=np.int64)
+            ks = np.minimum(qs, end - K)
+            parts.append(np.stack([ks, qs, np.full_like(qs, K)], 1))
+        start = end
+    tab = np.concatenate(parts) if parts else np.zeros((0, 3), np.int64)
+    return np.ascontiguousarray(tab, dtype=np.int32)
+
+
+def window_attention_varlen(qkv: Tensor, order: Tensor, win3: Tensor, num_windows: int, K: int, heads: int,
+                            channels: int, out: Optional[Tensor] = None) -> Tensor:
+    """Flash-mode attention (enable_flash=True, K = 1024): per-window key counts, online softmax (attention.hip)."""
+    n = qkv.shape[0]
+    d = channels // heads
+    if qkv.shape != (n, 3 * channels) or order.shape[0] != n or tuple(win3.shape) != (num_windows, 3):
+        raise ValueError(f"window_attention_varlen: shapes qkv {tuple(qkv.shape)} order {tuple(order.shape)} "
+                         f"win3 {tuple(win3.shape)} for C={channels}, {num_windows} windows")
+    if out is None:
+        out = torch.empty(n, channels, device=qkv.device, dtype=torch.float32)
+    call("sfx_window_attention_varlen", num_windows, K, heads, d, channels, ptr(qkv), ptr(order, torch.int32),
+         ptr(win3, torch.int32), float(d ** -0.5), ptr(out), stream())
+    return out
 
 
 def window_attention(qkv: Tensor, order: Tensor, win: Tensor, num_windows: int, K: int, heads: int, channels: int,

@@ -23,7 +23,8 @@ from torch import Tensor
 
 from . import ptv3_ops as ops
 from . import train_ops as tops
-from .ptv3 import Block, Point, PointTransformerV3, SerializedPooling, SerializedUnpooling, point_windows
+from .ptv3 import (Block, Point, PointTransformerV3, SerializedPooling, SerializedUnpooling, point_windows,
+                   point_windows_flash)
 
 MaskFn = Callable[[str, int, float], Optional[Tensor]]
 
@@ -75,9 +76,13 @@ def block_forward(blk: Block, name: str, point: Point, masks: MaskFn, conv_in: O
     u = ops.subm_conv(x if conv_in is None else conv_in, point.nbr, wf, bf)
     x1, h = ops.cpe_residual_ln(u, x, ln_c.weight, ln_c.bias, ln1.weight, ln1.bias, ln1.eps)
     qkv = ops.linear(h, blk.attn.qkv.weight, blk.attn.qkv.bias)
-    K, win, nw = point_windows(point, blk.attn.patch_size_max)
     order = point.order_phys[point.order_type[blk.attn.order_index]]
-    a = ops.window_attention(qkv, order, win, nw, K, blk.attn.num_heads, C)
+    if blk.attn.enable_flash:  # K = 1024 windows cut at cu_seqlens
+        K, win, nw = point_windows_flash(point, blk.attn.patch_size_max)
+        a = ops.window_attention_varlen(qkv, order, win, nw, K, blk.attn.num_heads, C)
+    else:
+        K, win, nw = point_windows(point, blk.attn.patch_size_max)
+        a = ops.window_attention(qkv, order, win, nw, K, blk.attn.num_heads, C)
     ma = masks(name + ".attn", n, blk.drop_prob, x.device)
     x2 = ops.linear(a, blk.attn.proj.weight, blk.attn.proj.bias, residual=x1, rowscale=ma)
     del a
@@ -118,8 +123,8 @@ def block_backward(rec: dict, dy: Tensor, need_input: bool):
     _trace(f"{nm}.dx2", dx2)
     del dh2
     da = tops.linear_bwd_data(dx2, wt(blk.attn.proj.weight), rowscale=rec["ma"])
-    dqkv = tops.window_attention_bwd(rec["qkv"], rec["order"], rec["win"], rec["nw"], rec["K"], blk.attn.num_heads, C,
-                                     da)
+    bwd = tops.window_attention_varlen_bwd if blk.attn.enable_flash else tops.window_attention_bwd
+    dqkv = bwd(rec["qkv"], rec["order"], rec["win"], rec["nw"], rec["K"], blk.attn.num_heads, C, da)
     _trace(f"{nm}.da", da)
     _trace(f"{nm}.dqkv", dqkv)
     del da

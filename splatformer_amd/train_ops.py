@@ -23,6 +23,7 @@ _lib.register("sfx_linear_wgrad", [I, I, I, P, L, P, L, P, L, P, P])
 _lib.register("sfx_transpose", [I, I, P, L, P, L, P])
 _lib.register("sfx_subm_conv_bwd_data", [I, I, I, P, L, P, P, P, P, P, P, P, L, P, P, P])
 _lib.register("sfx_window_attention_bwd", [I, I, I, I, I, P, P, P, F, P, P, P])
+_lib.register("sfx_window_attention_varlen_bwd", [I, I, I, I, I, P, P, P, F, P, P, P, P])
 _lib.register("sfx_layernorm_bwd", [I, I, P, L, P, P, L, P, L, F, P, L, P])
 _lib.register("sfx_cpe_ln_bwd", [I, I, P, P, P, P, P, P, F, P, P, P])
 _lib.register("sfx_colsum2_workspace_bytes", [I, I], Z)
@@ -97,6 +98,21 @@ def window_attention_bwd(qkv: Tensor, order: Tensor, win: Tensor, num_windows: i
     d = channels // heads
     call("sfx_window_attention_bwd", num_windows, K, heads, d, channels, ptr(qkv), ptr(order, torch.int32),
          ptr(win, torch.int32), float(d ** -0.5), ptr(dout), ptr(dqkv), stream())
+    return dqkv
+
+
+def window_attention_varlen_bwd(qkv: Tensor, order: Tensor, win3: Tensor, num_windows: int, K: int, heads: int,
+                                channels: int, dout: Tensor) -> Tensor:
+    """Backward of ptv3_ops.window_attention_varlen (enable_flash=True): query pass (dQ, per-query log-sum-exp and
+    dO.O) then key pass (dK, dV), attention.hip."""
+    n = qkv.shape[0]
+    if qkv.shape != (n, 3 * channels) or dout.shape != (n, channels) or tuple(win3.shape) != (num_windows, 3):
+        raise ValueError("window_attention_varlen_bwd: shape mismatch")
+    dqkv = torch.zeros_like(qkv)
+    stats = torch.empty(max(n, 1) * heads * 2, device=qkv.device, dtype=torch.float32)
+    d = channels // heads
+    call("sfx_window_attention_varlen_bwd", num_windows, K, heads, d, channels, ptr(qkv), ptr(order, torch.int32),
+         ptr(win3, torch.int32), float(d ** -0.5), ptr(dout), ptr(dqkv), ptr(stats), stream())
     return dqkv
 
 

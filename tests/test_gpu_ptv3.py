@@ -276,6 +276,34 @@ def test_window_attention_vs_reference_padding(device, n, heads, C, terms):
     assert rel_l2(out.cpu(), ref) < 2e-6
 
 
+@pytest.mark.parametrize("K", [1024, 256])
+@pytest.mark.parametrize("heads,C", [(2, 32), (4, 96), (8, 256)])
+def test_window_attention_flash_varlen(device, K, heads, C):
+    """enable_flash=True windows (pointtransformer_v3.py:121-123, K = 1024): batches of n < K (one n-key window),
+    n == K, ragged n > K (last window padded with the preceding points) and n = 2K, one launch; vs the oracle's
+    cu_seqlens restatement in fp64 (online softmax over 128-key blocks vs one softmax: order of summation only)."""
+    counts = [700, K, 2 * K + 333, 2 * K, 5, 1]
+    n = sum(counts)
+    offset = torch.tensor(counts).cumsum(0)
+    g = torch.Generator().manual_seed(K + C)
+    qkv = torch.randn(n, 3 * C, generator=g, dtype=torch.float64) * 2
+    batch = torch.repeat_interleave(torch.arange(len(counts)), torch.tensor(counts))
+    order = torch.cat([torch.randperm(c, generator=g) + (int(offset[i]) - c) for i, c in enumerate(counts)])
+    inverse = torch.empty_like(order)
+    inverse[order] = torch.arange(n)
+    point = ptv3_ref.Point(offset=offset, serialized_order=order[None], serialized_inverse=inverse[None], batch=batch)
+    ref = ptv3_ref.serialized_attention_flash(qkv, point, C, heads, K, 0)
+    tab = ops.window_table_varlen_np(offset.tolist(), K)
+    win3 = torch.from_numpy(tab).to(device)
+    out = ops.window_attention_varlen(qkv.float().to(device), order.int().to(device), win3, tab.shape[0], K, heads, C)
+    assert rel_l2(out.cpu(), ref) < 2e-6
+    # every point written exactly once (no stale rows): a NaN-filled output buffer comes back NaN-free
+    out2 = torch.full((n, C), float("nan"), device=device)
+    ops.window_attention_varlen(qkv.float().to(device), order.int().to(device), win3, tab.shape[0], K, heads, C,
+                                out=out2)
+    assert torch.equal(out2.cpu(), out.cpu())
+
+
 def test_layernorm_ops(device):
     g = torch.Generator().manual_seed(2)
     for C in (64, 96, 128, 256, 512, 48):  # vectorised row-group kernels + the generic fallback (48)
@@ -319,10 +347,13 @@ def _model(seed=0, **bk):
     (3000, True, {}),
     (5000, False, {}),
     (2000, True, dict(enc_depths=(1, 1, 1, 1, 1), dec_depths=(1, 1, 1, 1))),  # config A shape (depth 1)
+    (6000, False, dict(enable_flash=True)),  # K = 1024 windows (pointtransformer_v3.py:121-123)
 ])
 def test_feature_predictor_matches_oracle(device, n, unique, bk):
     model = _model(3, **bk)
     cfg = ptv3_ref.PTv3Config(**{k: v for k, v in bk.items()})
+    if cfg.enable_flash:
+        cfg.patch_size = 1024
     sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
     model = model.to(device)
     s = make_scene(n, 1, seed=n, unique_voxels=unique)

@@ -114,11 +114,14 @@ def test_refiner_train_grads_match_oracle(device, n, unique, bk):
     (3000, True, {}),
     (4000, False, {}),
     (2000, True, dict(enc_depths=(1, 1, 1, 1, 1), dec_depths=(1, 1, 1, 1))),
+    (6000, False, dict(enable_flash=True)),  # K = 1024 windows (sfx_window_attention_varlen[_bwd])
 ])
 def test_backbone_train_grads_match_oracle(device, n, unique, bk):
     """PTv3 train forward + backward from a random d(feature) (no ReLU heads): tight bar."""
     model = _model(31, **bk)
     cfg = ptv3_ref.PTv3Config(**bk)
+    if cfg.enable_flash:
+        cfg.patch_size = 1024
     sd = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
     model = model.to(device)
     for name, p in model.named_parameters():

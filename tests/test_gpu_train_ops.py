@@ -100,6 +100,31 @@ def test_window_attention_bwd(device, n, heads, C):
     assert rel_l2(dqkv, qkv.grad) < 1e-5
 
 
+@pytest.mark.parametrize("K", [1024, 256])
+@pytest.mark.parametrize("heads,C", [(2, 32), (4, 96), (8, 256)])
+def test_window_attention_varlen_bwd(device, K, heads, C):
+    """enable_flash=True backward vs fp64 autograd of the oracle's cu_seqlens restatement: batches of n < K,
+    n == K, ragged n > K (keys shared by two windows) and 2K."""
+    counts = [700, K, 2 * K + 333, 2 * K, 5]
+    n = sum(counts)
+    offset = torch.tensor(counts).cumsum(0)
+    g = torch.Generator().manual_seed(K + C + 1)
+    qkv = torch.randn(n, 3 * C, generator=g, dtype=torch.float64)
+    order = torch.cat([torch.randperm(c, generator=g) + (int(offset[i]) - c) for i, c in enumerate(counts)])
+    inverse = torch.empty_like(order)
+    inverse[order] = torch.arange(n)
+    point = ptv3_ref.Point(offset=offset, serialized_order=order[None], serialized_inverse=inverse[None])
+    qkv_ref = qkv.clone().requires_grad_()
+    out = ptv3_ref.serialized_attention_flash(qkv_ref, point, C, heads, K, 0)
+    dout = torch.randn(n, C, generator=g, dtype=torch.float64)
+    out.backward(dout)
+    tab = ops.window_table_varlen_np(offset.tolist(), K)
+    win3 = torch.from_numpy(tab).to(device)
+    dqkv = tops.window_attention_varlen_bwd(qkv.float().to(device), order.int().to(device), win3, tab.shape[0], K,
+                                            heads, C, dout.float().to(device))
+    assert rel_l2(dqkv, qkv_ref.grad) < 1e-5
+
+
 def test_layernorm_bwd_ops(device):
     g = torch.Generator().manual_seed(3)
     for C in (64, 96, 256, 512):
