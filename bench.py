@@ -74,6 +74,8 @@ def parse(argv=None):
     ap.add_argument("--views", type=int, default=None)
     ap.add_argument("--sh", type=int, default=None)
     ap.add_argument("--batch", type=int, default=None, help="scenes per step (C) / micro-steps (D)")
+    ap.add_argument("--flash", action="store_true",
+                    help="PointTransformerV3Model.enable_flash=True (K=1024 windows, pointtransformer_v3.py:121-123)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC passes")
     ap.add_argument("--cpu-sample", type=int, default=None,
@@ -432,7 +434,9 @@ def main(argv=None):
     train = args.config in ("C", "D")
     cams_cpu = make_cameras(args.width, args.height, n_views=args.views)
     cams = to_device(cams_cpu, dev)
-    bk = DEPTH1 if args.config == "A" else {}
+    bk = dict(DEPTH1) if args.config == "A" else {}
+    if args.flash:
+        bk["enable_flash"] = True
     torch.manual_seed(0)
     model = FeaturePredictor(sh_degree=args.sh, zeroinit=False, backbone_kwargs=bk).eval()
     sd_cpu = {k: v.detach().clone() for k, v in model.state_dict().items()}
@@ -548,7 +552,8 @@ def main(argv=None):
             "dtype": "fp32",
             "data": f"synthetic (seeded {args.n}-Gaussian scene(s) per rank, random-init ptv3_base weights)",
             "config": {"workload": workload, "scenes_per_step": (args.batch if train else 1) * world,
-                       "views_per_scene": args.views, "parallelism": par},
+                       "views_per_scene": args.views, "parallelism": par,
+                       "attention": "flash (K=1024 varlen)" if args.flash else "non-flash (K=128, ptv3_base.gin:27)"},
             "roofline": roof,
             "cpu_baseline": cpu,
         }
