@@ -255,10 +255,11 @@ int sfx_window_attention(int num_windows, int window, int heads, int head_dim, i
 /* (ABI v7) SerializedAttention with enable_flash=True (reference models/pointtransformer_v3.py:121-123: patch
  * 1024; Pointcept's flash branch cuts the padded sequence at cu_seqlens): win3[w] = (key_start, query_start,
  * key_count), key_count <= max_window <= 2^20 (a batch of n <= K points is one n-key window); online softmax over
- * 128-key blocks, exact fp32 MFMA.  Same qkv / order / out layout as sfx_window_attention. */
+ * 128-key blocks.  Same qkv / order / out layout and the same term forms as sfx_window_attention (fp16x2 when
+ * qkv_amax bounds |qkv|, bf16x3 without, exact fp32 MFMA under SFX_ATTN_PREC=fp32). */
 int sfx_window_attention_varlen(int num_windows, int max_window, int heads, int head_dim, int channels,
                                 const float* qkv, const int* order, const int* win3, float scale, float* out,
-                                void* stream);
+                                const unsigned long long* qkv_amax, unsigned qkv_tag, void* stream);
 
 /* Point.serialization: codes[R][n] = batch << 3*depth | enc_t(grid) for order types t0..t3 (0 z, 1 z-trans,
  * 2 hilbert, 3 hilbert-trans) and combined sort keys r << code_bits | code; finalize turns the argsort of

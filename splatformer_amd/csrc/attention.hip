@@ -709,6 +709,251 @@ window_attn_split_kernel(const float* __restrict__ qkv, const int* __restrict__ 
 }
 
 
+// Flash mode on split MFMA terms (default for sfx_window_attention_varlen): window_attn_split_kernel's
+// dataflow (per-lane query fragments, K / V^T term images, S^T = K Q^T and O^T = V^T P^T on fp16x2 or bf16x3
+// terms) with the window's keys streamed in 128-key blocks and an online softmax: the running maximum
+// rescales the accumulator by exp2(m_old - m_new), so every block's probabilities stay in (0, 1] (the 2^14
+// fp16 scale of P holds).  One workgroup per (window, 128-query block, head), XCD-aware numbering.
+template <int D, bool F16>
+__global__ void __launch_bounds__(256, D == 16 ? 4 : 3)
+window_attn_split_flash_kernel(const float* __restrict__ qkv, const int* __restrict__ order,
+                               const int* __restrict__ win3, int qblocks, int C, float scale, float* __restrict__ out,
+                               const unsigned long long* __restrict__ qkv_amax, unsigned qkv_tag, int nwin) {
+  typedef typename std::conditional<F16, _Float16, __bf16>::type elem_t;
+  typedef elem_t bf16x8 __attribute__((ext_vector_type(8)));  // (fragment type: bf16 or fp16 terms)
+  constexpr int NT = F16 ? 2 : 3;            // terms per operand
+  constexpr int KD = D == 16 ? 16 : 32;
+  constexpr int NKS = KD / 16;
+  constexpr int QROW = KD == 16 ? 48 : 64;  // bytes per Q/K term row
+  constexpr int VST = 136;                  // V^T row stride (16-bit elements)
+  constexpr int QK_BYTES = NT * KMAX * QROW;
+  constexpr int V_BYTES = NT * D * VST * 2;
+  // operand scales (F16): qkv by sq, probabilities by 2^14
+  float sq = 1.f, iq = 1.f;
+  if constexpr (F16) {
+    const float m = sfx::read_amax(qkv_amax, qkv_tag);
+    int e = 0;
+    if (m > 0.f && m <= 3.4028235e38f) {
+      (void)frexpf(m, &e);
+      e = 15 - e;
+      e = e > 126 ? 126 : (e < -126 ? -126 : e);
+    }
+    sq = ldexpf(1.f, e);
+    iq = ldexpf(1.f, -e);
+  }
+  auto split = [&](float4 v, float sc, uint2 (&t)[NT]) {
+    if constexpr (F16) sfx::split2h(v, sc, t); else sfx::split3(v, t);
+  };
+  __shared__ __attribute__((aligned(16))) char lds[QK_BYTES + V_BYTES];
+  __shared__ int rows[KMAX];   // keys of the current block
+  __shared__ int qrows[KMAX];  // this workgroup's queries
+  char* Ks = lds;
+  unsigned short* Vt = reinterpret_cast<unsigned short*>(lds + QK_BYTES);
+  // byte offset of 16-byte chunk c of term row r
+  auto qk_off = [](int r, int c) -> int {
+    return KD == 16 ? r * 48 + c * 16 : r * 64 + (((c ^ (r >> 2)) & 3) << 4);
+  };
+
+  // XCD-aware numbering over a 1-D grid padded to a multiple of 8: consecutive blocks go round-robin to the 8
+  // XCDs, so logical id L = xcd * (grid / 8) + slot puts all heads of a window on one XCD back to back -- the
+  // 128-byte qkv lines its heads share (d = 16: two heads per line) are fetched from HBM once into that L2.
+  const int heads = C / D;
+  const int nb = (int)gridDim.x;
+  const int L = (int)(blockIdx.x % 8) * (nb / 8) + (int)(blockIdx.x / 8);
+  if (L >= nwin * qblocks * heads) return;
+  const int wq = L / heads, head = L - wq * heads;
+  const int w = wq / qblocks, qb = wq - w * qblocks;
+  const int key_start = win3[3 * w], query_start = win3[3 * w + 1], count = win3[3 * w + 2];
+  const int q0 = qb * KMAX;
+  if (q0 >= count || key_start + q0 + KMAX <= query_start) return;  // workgroup-uniform, before any barrier
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, h = lane >> 5, l32 = lane & 31;
+  const long long ld = 3ll * C;
+
+  if (tid < KMAX) qrows[tid] = q0 + tid < count ? order[key_start + q0 + tid] : -1;
+  // zero padding: K columns D..KD-1 (never written by the staging below)
+  if (D < KD)
+    for (int rr = tid; rr < NT * KMAX; rr += 256)  // term rows, term-major
+      *reinterpret_cast<uint4*>(Ks + qk_off(rr, D / 8)) = make_uint4(0, 0, 0, 0);
+  __syncthreads();
+  // gather + split, one matrix at a time (wave-uniform paths): q, k rows as KMAX x D/4 float4; v as
+  // key pairs x D/4 float4 so the transposed V^T writes are whole dwords (keys 2m, 2m+1 are adjacent
+  // in the permuted order)
+  constexpr int CH = D / 4;
+  typedef unsigned uintx4 __attribute__((ext_vector_type(4)));
+  // this lane's query slices (B operand of S^T = K Q^T): dd = 16 ks + 8h + j, zero past D
+  bf16x8 qf[NKS][NT];
+  {
+    const int src = qrows[32 * wid + l32];
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      const int d0 = 16 * ks + 8 * h;
+      float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+      if (src >= 0 && d0 < D) {
+        const float* qp = qkv + (long long)src * ld + head * D + d0;
+        a = *reinterpret_cast<const float4*>(qp);
+        if (d0 + 4 < D) b = *reinterpret_cast<const float4*>(qp + 4);
+      }
+      // scale * log2(e) folded into q: the softmax exponentials are plain exp2
+      const float qs = scale * 1.4426950408889634f;
+      a.x *= qs; a.y *= qs; a.z *= qs; a.w *= qs;
+      b.x *= qs; b.y *= qs; b.z *= qs; b.w *= qs;
+      uint2 ta[NT], tb[NT];
+      split(a, sq, ta);  // (|q * qs| <= |q|: the qkv bound holds)
+      split(b, sq, tb);
+#pragma unroll
+      for (int q = 0; q < NT; ++q) qf[ks][q] = __builtin_bit_cast(bf16x8, (uintx4){ta[q].x, ta[q].y, tb[q].x, tb[q].y});
+    }
+  }
+  // term products, smallest first
+  constexpr int NP = F16 ? 3 : 6;
+  constexpr int QA[6] = {F16 ? 1 : 2, F16 ? 0 : 1, 0, 1, 0, 0}, QB[6] = {0, 1, F16 ? 0 : 2, 0, 1, 0};
+  auto mfma = [](const bf16x8& a, const bf16x8& b, floatx16 c) -> floatx16 {
+    if constexpr (F16) return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+    else return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+  };
+  float m_run = -INFINITY, l_run = 0.f;
+  floatx16 o;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) o[r] = 0.f;
+
+  for (int k0 = 0; k0 < count; k0 += KMAX) {
+    const int nk = min(KMAX, count - k0);
+    __syncthreads();  // the previous block's fragment reads are done
+    if (tid < KMAX) rows[tid] = tid < nk ? order[key_start + k0 + tid] : -1;
+    __syncthreads();
+    for (int e = tid; e < KMAX * CH; e += 256) {
+      const int row = e / CH, ch = e - row * CH;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      const int src = rows[row];
+      if (src >= 0) v = *reinterpret_cast<const float4*>(qkv + (long long)src * ld + C + head * D + 4 * ch);
+      uint2 t[NT];
+      split(v, sq, t);
+      const int o = qk_off(row, ch >> 1) + ((ch & 1) << 3);
+#pragma unroll
+      for (int q = 0; q < NT; ++q) *reinterpret_cast<uint2*>(Ks + q * KMAX * QROW + o) = t[q];
+    }
+    for (int e = tid; e < (KMAX / 2) * CH; e += 256) {
+      const int kp = e / CH, ch = e - kp * CH;
+      const int row = 2 * kp;
+      const int s0 = rows[row], s1 = rows[row + 1];
+      float4 v0 = make_float4(0.f, 0.f, 0.f, 0.f), v1 = v0;
+      if (s0 >= 0) v0 = *reinterpret_cast<const float4*>(qkv + (long long)s0 * ld + 2 * C + head * D + 4 * ch);
+      if (s1 >= 0) v1 = *reinterpret_cast<const float4*>(qkv + (long long)s1 * ld + 2 * C + head * D + 4 * ch);
+      uint2 t0[NT], t1[NT];
+      split(v0, sq, t0);
+      split(v1, sq, t1);
+      const int kk = row & 15;  // even: keys row, row + 1 land on adjacent positions
+      const int pos = (row & ~15) + 8 * ((kk >> 2) & 1) + (((kk >> 3) << 2) | (kk & 3));
+#pragma unroll
+      for (int q = 0; q < NT; ++q) {
+        unsigned* vt = reinterpret_cast<unsigned*>(Vt + (q * D + 4 * ch) * VST + pos);
+        vt[0] = (t0[q].x & 0xffffu) | (t1[q].x << 16);
+        vt[VST / 2] = (t0[q].x >> 16) | (t1[q].x & 0xffff0000u);
+        vt[VST] = (t0[q].y & 0xffffu) | (t1[q].y << 16);
+        vt[3 * VST / 2] = (t0[q].y >> 16) | (t1[q].y & 0xffff0000u);
+      }
+    }
+    __syncthreads();
+
+    // S^T[key][query] for this wave's 32 queries, 4 key blocks of 32
+    floatx16 s[4];
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s[kb][r] = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) {
+        bf16x8 kf[NT];
+#pragma unroll
+        for (int q = 0; q < NT; ++q)
+          kf[q] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(
+                                                 Ks + q * KMAX * QROW + qk_off(kb * 32 + l32, 2 * ks + h)));
+#pragma unroll
+        for (int j = 0; j < NP; ++j) s[kb] = mfma(kf[QA[j]], qf[ks][QB[j]], s[kb]);
+      }
+    }
+    if constexpr (F16) {  // S was formed from sq-scaled q and k
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s[kb][r] = s[kb][r] * iq * iq;
+    }
+    // online softmax over this key block (register axis + the other half-wave); keys >= nk are padding
+    if (nk < KMAX) {
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          if (key >= nk) s[kb][r] = -INFINITY;
+        }
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[kb][r]);
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    mx = fmaxf(mx, m_run);  // finite: every block holds at least one key
+    const float corr = __builtin_amdgcn_exp2f(m_run - mx);
+    float sum = 0.f;
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float e = __builtin_amdgcn_exp2f(s[kb][r] - mx);
+        s[kb][r] = e;
+        sum += e;
+      }
+    sum += __shfl_xor(sum, 32, 64);
+    l_run = l_run * corr + sum;
+    m_run = mx;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[r] *= corr;
+
+    // O^T[dd][query] += sum_key V^T[dd][key] P^T[key][query]
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        uint2 a[NT], b[NT];
+        // unnormalised exp values (0, 1] (F16: scaled by 2^14); 1/sum is applied to O
+        split(make_float4(s[kb][8 * st + 0], s[kb][8 * st + 1], s[kb][8 * st + 2], s[kb][8 * st + 3]), 16384.f, a);
+        split(make_float4(s[kb][8 * st + 4], s[kb][8 * st + 5], s[kb][8 * st + 6], s[kb][8 * st + 7]), 16384.f, b);
+        bf16x8 pf[NT], vf[NT];
+#pragma unroll
+        for (int q = 0; q < NT; ++q) {
+          pf[q] = __builtin_bit_cast(bf16x8, make_uint4(a[q].x, a[q].y, b[q].x, b[q].y));
+          uint4 vv = make_uint4(0, 0, 0, 0);  // dd = l32 >= D: zero rows of V^T
+          if (l32 < D) vv = *reinterpret_cast<const uint4*>(Vt + (q * D + l32) * VST + (2 * kb + st) * 16 + 8 * h);
+          vf[q] = __builtin_bit_cast(bf16x8, vv);
+        }
+#pragma unroll
+        for (int j = 0; j < NP; ++j) o = mfma(vf[QA[j]], pf[QB[j]], o);
+      }
+  }  // key blocks
+
+  const float rinv = 1.f / l_run;
+  const float oscale = F16 ? rinv * iq * (1.f / 16384.f) : rinv;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) o[r] *= oscale;
+  // scatter: query 32*wid + l32 (lane column), dd rows (r&3) + 8(r>>2) + 4h
+  const int qi = q0 + 32 * wid + l32;
+  if (qi < count && key_start + qi >= query_start) {
+    float* dst = out + (long long)qrows[32 * wid + l32] * C + head * D;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int dd = 8 * g + 4 * h;
+      if (dd + 3 < D) {
+        *reinterpret_cast<float4*>(dst + dd) = make_float4(o[4 * g + 0], o[4 * g + 1], o[4 * g + 2], o[4 * g + 3]);
+      }
+    }
+  }
+}
+
+
 // ---- backward (training, configs C/D) ---------------------------------------------------------------
 // Autograd of the non-flash attention math of visualize.py:140-179 for one (window, head):
 //   dV = P^T dO ; dP = dO V^T ; dS = P * (dP - rowsum(dO * O)) ; dQ = scale * dS K ; dK = dS^T (scale*Q)
@@ -998,7 +1243,7 @@ int sfx_window_attention(int num_windows, int window, int heads, int head_dim, i
 // flash mode: win3 [num_windows][3] = (key_start, query_start, key_count), key_count <= max_window
 int sfx_window_attention_varlen(int num_windows, int max_window, int heads, int head_dim, int channels,
                                 const float* qkv, const int* order, const int* win3, float scale, float* out,
-                                void* stream) {
+                                const unsigned long long* qkv_amax, unsigned qkv_tag, void* stream) {
   SFX_REQUIRE(num_windows >= 0, "sfx_window_attention_varlen: num_windows < 0");
   SFX_REQUIRE(max_window >= 1 && max_window <= (1 << 20), "sfx_window_attention_varlen: max_window out of [1, 2^20]");
   SFX_REQUIRE(heads * head_dim == channels, "sfx_window_attention_varlen: heads * head_dim != channels");
@@ -1007,16 +1252,38 @@ int sfx_window_attention_varlen(int num_windows, int max_window, int heads, int 
   if (num_windows == 0) return SFX_OK;
   SFX_REQUIRE(qkv && order && win3 && out, "sfx_window_attention_varlen: null buffer");
   const int qblocks = (max_window + KMAX - 1) / KMAX;
-  SFX_REQUIRE((long long)num_windows * qblocks < (1ll << 31) && heads <= 65535,
-              "sfx_window_attention_varlen: grid too large");
-  dim3 grid((unsigned)(num_windows * qblocks), heads);
+  const long long nblk = ((long long)num_windows * qblocks * heads + 7) / 8 * 8;
+  SFX_REQUIRE(nblk < (1ll << 31) && heads <= 65535, "sfx_window_attention_varlen: grid too large");
   hipStream_t st = sfx::as_stream(stream);
-  if (head_dim == 16)
-    window_attn_flash_kernel<16><<<grid, 256, 0, st>>>(qkv, order, win3, qblocks, channels, scale, out);
-  else if (head_dim == 24)
-    window_attn_flash_kernel<24><<<grid, 256, 0, st>>>(qkv, order, win3, qblocks, channels, scale, out);
-  else
-    window_attn_flash_kernel<32><<<grid, 256, 0, st>>>(qkv, order, win3, qblocks, channels, scale, out);
+  static int exact = -1;  // SFX_ATTN_PREC=fp32: the v_mfma_f32_32x32x2_f32 kernel
+  if (exact < 0) {
+    const char* e = getenv("SFX_ATTN_PREC");
+    exact = (e && e[0] == 'f') ? 1 : 0;
+  }
+  if (exact) {
+    dim3 grid((unsigned)(num_windows * qblocks), heads);
+    if (head_dim == 16)
+      window_attn_flash_kernel<16><<<grid, 256, 0, st>>>(qkv, order, win3, qblocks, channels, scale, out);
+    else if (head_dim == 24)
+      window_attn_flash_kernel<24><<<grid, 256, 0, st>>>(qkv, order, win3, qblocks, channels, scale, out);
+    else
+      window_attn_flash_kernel<32><<<grid, 256, 0, st>>>(qkv, order, win3, qblocks, channels, scale, out);
+    return sfx::check_launch("sfx_window_attention_varlen");
+  }
+#define SFX_ATTN(DD, F)                                                                                       \
+  window_attn_split_flash_kernel<DD, F><<<dim3((unsigned)nblk), 256, 0, st>>>(qkv, order, win3, qblocks, channels, \
+                                                                              scale, out, qkv_amax, qkv_tag,   \
+                                                                              num_windows)
+  if (qkv_amax) {  // fp16x2 terms (the caller bounds |qkv|)
+    if (head_dim == 16) SFX_ATTN(16, true);
+    else if (head_dim == 24) SFX_ATTN(24, true);
+    else SFX_ATTN(32, true);
+  } else {
+    if (head_dim == 16) SFX_ATTN(16, false);
+    else if (head_dim == 24) SFX_ATTN(24, false);
+    else SFX_ATTN(32, false);
+  }
+#undef SFX_ATTN
   return sfx::check_launch("sfx_window_attention_varlen");
 }
 

@@ -143,7 +143,8 @@ class Block(nn.Module):
         oi = point.order_type[self.attn.order_index]
         if self.attn.enable_flash:
             K, win3, nw = point_windows_flash(point, self.attn.patch_size_max)
-            a = ops.window_attention_varlen(qkv, point.order_phys[oi], win3, nw, K, self.attn.num_heads, C)
+            a = ops.window_attention_varlen(qkv, point.order_phys[oi], win3, nw, K, self.attn.num_heads, C,
+                                            qkv_amax=q_amax)
         else:
             K, win, nw = point_windows(point, self.attn.patch_size_max)
             a = ops.window_attention(qkv, point.order_phys[oi], win, nw, K, self.attn.num_heads, C, qkv_amax=q_amax)

@@ -25,7 +25,7 @@ _lib.register("sfx_layernorm", [I, I, P, L, P, P, F, P, L, P])
 _lib.register("sfx_cpe_residual_ln", [I, I, P, P, P, P, P, P, F, P, P, P])
 _lib.register("sfx_cpe_residual_ln_pairs", [I, I, P, P, P, L, P, P, P, P, P, F, P, P, P])
 _lib.register("sfx_window_attention", [I, I, I, I, I, P, P, P, F, P, P, I, P])
-_lib.register("sfx_window_attention_varlen", [I, I, I, I, I, P, P, P, F, P, P])
+_lib.register("sfx_window_attention_varlen", [I, I, I, I, I, P, P, P, F, P, P, I, P])
 _lib.register("sfx_serialize_keys", [I, P, P, I, I, I, I, I, I, I, P, P, P])
 _lib.register("sfx_serialize_finalize", [I, I, P, P, P, P])
 _lib.register("sfx_pool_run_flags", [I, I, P, P, I, P, P])
@@ -291,8 +291,10 @@ def window_table_varlen_np(offsets: Sequence[int], K: int) -> np.ndarray:
 
 
 def window_attention_varlen(qkv: Tensor, order: Tensor, win3: Tensor, num_windows: int, K: int, heads: int,
-                            channels: int, out: Optional[Tensor] = None) -> Tensor:
-    """Flash-mode attention (enable_flash=True, K = 1024): per-window key counts, online softmax (attention.hip)."""
+                            channels: int, out: Optional[Tensor] = None,
+                            qkv_amax: Optional[Tuple[int, int]] = None) -> Tensor:
+    """Flash-mode attention (enable_flash=True, K = 1024): per-window key counts, online softmax (attention.hip);
+    fp16x2 MFMA terms with an amax slot bounding |qkv|, bf16x3 otherwise (both fp32-accurate)."""
     n = qkv.shape[0]
     d = channels // heads
     if qkv.shape != (n, 3 * channels) or order.shape[0] != n or tuple(win3.shape) != (num_windows, 3):
@@ -301,7 +303,7 @@ def window_attention_varlen(qkv: Tensor, order: Tensor, win3: Tensor, num_window
     if out is None:
         out = torch.empty(n, channels, device=qkv.device, dtype=torch.float32)
     call("sfx_window_attention_varlen", num_windows, K, heads, d, channels, ptr(qkv), ptr(order, torch.int32),
-         ptr(win3, torch.int32), float(d ** -0.5), ptr(out), stream())
+         ptr(win3, torch.int32), float(d ** -0.5), ptr(out), *_slot_args(qkv_amax), stream())
     return out
 
 

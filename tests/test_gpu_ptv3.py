@@ -276,12 +276,14 @@ def test_window_attention_vs_reference_padding(device, n, heads, C, terms):
     assert rel_l2(out.cpu(), ref) < 2e-6
 
 
+@pytest.mark.parametrize("terms", ["bf16x3", "fp16x2"])
 @pytest.mark.parametrize("K", [1024, 256])
 @pytest.mark.parametrize("heads,C", [(2, 32), (4, 96), (8, 256)])
-def test_window_attention_flash_varlen(device, K, heads, C):
+def test_window_attention_flash_varlen(device, K, heads, C, terms):
     """enable_flash=True windows (pointtransformer_v3.py:121-123, K = 1024): batches of n < K (one n-key window),
     n == K, ragged n > K (last window padded with the preceding points) and n = 2K, one launch; vs the oracle's
-    cu_seqlens restatement in fp64 (online softmax over 128-key blocks vs one softmax: order of summation only)."""
+    cu_seqlens restatement in fp64 (online softmax over 128-key blocks vs one softmax: order of summation only).
+    Both MFMA term forms (fp16x2 from an 8x loose amax slot)."""
     counts = [700, K, 2 * K + 333, 2 * K, 5, 1]
     n = sum(counts)
     offset = torch.tensor(counts).cumsum(0)
@@ -295,12 +297,19 @@ def test_window_attention_flash_varlen(device, K, heads, C):
     ref = ptv3_ref.serialized_attention_flash(qkv, point, C, heads, K, 0)
     tab = ops.window_table_varlen_np(offset.tolist(), K)
     win3 = torch.from_numpy(tab).to(device)
-    out = ops.window_attention_varlen(qkv.float().to(device), order.int().to(device), win3, tab.shape[0], K, heads, C)
+    qd = qkv.float().to(device)
+    slot = None
+    if terms == "fp16x2":
+        slot = ops.new_amax(qd.device)
+        big = qd * 8  # a loose bound must do as well as the exact one
+        from splatformer_amd._lib import call, ptr, stream
+        call("sfx_amax_f32", n, 3 * C, ptr(big), 3 * C, slot[0], slot[1], stream())
+    out = ops.window_attention_varlen(qd, order.int().to(device), win3, tab.shape[0], K, heads, C, qkv_amax=slot)
     assert rel_l2(out.cpu(), ref) < 2e-6
     # every point written exactly once (no stale rows): a NaN-filled output buffer comes back NaN-free
     out2 = torch.full((n, C), float("nan"), device=device)
-    ops.window_attention_varlen(qkv.float().to(device), order.int().to(device), win3, tab.shape[0], K, heads, C,
-                                out=out2)
+    ops.window_attention_varlen(qd, order.int().to(device), win3, tab.shape[0], K, heads, C, out=out2,
+                                qkv_amax=slot)
     assert torch.equal(out2.cpu(), out.cpu())
 
 
