@@ -188,15 +188,17 @@ class SerializedPooling(nn.Module):
     def geometry_begin(self, point: Point):
         return ops.pool_geometry_begin(point.codes_phys, point.order_phys, self._pd(point))
 
-    def geometry_end(self, point: Point, perm: Sequence[int], state):
+    def geometry_end(self, point: Point, perm: Sequence[int], state, m: Optional[int] = None,
+                     deferred: Optional[list] = None):
         """The integer half of SerializedPooling.forward: clusters (code >> 3*pd, unique), their members
-        (sidx / idx_ptr CSR), the pooled coords, codes, orders and neighbour map.  -> (new Point, sidx, idx_ptr, m)"""
+        (sidx / idx_ptr CSR), the pooled coords, codes, orders and neighbour map.  -> (new Point, sidx, idx_ptr, m)
+        m: the cluster count when already known (PointTransformerV3.forward's pool_counts_begin)."""
         pd = self._pd(point)
         depth = point.serialized_depth - pd
         code_bits = point.code_bits - 3 * pd
         sidx, cluster, idx_ptr, m, codes, order, inverse, grid, batch = ops.pool_geometry_end(
             state, point.codes_phys, point.order_phys, point.order_type[0], pd, point.grid_coord, point.get("batch"),
-            point.code_bits)
+            point.code_bits, m=m, deferred=deferred)
         coord = ops.segment_mean(point.coord, idx_ptr, sidx, m)
         new = Point(coord=coord, grid_coord=grid, codes_phys=codes, order_phys=order,
                     inverse_phys=inverse, order_type=[point.order_type[p] for p in perm],
@@ -212,11 +214,11 @@ class SerializedPooling(nn.Module):
     def geometry(self, point: Point, perm: Sequence[int]):
         return self.geometry_end(point, perm, self.geometry_begin(point))
 
-    def run(self, point: Point, perm: Sequence[int]) -> Point:
+    def run(self, point: Point, perm: Sequence[int], m: Optional[int] = None, deferred: Optional[list] = None) -> Point:
         st = self.geometry_begin(point)
         # the projection does not depend on the clusters: enqueued while the host waits for the pooled count
         pf = ops.linear(point.feat, self.proj.weight, self.proj.bias)
-        new, sidx, idx_ptr, m = self.geometry_end(point, perm, st)
+        new, sidx, idx_ptr, m = self.geometry_end(point, perm, st, m, deferred)
         sc, sh = bn_affine(self.norm[0])
         new.feat = ops.segment_max_affine_act(pf, idx_ptr, sidx, m, sc, sh, ops.ACT_GELU)
         return new
@@ -381,12 +383,22 @@ class PointTransformerV3(nn.Module):
         emb_feat = ops.linear(feat, emb.weight, emb.bias, scale=sc, shift=sh, act=ops.ACT_GELU)
         point = self.prepare(data_dict, perms)
         point.feat = emb_feat
+        # every pooling's cluster count from the stage-0 codes, read back while stage 0 runs: no pooling waits
+        pools = [getattr(self.enc, f"enc{s}").down for s in range(1, self.num_stages)]
+        shifts, depth, cum = [], point.serialized_depth, 0
+        for mod in pools:
+            pd = (math.ceil(mod.stride) - 1).bit_length()
+            pd = 0 if pd > depth else pd
+            depth, cum = depth - pd, cum + pd
+            shifts.append(3 * cum)
+        counts_rd = ops.pool_counts_begin(point.codes_phys, point.order_phys, shifts)
+        deferred: list = []
         k = 1
         for s in range(self.num_stages):
             stage = getattr(self.enc, f"enc{s}")
             for name, mod in stage.named_children():
                 if name == "down":
-                    point = mod.run(point, self._draw_perm(perms, k))
+                    point = mod.run(point, self._draw_perm(perms, k), m=counts_rd.get()[k - 1], deferred=deferred)
                     k += 1
                 else:
                     point = mod.run(point)
@@ -401,6 +413,8 @@ class PointTransformerV3(nn.Module):
                     conv_in = point.pop("stale_conv_feat", None)
                     last = di == len(dec_names) - 1 and ci == len(children) - 1
                     point = mod.run(point, conv_in=conv_in, out=out if last else None)
+        for rd, m in deferred:  # (the whole refine is enqueued: this wait starves nothing)
+            ops.check_pool_runs(rd.get(), m)
         return point
 
 

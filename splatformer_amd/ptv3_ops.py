@@ -351,10 +351,11 @@ def serialize(grid_coord: Tensor, batch: Optional[Tensor], depth: int, code_bits
     return codes, order, inverse
 
 
-def scan_i32(x: Tensor, inclusive: bool = True) -> Tuple[Tensor, Tensor]:
+def scan_i32(x: Tensor, inclusive: bool = True, total: Optional[Tensor] = None) -> Tuple[Tensor, Tensor]:
     n = x.shape[0]
     out = torch.empty_like(x)
-    total = torch.zeros(1, device=x.device, dtype=torch.int32)
+    if total is None:
+        total = torch.zeros(1, device=x.device, dtype=torch.int32)
     ws = _lib.workspace(_lib.fn("sfx_scan_workspace_bytes")(n), x.device)
     call("sfx_scan_i32", n, ptr(x), ptr(out), 1 if inclusive else 0, ptr(ws), ws.numel(), ptr(total), stream())
     return out, total
@@ -371,18 +372,43 @@ def pool_geometry_begin(codes: Tensor, order: Tensor, pooling_depth: int):
     return flags, pos, _lib.HostRead(pos.view(R, n)[:, -1])
 
 
+def pool_counts_begin(codes: Tensor, order: Tensor, shifts: Sequence[int]) -> "_lib.HostRead":
+    """The cluster counts of every pooling of a forward, from the stage-0 serialization alone: codes are
+    hierarchical (a pooling keeps the head's code >> 3pd), so the m of the pooling reached after cumulative shift
+    k is the number of runs of code0 >> k along serialized row 0 -- one flag pass + scan per pooling, read back in
+    one asynchronous copy.  The forward then never waits for a pooled count (pool_geometry_end(m=...))."""
+    n = codes.shape[1]
+    counts = torch.zeros(max(len(shifts), 1), device=codes.device, dtype=torch.int32)
+    flags = torch.empty(n, device=codes.device, dtype=torch.int32)
+    for i, sh in enumerate(shifts):
+        call("sfx_pool_run_flags", n, 1, ptr(order[0], torch.int32), ptr(codes[0], torch.int64), sh, ptr(flags),
+             stream())
+        scan_i32(flags, total=counts[i:i + 1])
+    return _lib.HostRead(counts)
+
+
+def check_pool_runs(ends: Sequence[int], m: int) -> None:
+    runs = [ends[0]] + [ends[r] - ends[r - 1] for r in range(1, len(ends))]
+    if any(c != m for c in runs):
+        raise RuntimeError(f"sfx pooling: order rows count cluster runs {runs}, expected {m}; the serialization codes "
+                           "are not hierarchical (code >> 3 must be the parent cell's code)")
+
+
 def pool_geometry_end(state, codes: Tensor, order: Tensor, row0: int, pooling_depth: int, grid_coord: Tensor,
-                      batch: Optional[Tensor], code_bits: int):
+                      batch: Optional[Tensor], code_bits: int, m: Optional[int] = None,
+                      deferred: Optional[list] = None):
+    """m (from pool_counts_begin) skips the wait for this pooling's count; the per-row run counts are then checked
+    later by the caller from `deferred` ((HostRead, m) pairs)."""
     flags, pos, ends_rd = state
     R, n = codes.shape
     dev = codes.device
     shift = 3 * pooling_depth
-    ends = ends_rd.get()  # the pooled point count sizes every later buffer
-    runs = [ends[0]] + [ends[r] - ends[r - 1] for r in range(1, R)]
-    m = runs[0]
-    if any(c != m for c in runs):
-        raise RuntimeError(f"sfx pooling: order rows count different cluster runs {runs}; the serialization codes "
-                           "are not hierarchical (code >> 3 must be the parent cell's code)")
+    if m is None:
+        ends = ends_rd.get()  # the pooled point count sizes every later buffer
+        m = ends[0]
+        check_pool_runs(ends, m)
+    else:
+        deferred.append((ends_rd, m))
     cluster = torch.empty(n, device=dev, dtype=torch.int32)
     sidx = torch.empty(n, device=dev, dtype=torch.int32)
     idx_ptr = torch.empty(m + 1, device=dev, dtype=torch.int32)
