@@ -163,9 +163,21 @@ def _render_fused_views(gs, c2ws, cameras, meta=None):
     call("sfx_render_prep_project_views", n, V, nb, pm, lm, ps, ls, pq, lq, po, lo, pd, ldc, pr, lr, ptr(cams), fx, fy,
          cx, cy, H, W, BLOCK_WIDTH, ptr(rgbs), ptr(opac), ptr(xys), ptr(depths), ptr(radii), ptr(conics), ptr(tiles),
          stream())
-    total, cum = compute_cumulative_intersects(tiles)
+    # inclusive scan of the tiles hit; the per-view ends (and the total = the last of them) reach the host in ONE
+    # asynchronous read, with the count-independent record packing enqueued in front of the wait
+    cum = torch.empty(V * n, device=dev, dtype=torch.int32)
+    rec = f(V * n, 12)  # packed 48-byte records: one gather per Gaussian in the rasterizer's batch fetch
+    if n:
+        tot_dev = torch.zeros(1, device=dev, dtype=torch.int32)
+        ws = _lib.workspace(_lib.fn("sfx_scan_workspace_bytes")(V * n), dev)
+        call("sfx_scan_i32", V * n, ptr(tiles), ptr(cum), 1, ptr(ws), ws.numel(), ptr(tot_dev), stream())
+        ends_rd = _lib.HostRead(cum.view(V, n)[:, -1])
+        call("sfx_pack_raster_records", V * n, ptr(xys), ptr(conics), ptr(rgbs), ptr(opac), ptr(rec), stream())
+        ends = ends_rd.get()
+    else:
+        ends = [0] * V
+    total = ends[-1]
     # per-view intersection counts (gsplat's empty-image branch is per call: alpha = 1 there)
-    ends = cum.view(V, n)[:, -1].tolist() if n else [0] * V
     per_view = [ends[0]] + [ends[v] - ends[v - 1] for v in range(1, V)]
     bw = BLOCK_WIDTH
     tiles_x, tiles_y = (W + bw - 1) // bw, (H + bw - 1) // bw
@@ -186,8 +198,6 @@ def _render_fused_views(gs, c2ws, cameras, meta=None):
         bins = f(V * T, 2, dt=torch.int32)
         call("sfx_tile_bins", total, ptr(isect_s), V * T, ptr(bins), stream())
         final_Ts, final_idx = f(V, H, W), f(V, H, W, dt=torch.int32)
-        rec = f(V * n, 12)  # packed 48-byte records: one gather per Gaussian in the rasterizer's batch fetch
-        call("sfx_pack_raster_records", V * n, ptr(xys), ptr(conics), ptr(rgbs), ptr(opac), ptr(rec), stream())
         call("sfx_rasterize_fwd_views_packed", V, tiles_x, tiles_y, bw, H, W, ptr(gids_s), ptr(bins), ptr(rec),
              ptr(bg), 1, ptr(final_Ts), ptr(final_idx), ptr(out), ptr(alpha), stream())
     for v in range(V):

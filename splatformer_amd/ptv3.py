@@ -20,6 +20,7 @@ parameters) is `ptv3_train.py`, driven by `train.Trainer`.
 from __future__ import annotations
 
 import math
+import os
 from typing import Dict, List, Optional, Sequence
 
 import torch
@@ -30,6 +31,8 @@ from . import _lib
 from . import ptv3_ops as ops
 
 ORDERS = ("z", "z-trans", "hilbert", "hilbert-trans")
+# every pooling's cluster count from the stage-0 codes up front (default); SFX_POOL_COUNTS_UPFRONT=0 waits per pooling
+POOL_COUNTS_UPFRONT = os.environ.get("SFX_POOL_COUNTS_UPFRONT", "1") != "0"
 
 
 class Point(dict):
@@ -391,14 +394,15 @@ class PointTransformerV3(nn.Module):
             pd = 0 if pd > depth else pd
             depth, cum = depth - pd, cum + pd
             shifts.append(3 * cum)
-        counts_rd = ops.pool_counts_begin(point.codes_phys, point.order_phys, shifts)
+        counts_rd = ops.pool_counts_begin(point.codes_phys, point.order_phys, shifts) if POOL_COUNTS_UPFRONT else None
         deferred: list = []
         k = 1
         for s in range(self.num_stages):
             stage = getattr(self.enc, f"enc{s}")
             for name, mod in stage.named_children():
                 if name == "down":
-                    point = mod.run(point, self._draw_perm(perms, k), m=counts_rd.get()[k - 1], deferred=deferred)
+                    m = counts_rd.get()[k - 1] if counts_rd is not None else None
+                    point = mod.run(point, self._draw_perm(perms, k), m=m, deferred=deferred)
                     k += 1
                 else:
                     point = mod.run(point)
