@@ -57,6 +57,13 @@ SPLIT_PEAK_TFLOPS = round(F16_MFMA_PEAK_TFLOPS / 3, 1)
 HBM_PEAK_GBS = 8000.0
 GEMM_FAMILY = ("gemm_kernel", "wgrad_kernel")  # kernel-name prefixes of the dominant family
 
+
+def in_family(kernel_name: str) -> bool:
+    """GEMM-family dispatch: the GEMM kernels, and the LayerNorm kernel that sums SubM pair partials (the
+    conv's own reduction when it stores per-pair rows: `cpe_residual_ln4_kernel<G, NV, true>`)."""
+    return any(p in kernel_name for p in GEMM_FAMILY) or (
+        "cpe_residual_ln4_kernel<" in kernel_name and ", true>" in kernel_name)
+
 DEFAULTS = {  # n, res, views, sh, batch
     "A": (20_000, "256", 4, 0, 1), "B": (100_000, "800", 9, 1, 1), "C": (100_000, "800", 4, 1, 8),
     "D": (100_000, "800", 4, 1, 4), "E": (500_000, "1920x1080", 9, 3, 1)}
@@ -77,6 +84,7 @@ def parse(argv=None):
     ap.add_argument("--flash", action="store_true",
                     help="PointTransformerV3Model.enable_flash=True (K=1024 windows, pointtransformer_v3.py:121-123)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-psnr", action="store_true", help="skip the PSNR delta vs the oracle (eval configs)")
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC passes")
     ap.add_argument("--cpu-sample", type=int, default=None,
                     help="Gaussians in the CPU-oracle sample (default: the whole scene for A, 20000 otherwise)")
@@ -158,13 +166,18 @@ def _gemm_cost(kind, args, kw, res):
         cin = dx.shape[1]
         fl = 2.0 * (n + smap.num_pairs) * cin * cout
         return fl, (n * cout + 27 * cin * cout + 2 * n * cin + 27 * n) * f4, (n, cin, cout)
+    if kind == "cpe_residual_ln":  # timed only with SubM pair partials: the conv's own pair summation
+        return 0.0, 0, tuple(args[1].shape)
     raise KeyError(kind)
 
 
 class GemmTimer:
     """Wraps the GEMM-family entry points (ptv3_ops.linear / subm_conv / grouped_linear, train_ops
     linear_bwd_data / linear_wgrad / subm_conv_bwd_data) for one pass of real work: HIP events recorded on the
-    launch stream around each launch, in the real launch sequence (no replay, caches as they are)."""
+    launch stream around each launch, in the real launch sequence (no replay, caches as they are).  A SubM conv
+    that stores per-pair partial rows (ptv3_ops.SubmPartials) finishes in its consumer, cpe_residual_ln, which
+    sums them: those launches are timed with the family too (0 FLOP), so the family's TF/s covers the whole
+    conv."""
 
     def __init__(self):
         self.calls = []
@@ -174,16 +187,19 @@ class GemmTimer:
         self._saved = []
         for mod, name in [(ptv3_ops, "linear"), (ptv3_ops, "subm_conv"), (ptv3_ops, "grouped_linear"),
                           (train_ops, "linear_bwd_data"), (train_ops, "linear_wgrad"),
-                          (train_ops, "subm_conv_bwd_data")]:
+                          (train_ops, "subm_conv_bwd_data"), (ptv3_ops, "cpe_residual_ln")]:
             fn = getattr(mod, name)
             self._saved.append((mod, name, fn))
             setattr(mod, name, self._wrap(name, fn))
         return self
 
     def _wrap(self, kind, fn):
+        from splatformer_amd import ptv3_ops
         rec = self
 
         def wrapped(*args, **kw):
+            if kind == "cpe_residual_ln" and not isinstance(args[0], ptv3_ops.SubmPartials):
+                return fn(*args, **kw)  # (a LayerNorm, not part of the GEMM family)
             st = torch.cuda.current_stream()  # the stream libsfx launches on (_lib.stream())
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(st)
@@ -270,7 +286,7 @@ def _per_unit(csv_path, counter):
         raise RuntimeError(f"{counter}: {len(marks)} profile markers in {csv_path}")
     units = []
     for a, b in zip(marks[:-1], marks[1:]):
-        units.append(sum(v for d, k, v in rows if a < d < b and any(p in k for p in GEMM_FAMILY)) * 1024.0)
+        units.append(sum(v for d, k, v in rows if a < d < b and in_family(k)) * 1024.0)
     return statistics.median(units), len(units)
 
 
@@ -411,6 +427,38 @@ def cpu_baseline_train(scene_cpu, cams_cpu, sd0, sample_n, n_total, views, scene
     }
 
 
+# ---- PSNR delta vs the oracle (eval configs) ---------------------------------------------------------------
+def psnr_delta(model, scene, scene_cpu, cams, cams_cpu, sd_cpu, cfg_kw, sh, view=0):
+    """the PSNR delta vs the oracle on the same inputs, on one view of the benchmarked scene --
+    the HIP pipeline (refine + render) against the oracle pipeline (oracle refine with the same weights and
+    order shuffles, oracle render), both scored as the reference's evaluation does (uint8 truncation,
+    train.py:104-113; psnr on /255, utils/metrics.py:89-91) against the same target: the render of the
+    unrefined input scene (synthetic data has no ground-truth photo).  Outside the timed region."""
+    from oracle import gsplat_ref, ptv3_ref, render_ref
+    from splatformer_amd.gs_render import rasterize_gaussians_to_singleimg
+    threads, _, _ = cpu_threads()
+    torch.set_num_threads(threads)
+    t0 = time.perf_counter()
+    with torch.no_grad():
+        out = model([scene], [0])[0]
+        perms = [list(p) for p in model.backbone.backbone.last_perms]
+        c2w = cams["camera_to_worlds"][view]
+        hip = rasterize_gaussians_to_singleimg(out, c2w, **cams)[0].cpu()
+        gt = rasterize_gaussians_to_singleimg(scene, c2w, **cams)[0].cpu()
+    cfg = ptv3_ref.PTv3Config(in_channels=sd_cpu["backbone.backbone.embedding.0.weight"].shape[1], **cfg_kw)
+    if cfg.enable_flash:
+        cfg.patch_size = 1024  # (the flash branch's patch, pointtransformer_v3.py:121-123)
+    ref, _ = ptv3_ref.feature_predictor_forward(sd_cpu, cfg, scene_cpu, perms, sh_degree=sh)
+    orc, _ = render_ref.rasterize_gaussians_to_singleimg(ref, cams_cpu["camera_to_worlds"][view], **cams_cpu)
+    p_hip = float(gsplat_ref.psnr_u8(hip[None], gt[None]))
+    p_orc = float(gsplat_ref.psnr_u8(orc[None], gt[None]))
+    return {"psnr_delta_db": round(p_hip - p_orc, 7), "view": view, "psnr_hip_db": round(p_hip, 5),
+            "psnr_oracle_db": round(p_orc, 5), "max_abs_pixel_diff": float((hip - orc).abs().max()),
+            "target": "render of the unrefined input scene (same view)",
+            "oracle": f"oracle/ptv3_ref + oracle/render_ref, whole scene, {threads} threads, "
+                      f"{time.perf_counter() - t0:.1f}s"}
+
+
 # ---- main -----------------------------------------------------------------------------------------------------
 def main(argv=None):
     args = parse(argv)
@@ -519,6 +567,10 @@ def main(argv=None):
         else:
             cpu = cpu_baseline(scene_cpu, cams_cpu, sd_cpu, bk, sample, args.n, args.views, args.sh)
 
+    psnr = None
+    if rank == 0 and world == 1 and not train and not args.no_psnr and not args.profile_only:
+        psnr = psnr_delta(model, scene, scene_cpu, cams, cams_cpu, sd_cpu, bk, args.sh)
+
     if rank == 0:
         res = f"{args.width}x{args.height}"
         unit_name = "one training micro-step (train fwd + bwd of one scene)" if train else "one refine"
@@ -556,6 +608,7 @@ def main(argv=None):
                        "attention": "flash (K=1024 varlen)" if args.flash else "non-flash (K=128, ptv3_base.gin:27)"},
             "roofline": roof,
             "cpu_baseline": cpu,
+            "psnr": psnr,
         }
         print(json.dumps(line), flush=True)
     if multi:

@@ -62,15 +62,12 @@ using namespace sfxg;
 // waves rescale that row's accumulators before adding it.  The epilogue unscales each row by its final 1/s.
 // Error: that of fp32 arithmetic (dropped l*l <= 2^-22 relative, products exact in fp32) for every row,
 // whatever the other rows' magnitudes.
-//
-// SPL = 4: fp16x2 with A pre-split as well (sfx_split_rows layout, one scale per source row over the whole
-// row): the staging threads only copy both operands' term images, no split, no overflow check, no rescale.
 template <int BM, int BN, int WGM, int NW, bool VEC, int MODE, int SPL>
 __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs p, int tiles_n, int total_tiles) {
   constexpr bool SPLIT = SPL != 0;
-  constexpr bool F16 = SPL == 2 || SPL == 4;  // fp16x2 terms (A split in-kernel / pre-split)
+  constexpr bool F16 = SPL == 2;               // fp16x2 terms
   constexpr int NTERM = F16 ? 2 : 3;          // LDS term images per operand
-  static_assert(SPL == 0 || SPL == 2 || SPL == 3 || SPL == 4, "operand precision");
+  static_assert(SPL == 0 || SPL == 2 || SPL == 3, "operand precision");
   constexpr int NT = NW * 64;                  // threads
   constexpr int WGN = NW / WGM;                // waves along N
   constexpr int WM = BM / WGM, WN = BN / WGN;  // wave sub-tile
@@ -102,7 +99,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs
   int* s_flag = reinterpret_cast<int*>(s_inv + 2 * BM);  // [NBUF]
 
   const int g = blockIdx.z;
-  const float* A = (SPL == 4 ? p.Asp : p.A) + g * p.gA;
+  const float* A = p.A + g * p.gA;
   const float* bias = p.bias ? p.bias + g * p.gB : nullptr;
   float* Y = p.Y + g * p.gY;
   const __amdgpu_buffer_rsrc_t rA = rsrc(A);
@@ -119,7 +116,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs
     if (tid < NBUF) s_flag[tid] = 0;  // (published by the first barrier)
   }
   // byte offsets fit 31 bits (host checks every operand against the 2 GiB buffer range)
-  const unsigned lda32 = (unsigned)(SPL == 4 ? p.ldas : p.lda), ldw32 = (unsigned)p.ldw, ldy32 = (unsigned)p.ldy, ldws32 = (unsigned)p.ldws;
+  const unsigned lda32 = (unsigned)p.lda, ldw32 = (unsigned)p.ldw, ldy32 = (unsigned)p.ldy, ldws32 = (unsigned)p.ldws;
   const unsigned ldr32 = (unsigned)p.ldr, ldp32 = (unsigned)p.ldypre;
   const int lrow = tid >> 3, lcol = (tid & 7) * 4;  // staging coordinates: rows lrow + RPP i, cols lcol..+3
 
@@ -178,7 +175,6 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs
   };
 
   float4 ra[A_ITERS], rw[W_ITERS];
-  float rinv[A_ITERS];  // SPL == 4: 1/s of the staged source rows (loaded with a segment's first slab)
   auto load_tiles = [&](const Tile& ti, int kt, bool first) {
     const __amdgpu_buffer_rsrc_t rW = rsrc(ti.W);
     const int k = kt * BK + lcol;
@@ -198,14 +194,6 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs
         off = (mok && r >= 0 && kin && seg < p.S) ? ((unsigned)r * lda32 + (unsigned)kk) * 4u : OOB;
       } else {
         off = (mok && kin) ? ((unsigned)m * lda32 + (unsigned)kk) * 4u : OOB;
-      }
-      if constexpr (SPL == 4) {
-        if (first) {
-          unsigned ioff;
-          if constexpr (MODE != MODE_DENSE) ioff = (mok && grow[i] >= 0) ? (unsigned)grow[i] * 4u : OOB;
-          else ioff = mok ? (unsigned)m * 4u : OOB;
-          rinv[i] = bload1(rsrc(p.ainv), ioff);
-        }
       }
       if (VEC) {
         ra[i] = bload4(rA, off);
@@ -246,27 +234,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs
   auto store_tiles = [&](int buf, bool first, int par) {
     if constexpr (SPLIT) {
       const int b = NBUF == 2 ? buf : 0;
-      if constexpr (SPL == 4) {  // both operands pre-split: copy the h / l halves into the term images
-        if (first && (tid & 7) == 0) {
-#pragma unroll
-          for (int i = 0; i < A_ITERS; ++i) s_inv[par * BM + lrow + RPP * i] = rinv[i];
-        }
-#pragma unroll
-        for (int i = 0; i < A_ITERS; ++i) {
-          const uint4 w = __builtin_bit_cast(uint4, ra[i]);
-          const int o = swz(lrow + RPP * i, lcol >> 2);
-          *reinterpret_cast<uint2*>(sAs + ((b * 2 + 0) * BM) * 64 + o) = make_uint2(w.x, w.y);
-          *reinterpret_cast<uint2*>(sAs + ((b * 2 + 1) * BM) * 64 + o) = make_uint2(w.z, w.w);
-        }
-#pragma unroll
-        for (int i = 0; i < W_ITERS; ++i) {
-          const uint4 w = __builtin_bit_cast(uint4, rw[i]);
-          const int o = swz(lrow + RPP * i, lcol >> 2);
-          *reinterpret_cast<uint2*>(sWs + ((b * 2 + 0) * BN) * 64 + o) = make_uint2(w.x, w.y);
-          *reinterpret_cast<uint2*>(sWs + ((b * 2 + 1) * BN) * 64 + o) = make_uint2(w.z, w.w);
-        }
-        return;
-      } else if constexpr (SPL == 2) {
+      if constexpr (SPL == 2) {
         ++sq;
         float m[A_ITERS];
         bool over = false;
@@ -901,18 +869,13 @@ void launch(GemmArgs a, int groups, bool vec, hipStream_t st) {
     if (grid_x >= 8) grid_x = (grid_x + 7) / 8 * 8;  // whole XCD groups for the XCD-aware numbering
   }
   dim3 grid(grid_x, 1, groups);
-  constexpr bool PRE_A = MODE != MODE_GATHERS;  // pre-split A exists for single-row-source modes
   if constexpr (NW == 8) {  // split-only tiles (vec operands)
-    if (PRE_A && a.split == 4)
-      gemm_kernel<BM, BN, WGM, 8, true, MODE, PRE_A ? 4 : 2><<<grid, 512, 0, st>>>(a, tiles_n, total);
-    else if (a.split == 2)
+    if (a.split == 2)
       gemm_kernel<BM, BN, WGM, 8, true, MODE, 2><<<grid, 512, 0, st>>>(a, tiles_n, total);
     else
       gemm_kernel<BM, BN, WGM, 8, true, MODE, 3><<<grid, 512, 0, st>>>(a, tiles_n, total);
   } else {
-    if (PRE_A && vec && a.split == 4)
-      gemm_kernel<BM, BN, WGM, 4, true, MODE, PRE_A ? 4 : 2><<<grid, 256, 0, st>>>(a, tiles_n, total);
-    else if (vec && a.split == 2)
+    if (vec && a.split == 2)
       gemm_kernel<BM, BN, WGM, 4, true, MODE, 2><<<grid, 256, 0, st>>>(a, tiles_n, total);
     else if (vec && split)
       gemm_kernel<BM, BN, WGM, 4, true, MODE, 3><<<grid, 256, 0, st>>>(a, tiles_n, total);
@@ -1225,10 +1188,8 @@ void dispatch(const GemmArgs& a0, int groups, bool vec, hipStream_t st) {
   GemmArgs a = a0;
   a.split = vec ? split_mode(a.K) : 0;
   // fp16x2 needs the pre-split W (per-row scales of A' are chosen in the kernel); without one the launch runs the
-  // range-safe bf16x3 form.  SFX_GEMM_WS=1 routes fp16x2 launches to the warp-specialised kernel (gemm_ws.hip).
+  // range-safe bf16x3 form.
   if (a.split == 2 && !a.Wsp) a.split = 3;
-  if (a.split == 2 && a.Asp && groups == 1 && !(a.gidx && a.S != 1)) a.split = 4;  // A pre-split by the caller
-  if (a.split == 2 && launch_ws(a, groups, st)) return;
   if (a.pair_mode)
     dispatch_mode<MODE_PAIR>(a, groups, vec, st);
   else if (!a.gidx)
@@ -1239,105 +1200,33 @@ void dispatch(const GemmArgs& a0, int groups, bool vec, hipStream_t st) {
     launch<64, 128, 2, 4, MODE_GATHERS>(a, groups, vec, st);  // multi-segment gather: test/reference path only
 }
 
-// ---- pre-split A rows (split == 4) -------------------------------------------------------------------------
-// Row r of src (cols floats, row stride ld) -> dst row r in the pre-split layout (every 4 elements: 4 fp16 h
-// terms, then 4 fp16 l terms of x * 2^e_r), inv[r] = 2^-e_r with e_r = row_exp(max |row|) + 2 (the maximum in
-// [2^14, 2^15), like sfx_weight_split).  16 lanes per row, rows up to 512 wide held in registers.
-__global__ void __launch_bounds__(256) split_rows_kernel(int rows, int cols, const float* __restrict__ src,
-                                                         long long ld, float* __restrict__ dst,
-                                                         float* __restrict__ inv) {
-  const int row = (int)blockIdx.x * 16 + (int)(threadIdx.x >> 4);
-  const int l = threadIdx.x & 15;
-  if (row >= rows) return;  // whole 16-lane groups leave together
+// ---- weight pre-split: one wave per row -------------------------------------------------------------------
+// dst row n (contiguous, cols elements): per 4-element group, fp16 h terms then fp16 l terms of W[n, k] * 2^e_n,
+// with e_n putting the row's maximum in [2^14, 2^15) (0 for an all-zero row); inv[n] = 2^-e_n.
+__global__ void __launch_bounds__(256) weight_split_kernel(int rows, int cols, const float* __restrict__ src,
+                                                           long long ld, float* __restrict__ dst,
+                                                           float* __restrict__ inv) {
+  const int row = (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
   const float* s = src + (long long)row * ld;
-  constexpr int CH = 8;  // float4 chunks per lane kept in registers
-  float4 v[CH];
   float m = 0.f;
-#pragma unroll
-  for (int j = 0; j < CH; ++j) {
-    const int c = (l + 16 * j) * 4;
-    v[j] = c < cols ? *reinterpret_cast<const float4*>(s + c) : make_float4(0.f, 0.f, 0.f, 0.f);
-    m = fmaxf(m, fmaxf(fmaxf(fabsf(v[j].x), fabsf(v[j].y)), fmaxf(fabsf(v[j].z), fabsf(v[j].w))));
+  for (int c = lane * 4; c < cols; c += 256) {
+    const float4 v = *reinterpret_cast<const float4*>(s + c);
+    m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
   }
-  for (int c = (l + 16 * CH) * 4; c < cols; c += 64) {
-    const float4 u = *reinterpret_cast<const float4*>(s + c);
-    m = fmaxf(m, fmaxf(fmaxf(fabsf(u.x), fabsf(u.y)), fmaxf(fabsf(u.z), fabsf(u.w))));
-  }
-#pragma unroll
-  for (int o = 8; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 16));
+  m = sfx::wave_max(m);
   int e = 0;
   if (m > 0.f && m <= 3.4028235e38f) e = row_exp(m) + 2;
   const float sc = ldexpf(1.f, e);
-  uint4* d = reinterpret_cast<uint4*>(dst + (long long)row * cols);
-#pragma unroll
-  for (int j = 0; j < CH; ++j) {
-    const int c = (l + 16 * j) * 4;
-    if (c < cols) {
-      uint2 t[2];
-      split2h(v[j], sc, t);
-      d[c / 4] = make_uint4(t[0].x, t[0].y, t[1].x, t[1].y);
-    }
-  }
-  for (int c = (l + 16 * CH) * 4; c < cols; c += 64) {
+  uint2* d = reinterpret_cast<uint2*>(dst + (long long)row * cols);
+  for (int c = lane * 4; c < cols; c += 256) {
     uint2 t[2];
     split2h(*reinterpret_cast<const float4*>(s + c), sc, t);
-    d[c / 4] = make_uint4(t[0].x, t[0].y, t[1].x, t[1].y);
+    d[c / 2] = t[0];
+    d[c / 2 + 1] = t[1];
   }
-  if (l == 0) inv[row] = ldexpf(1.f, -e);
-}
-
-// A-split scratch: one grow-only buffer per (device, stream); a stream's launches are ordered, so each split
-// overwrites rows its previous GEMM has finished reading.  SFX_GEMM_ASPLIT=0 keeps the in-kernel split.
-bool asplit_enabled() {
-  static int on = -1;
-  if (on < 0) {
-    const char* e = getenv("SFX_GEMM_ASPLIT");
-    on = (e && *e) ? (atoi(e) != 0) : 0;
-  }
-  return on == 1;
-}
-
-float* asplit_scratch(size_t floats, hipStream_t st) {
-  struct Slot { int dev; hipStream_t st; float* p; size_t cap; };
-  static Slot slots[32] = {};
-  static int used = 0;
-  int dev = 0;
-  (void)hipGetDevice(&dev);
-  Slot* s = nullptr;
-  for (int i = 0; i < used; ++i)
-    if (slots[i].dev == dev && slots[i].st == st) s = &slots[i];
-  if (!s) {
-    if (used == 32) return nullptr;
-    s = &slots[used++];
-    *s = Slot{dev, st, nullptr, 0};
-  }
-  if (s->cap < floats) {
-    if (s->p) {
-      (void)hipStreamSynchronize(st);
-      (void)hipFree(s->p);
-      s->p = nullptr;
-      s->cap = 0;
-    }
-    const size_t want = floats + floats / 4;  // headroom: stage sizes vary per scene
-    if (hipMalloc(&s->p, want * sizeof(float)) != hipSuccess) return nullptr;
-    s->cap = want;
-  }
-  return s->p;
-}
-
-// Pre-split the `rows` source rows of a fp16x2 launch's A (a.A, a.lda, a.K columns) so the GEMM only copies term
-// images (split == 4).  No-op (the kernel then splits in place) when disabled, ineligible or out of scratch.
-void presplit_a(GemmArgs& a, long long rows, bool vec, hipStream_t st) {
-  if (!asplit_enabled() || !vec || !a.Wsp || rows <= 0 || split_mode(a.K) != 2) return;
-  const long long kp = (a.K + 3) / 4 * 4;
-  if (!fits(rows, kp)) return;
-  float* buf = asplit_scratch((size_t)(rows * kp + rows + 64), st);
-  if (!buf) return;
-  float* inv = buf + rows * kp;
-  split_rows_kernel<<<(unsigned)sfx::ceil_div(rows, 16), 256, 0, st>>>((int)rows, a.K, a.A, a.lda, buf, inv);
-  a.Asp = buf;
-  a.ldas = kp;
-  a.ainv = inv;
+  if (lane == 0) inv[row] = ldexpf(1.f, -e);
 }
 
 // ---- weight gradient: dW[N, K] += dY[M, N]^T X[M, K] (reduction over the point rows) ----------------
@@ -1464,6 +1353,17 @@ int sfx_gemm_force_config(int cfg, int stream_k) {
   return SFX_OK;
 }
 
+int sfx_weight_split(int rows, int cols, const float* w, long long ld, float* w_split, float* w_inv, void* stream) {
+  SFX_REQUIRE(rows >= 0 && cols > 0 && cols % 4 == 0 && ld >= cols && ld % 4 == 0,
+              "sfx_weight_split: bad sizes (cols and ld must be multiples of 4)");
+  if (rows == 0) return SFX_OK;
+  SFX_REQUIRE(w && w_split && w_inv, "sfx_weight_split: null buffer");
+  SFX_REQUIRE((reinterpret_cast<uintptr_t>(w) & 15) == 0 && (reinterpret_cast<uintptr_t>(w_split) & 15) == 0,
+              "sfx_weight_split: buffers must be 16-byte aligned");
+  weight_split_kernel<<<sfx::ceil_div(rows, 4), 256, 0, sfx::as_stream(stream)>>>(rows, cols, w, ld, w_split, w_inv);
+  return sfx::check_launch("sfx_weight_split");
+}
+
 int sfx_amax_f32(int rows, int cols, const float* x, long long ld, unsigned long long* slot, unsigned tag,
                  void* stream) {
   SFX_REQUIRE(rows >= 0 && cols >= 0 && ld >= cols, "sfx_amax_f32: bad sizes");
@@ -1510,7 +1410,6 @@ int sfx_linear(int M, int N, int K, const float* A, long long lda, const int* ga
     SFX_REQUIRE(groups == 1 || group_stride_W == (long long)N * K, "sfx_linear: w_split needs contiguous groups");
     a.Wsp = w_split; a.ldws = K; a.winv = w_inv; a.gWinv = N;
   }
-  if (!gather_idx && groups == 1) presplit_a(a, M, vec, sfx::as_stream(stream));
   dispatch(a, groups, vec, sfx::as_stream(stream));
   return sfx::check_launch("sfx_linear");
 }
@@ -1555,7 +1454,6 @@ static int subm_conv_impl(int n, int cin, int cout, const float* x, long long ld
                     AmaxJob{weight, 27ll * cin, 0, cout, 27 * cin, 1, nullptr, 0, 1}, st)) {
     a.a_amax = a.w_amax = nullptr;  // (dispatch falls back to bf16x3 for the pair launch)
   }
-  presplit_a(a, n, vec, st);  // x once, for the centre and the pair launch
   dispatch(a, 1, vec, st);
   int rc = sfx::check_launch("sfx_subm_conv(centre)");
   if (rc) return rc;

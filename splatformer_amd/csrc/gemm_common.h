@@ -1,5 +1,5 @@
-// Shared declarations of the fp32-accurate GEMM kernels (gemm.hip: the general tile kernel; gemm_ws.hip: the
-// warp-specialised fp16x2 kernel): launch arguments, epilogue helpers and raw-buffer access.
+// Shared declarations of the fp32-accurate GEMM kernels (gemm.hip): launch arguments, epilogue helpers and
+// raw-buffer access.
 #pragma once
 
 #include <type_traits>
@@ -83,7 +83,7 @@ struct GemmArgs {
   unsigned a_tag, w_tag;
   unsigned long long* y_amax;  // optional: max |Y| of this launch's outputs -> slot, tag y_tag
   unsigned y_tag;
-  // pre-split W (sfx_weight_split; the warp-specialised kernel): W's element layout in 4-byte units, every group
+  // pre-split W (sfx_weight_split): W's element layout in 4-byte units, every group
   // of 4 consecutive elements held as 4 fp16 h terms then 4 fp16 l terms of W[n, k] * 2^e_n; winv[n] = 2^-e_n.
   // Slices / groups use the same element offsets as W (slice_w_stride, gW); winv is grouped by gWinv.
   const float* Wsp;
@@ -91,13 +91,7 @@ struct GemmArgs {
   const float* winv;
   long long gWinv;
   long long slice_winv_stride;  // pair mode: winv offset per slice (row-sliced weights, e.g. the conv backward)
-  int epi_vec;  // epilogue operands allow 16-byte accesses (set by launch_ws)
   int tuned, tuned_sk;  // measured tile configuration + 1 (0: cost model / table) and its Stream-K flag
-  // pre-split A (split == 4): the source rows of A in the Wsp layout (row stride ldas, 4-byte units), ainv[r] =
-  // 1/s of source row r (the row A is gathered from: dense m, gidx[m], pair_in[m])
-  const float* Asp;
-  long long ldas;
-  const float* ainv;
   int pair_store;  // pair mode: store each pair's row at row `pair index` of Y instead of adding into pair_out
 };
 
@@ -159,10 +153,5 @@ using sfx::split3;   // fp32 -> three bf16 terms (common.h)
 using sfx::split2h;  // fp32 -> two fp16 terms of the scaled value (common.h)
 
 enum Mode { MODE_DENSE = 0, MODE_GATHER1 = 1, MODE_GATHERS = 2, MODE_PAIR = 3 };
-
-// Warp-specialised fp16x2 launcher (gemm_ws.hip): false when the launch is not eligible (the caller then runs
-// the general kernel).  Needs vec operands, split == 2, a pre-split W (Wsp / winv) and no Stream-K.
-bool launch_ws(const GemmArgs& a, int groups, hipStream_t st);
-bool ws_enabled();
 
 }  // namespace sfxg

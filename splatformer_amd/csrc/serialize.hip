@@ -121,7 +121,9 @@ __global__ void pool_assign_runs_kernel(int n, int m, int row0, const int* __res
   const int c = pos[q] - 1 - row0 * m;
   cluster[p] = c;
   sidx[j] = p;
-  if (flags[q]) {
+  // a run index past m (codes that are not hierarchical: the caller's deferred run check raises) is never used
+  // as an address
+  if (flags[q] && (unsigned)c < (unsigned)m) {
     idx_ptr[c] = j;
     head[c] = p;
   }
@@ -137,6 +139,7 @@ __global__ void pool_reorder_kernel(int n, int m, int R, const int* __restrict__
   const int r = (int)(q / n);
   const int k = pos[q] - 1 - r * m;
   const int c = cluster[order[q]];
+  if ((unsigned)k >= (unsigned)m || (unsigned)c >= (unsigned)m) return;  // (see pool_assign_runs_kernel)
   new_order[(long long)r * m + k] = c;
   new_inverse[(long long)r * m + c] = k;
 }

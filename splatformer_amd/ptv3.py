@@ -139,7 +139,8 @@ class Block(nn.Module):
         # publishes max |qkv| for the attention's fp16x2 q / k / v terms (ptv3_ops.new_amax)
         # the conv's pair products go to per-pair rows that the LN kernel sums in a fixed order (no float atomics,
         # reproducible); SFX_SUBM_ATOMIC=1 restores the atomic accumulation
-        t = ops.subm_conv(x if conv_in is None else conv_in, point.nbr, wf, bf, partials=ops.SUBM_PARTIALS)
+        xc = x if conv_in is None else conv_in
+        t = ops.subm_conv(xc, point.nbr, wf, bf, partials=ops.subm_partials_ok(xc, point.nbr, C))
         ln1 = self.norm1[0]
         x1, h = ops.cpe_residual_ln(t, x, ln_c.weight, ln_c.bias, ln1.weight, ln1.bias, ln1.eps)
         qkv, q_amax = ops.linear(h, self.attn.qkv.weight, self.attn.qkv.bias, y_amax=True)
@@ -184,9 +185,13 @@ class SerializedPooling(nn.Module):
         self.norm = PointSequential(norm_layer(out_channels))
         self.act = PointSequential(act_layer())
 
-    def _pd(self, point: Point) -> int:
+    def pooling_depth(self, depth: int) -> int:
+        """Pointcept's pooling_depth (ceil(stride) - 1).bit_length(), 0 when it exceeds the serialized depth."""
         pd = (math.ceil(self.stride) - 1).bit_length()
-        return 0 if pd > point.serialized_depth else pd
+        return 0 if pd > depth else pd
+
+    def _pd(self, point: Point) -> int:
+        return self.pooling_depth(point.serialized_depth)
 
     def geometry_begin(self, point: Point):
         return ops.pool_geometry_begin(point.codes_phys, point.order_phys, self._pd(point))
@@ -389,9 +394,8 @@ class PointTransformerV3(nn.Module):
         # every pooling's cluster count from the stage-0 codes, read back while stage 0 runs: no pooling waits
         pools = [getattr(self.enc, f"enc{s}").down for s in range(1, self.num_stages)]
         shifts, depth, cum = [], point.serialized_depth, 0
-        for mod in pools:
-            pd = (math.ceil(mod.stride) - 1).bit_length()
-            pd = 0 if pd > depth else pd
+        for mod in pools:  # the same pooling depths the poolings themselves will use (SerializedPooling._pd)
+            pd = mod.pooling_depth(depth)
             depth, cum = depth - pd, cum + pd
             shifts.append(3 * cum)
         counts_rd = ops.pool_counts_begin(point.codes_phys, point.order_phys, shifts) if POOL_COUNTS_UPFRONT else None

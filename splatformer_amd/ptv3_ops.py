@@ -524,6 +524,15 @@ def subm_neighbors(grid_coord: Tensor, batch: Optional[Tensor], with_pairs: bool
 
 # eval-path SubM convs: store per-pair partials and sum them in the consumer (default), or add them atomically
 SUBM_PARTIALS = os.environ.get("SFX_SUBM_ATOMIC", "0") != "1"
+PAIRS_LN_CHANNELS = (64, 96, 128, 256, 512)  # the channel counts sfx_cpe_residual_ln_pairs has kernels for
+
+
+def subm_partials_ok(x: Tensor, smap: "SubmMap", cout: int) -> bool:
+    """Whether the atomic-free SubM form can run for this launch: its consumer (sfx_cpe_residual_ln_pairs) needs
+    C in PAIRS_LN_CHANNELS, 16-byte aligned contiguous rows and partials below the 2 GiB buffer range; other
+    launches (e.g. enc_dim=32's C=32 stage 0, reference pointtransformer_v3.py:113) take the atomic form."""
+    return (SUBM_PARTIALS and cout in PAIRS_LN_CHANNELS and x.shape[1] == cout and x.is_contiguous()
+            and x.data_ptr() % 16 == 0 and smap.num_pairs * cout * 4 + 64 < 0x7ffffff0)
 
 
 class SubmPartials:

@@ -151,6 +151,9 @@ class Trainer:
         self.step_count += 1
         for p, m1, m2 in zip(self.params, self.exp_avg, self.exp_avg_sq):
             tops.adam_step(p.data, p.grad, m1, m2, self.step_count, self.lr, self.betas, self.eps, grad_scale=coef)
+            # adam_step writes through a raw pointer, which torch does not see: bump the parameter's version so
+            # every cache keyed on it (fp16x2 pre-split ops.weight_split, W^T ptv3_train.wt) is rebuilt
+            torch.autograd.graph.increment_version(p)
         self.flat_grad.zero_()
         self.micro = 0
 

@@ -14,7 +14,8 @@ import torch.multiprocessing as mp
 pytestmark = pytest.mark.gpu
 
 PERMS = [[1, 0, 3, 2], [2, 3, 0, 1], [0, 1, 2, 3], [3, 2, 1, 0], [1, 3, 0, 2]]
-N = (2500, 2200)
+SMALL = ((2500, 2200), True)       # per-rank scene sizes, unique stage-0 voxels
+LARGE = ((100_000, 100_000), False)  # config D's workload: 100k Gaussians per rank, duplicate voxels kept
 
 
 def _free_port():
@@ -25,12 +26,12 @@ def _free_port():
     return p
 
 
-def _scene(r):
+def _scene(r, sizes=SMALL):
     from splatformer_amd.scenes import make_scene
-    return make_scene(N[r], 1, seed=40 + r, unique_voxels=True)
+    return make_scene(sizes[0][r], 1, seed=40 + r, unique_voxels=sizes[1])
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, sizes=SMALL):
     import sys
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
@@ -51,7 +52,7 @@ def _worker(rank, world, port, q):
         for p in params:
             p.grad = flat[off:off + p.numel()].view_as(p)
             off += p.numel()
-        s = _scene(rank)
+        s = _scene(rank, sizes)
         n = s["means"].shape[0]
         data = ptv3_ref.batchify(s)
         dd = {k: (v.to(dev) if isinstance(v, torch.Tensor) else v) for k, v in data.items()}
@@ -72,13 +73,12 @@ def _worker(rank, world, port, q):
             torch.distributed.destroy_process_group()
 
 
-def test_two_rank_syncbn_ddp_grads(device):
-    from oracle import ptv3_ref
-    from test_gpu_ptv3 import _model, rel_l2
-    world, port = 2, _free_port()
+def _run_ranks(sizes, world=2):
+    """Both ranks' (averaged bucket, DropPath masks, dfeat, features), HIP side."""
+    port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, sizes)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted((q.get(timeout=600) for _ in range(world)), key=lambda t: t[0])
@@ -88,21 +88,27 @@ def test_two_rank_syncbn_ddp_grads(device):
         p.join(timeout=120)
         assert p.exitcode == 0
     assert torch.equal(res[0][1], res[1][1])  # every rank holds the same averaged bucket
-    flat_hip = res[0][1].double()
+    return res
 
+
+def _oracle_batch(res, sizes, dtype, world=2):
+    """The oracle's single train forward over the ranks' scenes as one batch (its BatchNorms see every scene:
+    SyncBatchNorm's statistics) + autograd of sum_r <feat_r, dfeat_r>; -> (qkv grads / world, features)."""
+    from oracle import ptv3_ref
+    from test_gpu_ptv3 import _model
     model = _model(41)
     sd = {k: v.detach().clone() for k, v in model.state_dict().items()}
     names = [k for k, p in model.named_parameters() if "attn.qkv" in k]
-    scenes = [_scene(r) for r in range(world)]
-    datas = [ptv3_ref.batchify(s) for s in scenes]
+    datas = [ptv3_ref.batchify(_scene(r, sizes)) for r in range(world)]
     counts = [d["feat"].shape[0] for d in datas]
     batch = dict(coord=torch.cat([d["coord"] for d in datas]), feat=torch.cat([d["feat"] for d in datas]),
                  grid_coord=torch.cat([d["grid_coord"] for d in datas]),
                  offset=torch.tensor([counts[0], counts[0] + counts[1]]))
     masks = {k: torch.cat([res[0][2][k], res[1][2][k]]) for k in res[0][2]}
     dfeat = torch.cat([res[0][3], res[1][3]])
-
-    def oracle(dtype):
+    prev = torch.get_default_dtype()
+    torch.set_default_dtype(dtype)
+    try:
         sdd = {k: (v.to(dtype) if v.is_floating_point() else v).clone() for k, v in sd.items()}
         for k in names:
             sdd[k].requires_grad_()
@@ -110,16 +116,48 @@ def test_two_rank_syncbn_ddp_grads(device):
         pnt = ptv3_ref.ptv3_forward(sdd, ptv3_ref.PTv3Config(), dat, PERMS, prefix="backbone.backbone.", train=True,
                                     masks={k: m.to(dtype) for k, m in masks.items()})
         (pnt.feat * dfeat.to(dtype)).sum().backward()
-        return torch.cat([sdd[k].grad.double().reshape(-1) for k in names]) / world, pnt.feat.detach()
-
-    g32, f32 = oracle(torch.float32)
-    assert rel_l2(torch.cat([res[0][4], res[1][4]]), f32) < 1e-5  # per-rank features == batch features
-    prev = torch.get_default_dtype()
-    torch.set_default_dtype(torch.float64)
-    try:
-        g64, _ = oracle(torch.float64)
     finally:
         torch.set_default_dtype(prev)
+    return torch.cat([sdd[k].grad.double().reshape(-1) for k in names]) / world, pnt.feat.detach()
+
+
+def test_two_rank_syncbn_ddp_grads(device):
+    from test_gpu_ptv3 import rel_l2
+    res = _run_ranks(SMALL)
+    flat_hip = res[0][1].double()
+    g32, f32 = _oracle_batch(res, SMALL, torch.float32)
+    assert rel_l2(torch.cat([res[0][4], res[1][4]]), f32) < 1e-5  # per-rank features == batch features
+    g64, _ = _oracle_batch(res, SMALL, torch.float64)
     e_hip, e_ref = rel_l2(flat_hip, g64), rel_l2(g32, g64)
     print(f"\n[ddp x2] HIP {e_hip:.2e} fp32 oracle {e_ref:.2e} (to fp64)")
+    assert e_hip <= 2.0 * e_ref + 1e-5
+
+
+# ---- config D's workload: 100k Gaussians per rank -----------------------------------------
+@pytest.fixture(scope="module")
+def ddp_large(device):
+    return _run_ranks(LARGE)
+
+
+@pytest.fixture(scope="module")
+def ddp_large_oracle32(ddp_large):
+    return _oracle_batch(ddp_large, LARGE, torch.float32)
+
+
+@pytest.mark.timeout(900)
+def test_two_rank_syncbn_ddp_100k_forward(ddp_large, ddp_large_oracle32):
+    from test_gpu_ptv3 import rel_l2
+    _, f32 = ddp_large_oracle32
+    err = rel_l2(torch.cat([ddp_large[0][4], ddp_large[1][4]]), f32)
+    print(f"\n[ddp x2, 100k/rank] train features rel L2 {err:.2e}")
+    assert err < 1e-5
+
+
+@pytest.mark.timeout(900)
+def test_two_rank_syncbn_ddp_100k_grads(ddp_large, ddp_large_oracle32):
+    from test_gpu_ptv3 import rel_l2
+    g32, _ = ddp_large_oracle32
+    g64, _ = _oracle_batch(ddp_large, LARGE, torch.float64)
+    e_hip, e_ref = rel_l2(ddp_large[0][1].double(), g64), rel_l2(g32, g64)
+    print(f"\n[ddp x2, 100k/rank] HIP {e_hip:.2e} fp32 oracle {e_ref:.2e} (to fp64)")
     assert e_hip <= 2.0 * e_ref + 1e-5

@@ -357,10 +357,13 @@ def _model(seed=0, **bk):
     (5000, False, {}),
     (2000, True, dict(enc_depths=(1, 1, 1, 1, 1), dec_depths=(1, 1, 1, 1))),  # config A shape (depth 1)
     (6000, False, dict(enable_flash=True)),  # K = 1024 windows (pointtransformer_v3.py:121-123)
+    (3000, False, dict(enc_dim=32)),  # enc_channels (32, 64, ...) (pointtransformer_v3.py:113): C=32 stage 0
 ])
 def test_feature_predictor_matches_oracle(device, n, unique, bk):
     model = _model(3, **bk)
-    cfg = ptv3_ref.PTv3Config(**{k: v for k, v in bk.items()})
+    cfg = ptv3_ref.PTv3Config(**{k: v for k, v in bk.items() if k != "enc_dim"})
+    if bk.get("enc_dim") == 32:
+        cfg.enc_channels = (32, 64, 128, 256, 512)
     if cfg.enable_flash:
         cfg.patch_size = 1024
     sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}

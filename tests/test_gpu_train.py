@@ -188,3 +188,28 @@ def test_trainer_step_runs_and_updates(device):
     changed = sum(int(not torch.equal(a, p.detach())) for a, p in zip(before, tr.params))
     assert changed == len(tr.params)
     assert float(tr.flat_grad.abs().max()) == 0.0  # zeroed after the optimiser step
+
+
+def test_trainer_second_step_uses_updated_weights(device):
+    """Adam updates the qkv weights through a raw pointer: the GEMM's cached fp16x2 pre-split (and W^T) must be
+    rebuilt, so that after a step the qkv projection computes h @ W_new^T (the split was keyed on
+    the tensor version, which the raw write did not bump)."""
+    torch.manual_seed(0)
+    from splatformer_amd import ptv3_ops as ops
+    from splatformer_amd import ptv3_train as pt
+    from splatformer_amd.feature_predictor import FeaturePredictor
+    model = FeaturePredictor(sh_degree=1, zeroinit=False).to(device)
+    tr = strain.Trainer(model, lr=1e-2, generator=torch.Generator(device=device).manual_seed(0))
+    s = to_device(make_scene(2500, 1, seed=4), device)
+    cams = to_device(make_cameras(64, 64, n_views=2), device)
+    gt = [torch.rand(64, 64, 3, device=device) for _ in range(2)]
+    qkv = model.backbone.backbone.enc.enc0.block0.attn.qkv
+    h = torch.randn(3000, qkv.weight.shape[1], generator=torch.Generator().manual_seed(1)).to(device)
+    for step in range(2):
+        tr.step([s], [cams], [gt])
+        w = qkv.weight.detach().cpu().double()
+        ref = h.cpu().double() @ w.T + qkv.bias.detach().cpu().double()
+        got = ops.linear(h, qkv.weight, qkv.bias).cpu().double()
+        assert rel_l2(got, ref) < 1e-6, f"step {step}: qkv GEMM does not use the updated weight"
+        wt_ref = qkv.weight.detach().reshape(qkv.weight.shape[0], -1).T.cpu()
+        assert torch.equal(pt.wt(qkv.weight).cpu(), wt_ref), f"step {step}: stale cached W^T"
