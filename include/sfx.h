@@ -138,8 +138,8 @@ int sfx_linear(int M, int N, int K, const float* A, long long lda, const int* ga
  * W[n, k..k+3] * 2^e_n, where 2^e_n puts the row's largest magnitude in [2^14, 2^15); w_inv[n] = 2^-e_n.
  * cols and ld multiples of 4, buffers 16-byte aligned.  Passing (w_split, w_inv) of a weight to sfx_linear /
  * sfx_subm_conv / sfx_linear_bwd_data / sfx_subm_conv_bwd_data (split of the matrix passed as W / weight / Wt)
- * selects the warp-specialised kernel, which also scales every row of A' by its own power of two (chosen
- * online from the row's values), so no operand maxima are needed; NULL keeps the amax-slot form. */
+ * selects the fp16x2 kernel, which also scales every row of A' by its own power of two (chosen online from the
+ * row's values), so no operand maxima are needed; NULL keeps the range-safe bf16x3 form. */
 int sfx_weight_split(int rows, int cols, const float* w, long long ld, float* w_split, float* w_inv, void* stream);
 
 /* fp16x2 operand maxima ("amax slots").  The GEMMs run K >= 64 products on split operands: fp16x2 by default
@@ -387,6 +387,21 @@ int sfx_voxel_keys(int n, const float* points, long long ld, float voxel_size, u
                    void* stream);
 int sfx_nn1(int n, int m, const float* queries, const float* refs, int* out, void* stream);
 int sfx_fps(int n, int m, const float* xyz, int start, int* out, float* dist_ws, void* stream);
+
+/* (ABI v8) Fused Block MLP tail, eval (reference Block.forward restated in calflops.py:72-82: norm2 -> mlp ->
+ * + shortcut; MLP = Linear(C, 4C) -> GELU(erf) -> Linear(4C, C)):  Y = X + fc2(GELU(fc1(LN(X)))), one launch, the
+ * LayerNorm output and the [M, 4C] hidden activation stay on chip.  fp32-accurate (fp16x2 MFMA terms with
+ * power-of-two row scales, fp32 accumulation).  C in {64, 96, 128, 256}.
+ * sfx_mlp_pack (once per weight version): w1 [4C][C], b1 [4C], w2 [C][4C], b2 [C], gamma / beta [C] (torch
+ *   Linear / LayerNorm layouts, contiguous) -> `stream` (sfx_mlp_stream_floats(C) floats: the pre-split weights
+ *   in the kernel's LDS-DMA slab order) and `params` (sfx_mlp_params_floats(C) floats); workspace: 9C ints.
+ * sfx_block_mlp: X [M][ldx], Y [M][ldy] (distinct buffers), 16-byte aligned rows; eps = the LayerNorm eps. */
+size_t sfx_mlp_stream_floats(int C);
+size_t sfx_mlp_params_floats(int C);
+int sfx_mlp_pack(int C, const float* w1, const float* b1, const float* w2, const float* b2, const float* gamma,
+                 const float* beta, float* stream, float* params, int* workspace, void* stream_);
+int sfx_block_mlp(int M, int C, const float* x, long long ldx, const float* stream, const float* params, float eps,
+                  float* y, long long ldy, void* stream_);
 
 #ifdef __cplusplus
 }

@@ -321,7 +321,8 @@ def batchify(gs: Dict[str, torch.Tensor], grid_resolution: int = 384):
     coord = gs["means"]
     return dict(coord=coord, grid_size=torch.ones(3) * 1.0 / grid_resolution,
                 offset=torch.tensor([coord.shape[0]]), feat=feat,
-                grid_coord=torch.floor(coord * grid_resolution).int())
+                # feature_predictor.py:156 on the fp32 means (an fp64 check run keeps the fp32 voxel geometry)
+                grid_coord=torch.floor(coord.float() * grid_resolution).int())
 
 
 def heads_forward(sd, y: torch.Tensor, feat: torch.Tensor, in_gs: Dict[str, torch.Tensor], sh_degree: int = 1,

@@ -1,0 +1,459 @@
+// Fused PTv3 Block MLP tail (eval): Y = X2 + fc2(GELU(fc1(LN2(X2))))  -- reference Block.forward, restated in
+// calflops.py:72-82 (norm2 -> mlp -> drop_path(identity in eval) -> + shortcut), MLP = Linear(C,4C) -> GELU
+// (erf) -> Linear(4C,C) (pointtransformer_v3.py:145, Pointcept MLP).
+//
+// One launch replaces LayerNorm + two GEMMs: the [M, C] LayerNorm output and the [M, 4C] hidden activation never
+// reach HBM (in the unfused form they are written and read back: 10 C floats per point, 8.6 GB per config-B
+// refine).  HBM traffic is the algorithmic X2 read + Y write; the weights stream from L2.
+//
+// Arithmetic: fp32-accurate fp16x2 MFMA (the GEMM family's scheme, gemm.hip): every operand is a power-of-two
+// scaled pair of fp16 terms h + l and every 32x32x16 block is h*h + h*l + l*h on v_mfma_f32_32x32x16_f16 with
+// fp32 accumulation.  Scales:
+//   * LN2 output row p: its exact row maximum (known here: the whole row is LayerNormed in the workgroup) in
+//     [2^13, 2^14);
+//   * hidden row p (all 4C units, every chunk): one scale from the bound |GELU(z)| <= max(|z|, 0.17),
+//     |z_u| <= ||LN2(x)_p||_2 max_u ||W1_u||_2 + max|b1| (Cauchy-Schwarz; the bound puts the row in [2^14, 2^15)
+//     at most, so no chunk overflows fp16 and no running rescale is needed);
+//   * W1 rows / W2 rows: their own maxima in [2^14, 2^15) (pre-split once per weight version, sfx_mlp_pack).
+//
+// Work decomposition: one workgroup = 64 points, 4 waves as 2 (point halves pm) x 2 (unit halves cn).  The hidden
+// layer is processed in chunks of 64 units.  Computed transposed (points on the lanes): per chunk, wave (pm, cn)
+// forms hid^T[32 units (cn), 32 points (pm)] = W1_chunk(cn) . LN2(X2)^T (A = W1 rows from LDS, B = the LN2 image
+// in LDS), applies bias + GELU + split in registers, and feeds the accumulator registers straight back as the
+// B operand of fc2 (a 32x32 accumulator's registers 8s..8s+7 are the k-step s fragment of A.X, the k order
+// permuted: cdna_hip_programming.md §3) -- the hidden never touches LDS either.  fc2^T: acc2^T[C channels,
+// 32 points] += W2[:, the wave's 32 units] . hid^T; the two unit halves' partial sums of a point half are added
+// once per tile through LDS.
+//
+// Weights stream through an LDS ring by LDS-DMA (global_load_lds_dwordx4): sfx_mlp_pack lays W1 / W2 out as
+// 8 KB slabs in exactly the swizzled order the fragments are read in (so a slab is a plain contiguous copy) and in
+// consumption order: per chunk C/32 fc1 slabs ([2 halves][2 terms][32 units][32 k]) then C/32 fc2 slabs
+// ([2 halves][2 terms][32 channels][32 units, permuted]).  A phase = 2 slabs (16 KB) = 12 MFMAs per wave; the ring
+// holds RING phases, RING-1 in flight; one barrier per phase (RAW for the arriving slabs, WAR for the refilled
+// slot), counted vmcnt, raw s_barrier (no __syncthreads: its fence would drain the DMA queue).
+#include "gemm_common.h"
+
+namespace {
+
+using namespace sfxg;
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int MLP_BM = 64;          // points per workgroup
+constexpr int SLAB_BYTES = 8192;    // one streamed weight slab
+constexpr int PHASE_BYTES = 2 * SLAB_BYTES;
+
+template <int C>
+struct MlpGeom {
+  static constexpr int NB = C / 32;           // 32-channel blocks = fc1 slabs per chunk = fc2 slabs per chunk
+  static constexpr int NCH = C / 16;          // hidden chunks of 64 units (4C / 64)
+  static constexpr int PPC = NB;              // phases per chunk (2 * NB slabs, 2 per phase)
+  static constexpr int NP = NCH * PPC;        // phases per tile
+  static constexpr int RS = 2 * C + 16;       // LN2 image row stride in bytes (pad: conflict-free b128 reads)
+  static constexpr int IMG = 2 * MLP_BM * RS; // two term images
+  static constexpr int PAR = 12 * C + 4;      // parameter table floats
+};
+
+// Parameter table (floats): [0,C) gamma, [C,2C) beta, [2C,10C) (1/s_u, b1_u) pairs in fc1-epilogue order,
+// [10C,12C) (1/s_c, b2_c) pairs in fc2-epilogue order, [12C] max_u ||W1_u||_2, [12C+1] max |b1|.
+__device__ __forceinline__ int fc1_par_index(int j, int cn, int h, int i) { return ((j * 2 + cn) * 2 + h) * 16 + i; }
+__device__ __forceinline__ int fc2_par_index(int b, int h, int i) { return (b * 2 + h) * 16 + i; }
+// accumulator register i of lane half h -> row within the 32-row block (MFMA 32x32 C/D layout)
+__device__ __forceinline__ int acc_row(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
+// byte offset of fp16 element q (0..31) of row r in a swizzled [32 rows][64 B] term image (16-B chunk c at
+// c ^ ((r >> 2) & 3): the fragment reads of 16 rows x one chunk are bank-conflict free)
+__device__ __forceinline__ int slab_off(int r, int q) {
+  return r * 64 + ((((q >> 3) ^ (r >> 2)) & 3) << 4) + ((q & 7) << 1);
+}
+
+template <int RING>
+__device__ __forceinline__ void wait_vm_pipeline() {
+  // this wave's DMAs of the phase about to be read have landed: RING-2 younger phases (4 pieces each) may fly
+  if constexpr (RING == 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if constexpr (RING == 3) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <int C, int RING>
+__global__ void __launch_bounds__(256, C <= 96 ? 2 : 1) mlp_kernel(int M, const float* __restrict__ X, long long ldx,
+                                                     const float* __restrict__ stream, const float* __restrict__ par,
+                                                     float eps, float* __restrict__ Y, long long ldy) {
+  using G = MlpGeom<C>;
+  constexpr int NB = G::NB, NP = G::NP, PPC = G::PPC, RS = G::RS;
+  constexpr int RING_OFF = G::IMG;
+  constexpr int PAR_OFF = RING_OFF + RING * PHASE_BYTES;
+  constexpr int PT_OFF = PAR_OFF + G::PAR * 4;
+  constexpr int LDS_BYTES = PT_OFF + MLP_BM * 16;
+  static_assert(LDS_BYTES <= 163840, "LDS budget");
+  static_assert(2 * NB * 4096 <= G::IMG, "the tile-end exchange reuses the LN2 image");
+  __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
+  float* s_par = reinterpret_cast<float*>(lds + PAR_OFF);
+  float* s_pt = reinterpret_cast<float*>(lds + PT_OFF);  // per point: 1/s (LN2 split), t (hidden scale), 1/t
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int pm = wid >> 1, cn = wid & 1;
+  const int h = lane >> 5, r32 = lane & 31;
+  const int m0 = (int)blockIdx.x * MLP_BM;
+
+  // ---- weight stream: phase q -> ring slot q % RING; 16 pieces of 1 KB, 4 per wave ----
+  const char* gstream = reinterpret_cast<const char*>(stream);
+  auto issue = [&](int q) {
+    const char* src = gstream + (size_t)q * PHASE_BYTES + wid * 4096 + lane * 16;
+    char* dst = lds + RING_OFF + (q % RING) * PHASE_BYTES + wid * 4096;
+#pragma unroll
+    for (int pc = 0; pc < 4; ++pc)
+      __builtin_amdgcn_global_load_lds(src + pc * 1024, (__attribute__((address_space(3))) void*)(dst + pc * 1024),
+                                       16, 0, 0);
+  };
+#pragma unroll
+  for (int q = 0; q < RING - 1; ++q)
+    if (q < NP) issue(q);
+
+  // ---- prologue: parameter table, X2 tile, LayerNorm, LN2 term images, per-point scales ----
+  for (int i = tid; i < G::PAR; i += 256) s_par[i] = par[i];
+  const int pt = tid >> 2, qd = tid & 3;  // 4 threads per point, float4 f = qd + 4 i
+  constexpr int NV = C / 16;
+  const unsigned Mu = (unsigned)M;
+  const __amdgpu_buffer_rsrc_t rX = rsrc_ext(X, Mu * (unsigned)ldx * 4u);
+  float4 v[NV];
+  const unsigned xrow = (unsigned)(m0 + pt) * (unsigned)ldx;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) v[i] = bload4(rX, (m0 + pt < M) ? (xrow + 4u * (unsigned)(qd + 4 * i)) * 4u : OOB);
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+  s += __shfl_xor(s, 1, 64);
+  s += __shfl_xor(s, 2, 64);
+  const float mean = s / (float)C;
+  float q2 = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const float a = v[i].x - mean, b = v[i].y - mean, c = v[i].z - mean, d = v[i].w - mean;
+    q2 += (a * a + b * b) + (c * c + d * d);
+  }
+  q2 += __shfl_xor(q2, 1, 64);
+  q2 += __shfl_xor(q2, 2, 64);
+  const float rstd = 1.f / sqrtf(q2 / (float)C + eps);
+  __syncthreads();  // s_par visible (no DMA is waited for here: only plain stores precede it)
+  float mx = 0.f, nrm = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = 4 * (qd + 4 * i);
+    const float4 g = *reinterpret_cast<const float4*>(s_par + c);
+    const float4 b = *reinterpret_cast<const float4*>(s_par + C + c);
+    v[i] = make_float4((v[i].x - mean) * rstd * g.x + b.x, (v[i].y - mean) * rstd * g.y + b.y,
+                       (v[i].z - mean) * rstd * g.z + b.z, (v[i].w - mean) * rstd * g.w + b.w);
+    mx = fmaxf(mx, fmaxf(fmaxf(fabsf(v[i].x), fabsf(v[i].y)), fmaxf(fabsf(v[i].z), fabsf(v[i].w))));
+    nrm += (v[i].x * v[i].x + v[i].y * v[i].y) + (v[i].z * v[i].z + v[i].w * v[i].w);
+  }
+  mx = fmaxf(mx, __shfl_xor(mx, 1, 64));
+  mx = fmaxf(mx, __shfl_xor(mx, 2, 64));
+  nrm += __shfl_xor(nrm, 1, 64);
+  nrm += __shfl_xor(nrm, 2, 64);
+  int e = 0;
+  if (mx > 0.f && mx <= 3.4028235e38f) e = row_exp(mx) + 1;  // row max in [2^13, 2^14)
+  const float sc = ldexpf(1.f, e);
+  // hidden bound: |GELU(z)| <= max(|z|, 0.17), |z| <= ||h2|| max||W1_u|| + max|b1| (1.001: the sums' rounding)
+  const float U = fmaxf((sqrtf(nrm) * s_par[12 * C] + s_par[12 * C + 1]) * 1.001f, 0.17f);
+  int et = 0;
+  if (U <= 3.4028235e38f) et = row_exp(U) + 2;  // bound in [2^14, 2^15)
+  if (qd == 0) {
+    s_pt[4 * pt + 0] = ldexpf(1.f, -e);
+    s_pt[4 * pt + 1] = ldexpf(1.f, et);
+    s_pt[4 * pt + 2] = ldexpf(1.f, -et);
+  }
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    uint2 t[2];
+    split2h(v[i], sc, t);
+    const int c = 4 * (qd + 4 * i);
+    *reinterpret_cast<uint2*>(lds + pt * RS + 2 * c) = t[0];
+    *reinterpret_cast<uint2*>(lds + MLP_BM * RS + pt * RS + 2 * c) = t[1];
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  const int ptw = pm * 32 + r32;  // this lane's point within the tile
+  const float4 ps = *reinterpret_cast<const float4*>(s_pt + 4 * ptw);
+  const float sinv = ps.x, tsc = ps.y, tinv = ps.z;
+
+  floatx16 acc2[NB];
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc2[b][i] = 0.f;
+  floatx16 acc1;
+  f16x8 hf[2][2];  // hidden fragments: [k-step][term]
+
+  const char* img_h = lds + ptw * RS + 16 * h;           // LN2 h term, this lane's point, lane-half offset
+  const char* img_l = img_h + MLP_BM * RS;
+
+  auto mfma3 = [](const f16x8& ah, const f16x8& al, const f16x8& bh, const f16x8& bl, floatx16 c) {
+    c = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, c, 0, 0, 0);  // smallest terms first
+    c = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, c, 0, 0, 0);
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, c, 0, 0, 0);
+  };
+
+  // one slab of the chunk body: sl < NB -> fc1 slab sl (k = 32 sl .. +32), else fc2 slab sl - NB (channels)
+  auto slab = [&](const char* base, int sl, int j) {
+    const char* half = base + cn * 4096;  // this wave's [2 terms][32 rows][64 B]
+    if (sl < NB) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int q = 16 * t + 8 * h;
+        const f16x8 ah = *reinterpret_cast<const f16x8*>(half + slab_off(r32, q));
+        const f16x8 al = *reinterpret_cast<const f16x8*>(half + 2048 + slab_off(r32, q));
+        const int ko = 2 * (32 * sl + 16 * t);
+        const f16x8 bh = *reinterpret_cast<const f16x8*>(img_h + ko);
+        const f16x8 bl = *reinterpret_cast<const f16x8*>(img_l + ko);
+        acc1 = mfma3(ah, al, bh, bl, acc1);
+      }
+      if (sl == NB - 1) {  // hidden chunk complete: bias, GELU, split -> fc2 B fragments (registers)
+        const float4* pp = reinterpret_cast<const float4*>(s_par + 2 * C + 2 * fc1_par_index(j, cn, h, 0));
+        float g[16];
+#pragma unroll
+        for (int i2 = 0; i2 < 8; ++i2) {
+          const float4 wb = pp[i2];  // (1/s_u, b1_u) of registers 2 i2, 2 i2 + 1
+          g[2 * i2 + 0] = gelu_erf(acc1[2 * i2 + 0] * (sinv * wb.x) + wb.y) * tsc;
+          g[2 * i2 + 1] = gelu_erf(acc1[2 * i2 + 1] * (sinv * wb.z) + wb.w) * tsc;
+        }
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+          unsigned uh[4], ul[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const float x0 = g[8 * st + 2 * k], x1 = g[8 * st + 2 * k + 1];
+            uh[k] = sfx::pk_f16(x0, x1);
+            const sfx::sfx_f16x2 hh = __builtin_bit_cast(sfx::sfx_f16x2, uh[k]);
+            ul[k] = sfx::pk_f16(x0 - (float)hh.x, x1 - (float)hh.y);
+          }
+          hf[st][0] = __builtin_bit_cast(f16x8, make_uint4(uh[0], uh[1], uh[2], uh[3]));
+          hf[st][1] = __builtin_bit_cast(f16x8, make_uint4(ul[0], ul[1], ul[2], ul[3]));
+        }
+      }
+    } else {
+      const int b = sl - NB;
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        const int q = 16 * st + 8 * h;
+        const f16x8 ah = *reinterpret_cast<const f16x8*>(half + slab_off(r32, q));
+        const f16x8 al = *reinterpret_cast<const f16x8*>(half + 2048 + slab_off(r32, q));
+        acc2[b] = mfma3(ah, al, hf[st][0], hf[st][1], acc2[b]);
+      }
+    }
+  };
+
+  int p = 0;
+  for (int j = 0; j < G::NCH; ++j) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc1[i] = 0.f;
+#pragma unroll
+    for (int pi = 0; pi < PPC; ++pi, ++p) {
+      if (p + RING - 1 < NP) wait_vm_pipeline<RING>();
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tail: nothing younger than this phase in flight
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");  // no LDS access moves across the barrier
+      if (p + RING - 1 < NP) issue(p + RING - 1);  // refills the slot every wave finished before the barrier
+      const char* base = lds + RING_OFF + (p % RING) * PHASE_BYTES;
+      slab(base, 2 * pi, j);
+      slab(base + SLAB_BYTES, 2 * pi + 1, j);
+    }
+  }
+
+  // ---- tile end: add the unit halves' partial sums (block b finishes on wave cn = b % 2), epilogue ----
+  __builtin_amdgcn_s_barrier();  // every wave is past its last LN2-image read: the image area is free
+  float* exch = reinterpret_cast<float*>(lds);
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    if ((b & 1) == cn) continue;
+    float4* d = reinterpret_cast<float4*>(exch + ((pm * NB + b) * 64 + lane) * 16);
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4)
+      d[g4] = make_float4(acc2[b][4 * g4], acc2[b][4 * g4 + 1], acc2[b][4 * g4 + 2], acc2[b][4 * g4 + 3]);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  const __amdgpu_buffer_rsrc_t rY = rsrc_ext(Y, Mu * (unsigned)ldy * 4u);
+  const int prow = m0 + ptw;
+  const bool pok = prow < M;
+  const unsigned yrow = (unsigned)prow * (unsigned)ldy, xr = (unsigned)prow * (unsigned)ldx;
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    if ((b & 1) != cn) continue;
+    const float4* o = reinterpret_cast<const float4*>(exch + ((pm * NB + b) * 64 + lane) * 16);
+    const float4* pp = reinterpret_cast<const float4*>(s_par + 10 * C + 2 * fc2_par_index(b, h, 0));
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const float4 ot = o[g4];
+      const float4 w01 = pp[2 * g4], w23 = pp[2 * g4 + 1];  // (1/s_c, b2_c) of registers 4 g4 .. 4 g4 + 3
+      const int c0 = 32 * b + 8 * g4 + 4 * h;
+      const float4 xres = bload4(rX, pok ? (xr + (unsigned)c0) * 4u : OOB);
+      float4 y;
+      y.x = xres.x + ((acc2[b][4 * g4 + 0] + ot.x) * (tinv * w01.x) + w01.y);
+      y.y = xres.y + ((acc2[b][4 * g4 + 1] + ot.y) * (tinv * w01.z) + w01.w);
+      y.z = xres.z + ((acc2[b][4 * g4 + 2] + ot.z) * (tinv * w23.x) + w23.y);
+      y.w = xres.w + ((acc2[b][4 * g4 + 3] + ot.w) * (tinv * w23.z) + w23.w);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, y), rY, pok ? (yrow + (unsigned)c0) * 4u : OOB,
+                                             0, 0);
+    }
+  }
+}
+
+// ---- weight packing (once per weight version) ----------------------------------------------------------------
+// per-row exponents (max in [2^14, 2^15)) and W1 row norms
+__global__ void __launch_bounds__(256) mlp_rowstats_kernel(int rows, int cols, const float* __restrict__ W,
+                                                           int* __restrict__ e_out, float* __restrict__ nrm_out) {
+  const int row = (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  float m = 0.f, s = 0.f;
+  for (int c = lane; c < cols; c += 64) {
+    const float x = W[(long long)row * cols + c];
+    m = fmaxf(m, fabsf(x));
+    s += x * x;
+  }
+  m = sfx::wave_max(m);
+  s = sfx::wave_sum(s);
+  if (lane == 0) {
+    e_out[row] = (m > 0.f && m <= 3.4028235e38f) ? row_exp(m) + 2 : 0;
+    if (nrm_out) nrm_out[row] = sqrtf(s);
+  }
+}
+
+// one thread per (slab, half, row, position): both terms of one element
+template <int C>
+__global__ void __launch_bounds__(256) mlp_pack_stream_kernel(const float* __restrict__ W1,
+                                                              const float* __restrict__ W2, const int* __restrict__ e1,
+                                                              const int* __restrict__ e2, float* __restrict__ stream) {
+  using G = MlpGeom<C>;
+  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+  const long long total = (long long)G::NCH * 2 * G::NB * 2 * 32 * 32;
+  if (idx >= total) return;
+  const int q = (int)(idx & 31), r = (int)((idx >> 5) & 31), cn = (int)((idx >> 10) & 1);
+  const long long sidx = idx >> 11;  // slab index in stream order
+  const int j = (int)(sidx / (2 * G::NB)), sl = (int)(sidx % (2 * G::NB));
+  float w;
+  int e;
+  if (sl < G::NB) {  // fc1 slab: row r = unit 64 j + 32 cn + r, position q = input channel 32 sl + q
+    const int u = 64 * j + 32 * cn + r;
+    w = W1[(long long)u * C + 32 * sl + q];
+    e = e1[u];
+  } else {  // fc2 slab: row r = channel 32 b + r, position q = k-step q >> 4, lane half / element -> unit
+    const int b = sl - G::NB, c = 32 * b + r;
+    const int st = q >> 4, qq = q & 15, hh = qq >> 3, jj = qq & 7;
+    const int u = 64 * j + 32 * cn + 16 * st + 8 * (jj >> 2) + 4 * hh + (jj & 3);
+    w = W2[(long long)c * (4 * C) + u];
+    e = e2[c];
+  }
+  const float x = w * ldexpf(1.f, e);
+  const _Float16 hv = (_Float16)x;
+  const _Float16 lv = (_Float16)(x - (float)hv);
+  char* slab = reinterpret_cast<char*>(stream) + sidx * SLAB_BYTES + cn * 4096;
+  *reinterpret_cast<_Float16*>(slab + slab_off(r, q)) = hv;
+  *reinterpret_cast<_Float16*>(slab + 2048 + slab_off(r, q)) = lv;
+}
+
+template <int C>
+__global__ void __launch_bounds__(256) mlp_pack_params_kernel(const float* __restrict__ gamma,
+                                                              const float* __restrict__ beta,
+                                                              const float* __restrict__ b1,
+                                                              const float* __restrict__ b2, const int* __restrict__ e1,
+                                                              const int* __restrict__ e2, const float* __restrict__ n1,
+                                                              float* __restrict__ par) {
+  using G = MlpGeom<C>;
+  const int tid = (int)blockIdx.x * 256 + threadIdx.x;
+  if (tid < C) {
+    par[tid] = gamma[tid];
+    par[C + tid] = beta[tid];
+  }
+  if (tid < 4 * C) {  // fc1 entry tid = ((j * 2 + cn) * 2 + h) * 16 + i
+    const int i = tid & 15, hh = (tid >> 4) & 1, cn = (tid >> 5) & 1, j = tid >> 6;
+    const int u = 64 * j + 32 * cn + acc_row(i, hh);
+    par[2 * C + 2 * tid] = ldexpf(1.f, -e1[u]);
+    par[2 * C + 2 * tid + 1] = b1[u];
+  }
+  if (tid < C) {  // fc2 entry tid = (b * 2 + h) * 16 + i
+    const int i = tid & 15, hh = (tid >> 4) & 1, b = tid >> 5;
+    const int c = 32 * b + acc_row(i, hh);
+    par[10 * C + 2 * tid] = ldexpf(1.f, -e2[c]);
+    par[10 * C + 2 * tid + 1] = b2[c];
+  }
+  if (tid == 0) {  // max row norm of W1, max |b1| (one thread: 4C <= 1024 values each)
+    float mn = 0.f, mb = 0.f;
+    for (int u = 0; u < 4 * C; ++u) {
+      mn = fmaxf(mn, n1[u]);
+      mb = fmaxf(mb, fabsf(b1[u]));
+    }
+    par[12 * C] = mn;
+    par[12 * C + 1] = mb;
+    par[12 * C + 2] = 0.f;
+    par[12 * C + 3] = 0.f;
+  }
+  (void)G::NB;
+}
+
+template <int C>
+int pack_impl(const float* w1, const float* b1, const float* w2, const float* b2, const float* gamma,
+              const float* beta, float* stream, float* par, int* ws, hipStream_t st) {
+  int* e1 = ws;
+  int* e2 = ws + 4 * C;
+  float* n1 = reinterpret_cast<float*>(ws + 5 * C);
+  mlp_rowstats_kernel<<<sfx::ceil_div(4 * C, 4), 256, 0, st>>>(4 * C, C, w1, e1, n1);
+  mlp_rowstats_kernel<<<sfx::ceil_div(C, 4), 256, 0, st>>>(C, 4 * C, w2, e2, nullptr);
+  const long long total = (long long)MlpGeom<C>::NCH * 2 * MlpGeom<C>::NB * 2048;
+  mlp_pack_stream_kernel<C><<<sfx::ceil_div(total, 256), 256, 0, st>>>(w1, w2, e1, e2, stream);
+  mlp_pack_params_kernel<C><<<sfx::ceil_div(4 * C, 256), 256, 0, st>>>(gamma, beta, b1, b2, e1, e2, n1, par);
+  return sfx::check_launch("sfx_mlp_pack");
+}
+
+template <int C, int RING>
+int run_impl(int M, const float* x, long long ldx, const float* stream, const float* par, float eps, float* y,
+             long long ldy, hipStream_t st) {
+  mlp_kernel<C, RING><<<sfx::ceil_div(M, MLP_BM), 256, 0, st>>>(M, x, ldx, stream, par, eps, y, ldy);
+  return sfx::check_launch("sfx_block_mlp");
+}
+
+inline bool mlp_channels_ok(int C) { return C == 64 || C == 96 || C == 128 || C == 256; }
+
+}  // namespace
+
+extern "C" {
+
+size_t sfx_mlp_stream_floats(int C) { return mlp_channels_ok(C) ? (size_t)8 * C * C : 0; }
+size_t sfx_mlp_params_floats(int C) { return mlp_channels_ok(C) ? (size_t)(12 * C + 4) : 0; }
+
+int sfx_mlp_pack(int C, const float* w1, const float* b1, const float* w2, const float* b2, const float* gamma,
+                 const float* beta, float* stream, float* params, int* workspace, void* stream_) {
+  SFX_REQUIRE(mlp_channels_ok(C), "sfx_mlp_pack: C must be one of 64, 96, 128, 256 (got %d)", C);
+  SFX_REQUIRE(w1 && b1 && w2 && b2 && gamma && beta && stream && params && workspace, "sfx_mlp_pack: null buffer");
+  hipStream_t st = sfx::as_stream(stream_);
+  switch (C) {
+    case 64: return pack_impl<64>(w1, b1, w2, b2, gamma, beta, stream, params, workspace, st);
+    case 96: return pack_impl<96>(w1, b1, w2, b2, gamma, beta, stream, params, workspace, st);
+    case 128: return pack_impl<128>(w1, b1, w2, b2, gamma, beta, stream, params, workspace, st);
+    default: return pack_impl<256>(w1, b1, w2, b2, gamma, beta, stream, params, workspace, st);
+  }
+}
+
+int sfx_block_mlp(int M, int C, const float* x, long long ldx, const float* stream, const float* params, float eps,
+                  float* y, long long ldy, void* stream_) {
+  SFX_REQUIRE(M >= 0 && mlp_channels_ok(C), "sfx_block_mlp: C must be one of 64, 96, 128, 256 (got %d)", C);
+  if (M == 0) return SFX_OK;
+  SFX_REQUIRE(x && stream && params && y, "sfx_block_mlp: null buffer");
+  SFX_REQUIRE(ldx >= C && ldy >= C && ldx % 4 == 0 && ldy % 4 == 0, "sfx_block_mlp: leading dimensions");
+  SFX_REQUIRE(((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y) |
+                reinterpret_cast<uintptr_t>(stream) | reinterpret_cast<uintptr_t>(params)) & 15) == 0,
+              "sfx_block_mlp: buffers must be 16-byte aligned");
+  SFX_REQUIRE((long long)M * ldx * 4 + 64 < (long long)OOB && (long long)M * ldy * 4 + 64 < (long long)OOB,
+              "sfx_block_mlp: operand exceeds the 2 GiB buffer-descriptor range");
+  SFX_REQUIRE(x != y, "sfx_block_mlp: in-place output is not supported");
+  hipStream_t st = sfx::as_stream(stream_);
+  switch (C) {
+    case 64: return run_impl<64, 3>(M, x, ldx, stream, params, eps, y, ldy, st);
+    case 96: return run_impl<96, 3>(M, x, ldx, stream, params, eps, y, ldy, st);
+    case 128: return run_impl<128, 4>(M, x, ldx, stream, params, eps, y, ldy, st);
+    default: return run_impl<256, 4>(M, x, ldx, stream, params, eps, y, ldy, st);
+  }
+}
+
+}  // extern "C"

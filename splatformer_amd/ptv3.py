@@ -154,8 +154,11 @@ class Block(nn.Module):
             a = ops.window_attention(qkv, point.order_phys[oi], win, nw, K, self.attn.num_heads, C, qkv_amax=q_amax)
         x2 = ops.linear(a, self.attn.proj.weight, self.attn.proj.bias, residual=x1)
         ln2 = self.norm2[0]
-        h2 = ops.layernorm(x2, ln2.weight, ln2.bias, ln2.eps)
         mlp = self.mlp[0]
+        if ops.block_mlp_ok(x2, C):  # norm2 -> fc1 -> GELU -> fc2 -> + shortcut in one launch (csrc/mlp.hip)
+            point.feat = ops.block_mlp(x2, ln2, mlp.fc1, mlp.fc2, out=out)
+            return point
+        h2 = ops.layernorm(x2, ln2.weight, ln2.bias, ln2.eps)
         m = ops.linear(h2, mlp.fc1.weight, mlp.fc1.bias, act=ops.ACT_GELU)
         point.feat = ops.linear(m, mlp.fc2.weight, mlp.fc2.bias, residual=x2, out=out)
         return point

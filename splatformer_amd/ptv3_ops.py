@@ -45,6 +45,10 @@ _lib.register("sfx_subm_pair_pos", [I, L, P, P, P, P])
 _lib.register("sfx_gs_pack", [I, P, L, P, L, P, L, P, L, P, L, P, L, I, F, P, L, P, P, P])
 _lib.register("sfx_offsets_to_batch", [I, I, P, P, P])
 _lib.register("sfx_gemm_force_config", [I, I])
+_lib.register("sfx_mlp_stream_floats", [I], Z)
+_lib.register("sfx_mlp_params_floats", [I], Z)
+_lib.register("sfx_mlp_pack", [I, P, P, P, P, P, P, P, P, P, P])
+_lib.register("sfx_block_mlp", [I, I, P, L, P, P, F, P, L, P])
 
 ACT_NONE, ACT_GELU, ACT_RELU, ACT_TANH = 0, 1, 2, 3
 # gemm.hip kCfgs: 128x128, 128x96, 128x64, 64x128, 64x64 (4 waves, 2 per CU), 256x128, 128x256 (8 waves)
@@ -210,6 +214,50 @@ def grouped_linear(x: Tensor, weight: Tensor, bias: Tensor, groups: int, *, act:
          ldy, None, 0, G, K, N * K, N, N, None, None, 0, *_slot_args(a_amax), *_slot_args(w_amax),
          *_slot_args(ys), *weight_split(weight, G * N), stream())
     return (out, ys) if y_amax else out
+
+
+# ---- fused Block MLP tail (csrc/mlp.hip) ---------------------------------------------------------------------
+MLP_FUSED = os.environ.get("SFX_MLP_FUSED", "1") != "0"  # SFX_MLP_FUSED=0: LayerNorm + two GEMM launches
+MLP_CHANNELS = (64, 96, 128, 256)
+
+
+def mlp_pack(ln2, fc1, fc2) -> Tuple[Tensor, Tensor]:
+    """(weight stream, parameter table) of sfx_block_mlp for LayerNorm `ln2` and Linear `fc1` / `fc2`: the fp16x2
+    pre-split W1 / W2 laid out as the kernel's LDS-DMA slabs, plus gamma / beta / biases / row scales.  Cached on
+    fc1 until one of the six tensors changes (storage or version)."""
+    ts = (ln2.weight, ln2.bias, fc1.weight, fc1.bias, fc2.weight, fc2.bias)
+    key = tuple((t.data_ptr(), t._version) for t in ts)
+    c = fc1.__dict__.get("_sfx_mlp")
+    if c is not None and c[0] == key:
+        return c[1], c[2]
+    C = fc1.weight.shape[1]
+    dev = fc1.weight.device
+    st = torch.empty(int(_lib.fn("sfx_mlp_stream_floats")(C)), device=dev, dtype=torch.float32)
+    pr = torch.empty(int(_lib.fn("sfx_mlp_params_floats")(C)), device=dev, dtype=torch.float32)
+    ws = torch.empty(9 * C, device=dev, dtype=torch.int32)
+    w = [t.detach().contiguous() for t in ts]
+    call("sfx_mlp_pack", C, ptr(w[2]), ptr(w[3]), ptr(w[4]), ptr(w[5]), ptr(w[0]), ptr(w[1]), ptr(st), ptr(pr),
+         ptr(ws), stream())
+    fc1.__dict__["_sfx_mlp"] = (key, st, pr, w)
+    return st, pr
+
+
+def block_mlp_ok(x: Tensor, C: int) -> bool:
+    return MLP_FUSED and C in MLP_CHANNELS and x.dim() == 2 and x.stride(1) == 1 and x.data_ptr() % 16 == 0 \
+        and x.stride(0) % 4 == 0
+
+
+def block_mlp(x2: Tensor, ln2, fc1, fc2, out: Optional[Tensor] = None) -> Tensor:
+    """Y = x2 + fc2(GELU(fc1(LN2(x2)))) in one launch (Block.forward's norm2 / mlp / shortcut, calflops.py:72-82;
+    csrc/mlp.hip): the LayerNorm output and the [M, 4C] hidden stay on chip.  C in MLP_CHANNELS."""
+    M, C = x2.shape
+    st, pr = mlp_pack(ln2, fc1, fc2)
+    if out is None:
+        out = torch.empty(M, C, device=x2.device, dtype=torch.float32)
+    px, ldx = _rows(x2)
+    py, ldy = _rows(out)
+    call("sfx_block_mlp", M, C, px, ldx, ptr(st), ptr(pr), float(ln2.eps), py, ldy, stream())
+    return out
 
 
 def layernorm(x: Tensor, gamma: Tensor, beta: Tensor, eps: float, out: Optional[Tensor] = None) -> Tensor:

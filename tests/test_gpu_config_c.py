@@ -106,7 +106,7 @@ def hip_c(device):
     names = [k for k in sd if "attn.qkv" in k]
     return dict(sd=sd, scene=scene, perms=perms, masks=masks.masks, relu=relu, packed=cpu(packed),
                 d_packed=cpu(d_packed), views=vcap, cams=make_cameras(RES, RES, n_views=VIEWS),
-                grads={k: cpu(mpar[k].grad) for k in names}, names=names, loss=float(loss))
+                grads={k: cpu(mpar[k].grad) for k in names}, names=names, loss=float(loss.detach()))
 
 
 def _oracle(hip, dtype):

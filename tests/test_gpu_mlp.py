@@ -1,0 +1,84 @@
+"""Fused Block MLP tail (csrc/mlp.hip, sfx_block_mlp): Y = X + fc2(GELU(fc1(LN2(X)))) -- reference Block.forward
+restated in calflops.py:72-82 (norm2 -> mlp -> + shortcut) -- against the fp64 torch reference of the same ops,
+at the bar of the GEMM family's tests (relative L2 <= 2e-6, each row's error within 4x that of torch's fp32 CPU
+evaluation of the unfused ops), for every channel count the kernel serves and ragged point counts."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from splatformer_amd import ptv3_ops as ops
+from test_gpu_ptv3 import rel_l2
+
+pytestmark = pytest.mark.gpu
+
+
+def _mods(C, seed):
+    g = torch.Generator().manual_seed(seed)
+    ln = torch.nn.LayerNorm(C)
+    fc1, fc2 = torch.nn.Linear(C, 4 * C), torch.nn.Linear(4 * C, C)
+    with torch.no_grad():
+        ln.weight.copy_(torch.rand(C, generator=g) + 0.5)
+        ln.bias.copy_(torch.randn(C, generator=g) * 0.1)
+        for lin in (fc1, fc2):
+            lin.weight.copy_(torch.randn(lin.weight.shape, generator=g) / lin.weight.shape[1] ** 0.5)
+            lin.bias.copy_(torch.randn(lin.bias.shape, generator=g) * 0.1)
+    return ln, fc1, fc2
+
+
+def _ref(x, ln, fc1, fc2, dtype):
+    x = x.to(dtype)
+    h = F.layer_norm(x, (x.shape[1],), ln.weight.to(dtype), ln.bias.to(dtype), ln.eps)
+    m = F.gelu(F.linear(h, fc1.weight.to(dtype), fc1.bias.to(dtype)))
+    return x + F.linear(m, fc2.weight.to(dtype), fc2.bias.to(dtype))
+
+
+@pytest.mark.parametrize("C", ops.MLP_CHANNELS)
+@pytest.mark.parametrize("M", [1, 63, 4097])
+def test_block_mlp_matches_fp64(device, C, M):
+    ln, fc1, fc2 = _mods(C, C + M)
+    g = torch.Generator().manual_seed(M)
+    x = torch.randn(M, C, generator=g) * 2.0
+    x[::3] *= 1e3   # rows of very different magnitudes (LayerNorm normalises them; the residual keeps them)
+    x[1::5] *= 1e-3
+    ref = _ref(x, ln, fc1, fc2, torch.float64)
+    r32 = _ref(x, ln, fc1, fc2, torch.float32).double()
+    lnd, f1d, f2d = ln.to(device), fc1.to(device), fc2.to(device)
+    y = ops.block_mlp(x.to(device), lnd, f1d, f2d).cpu().double()
+    assert torch.isfinite(y).all()
+    # the MLP branch (Y - X) is what the kernel computes; the residual add is exact up to one rounding
+    br, bh, b32 = ref - x.double(), y - x.double(), r32 - x.double()
+    # (rows scaled by 1e3 carry the fp32 rounding of the residual add: the bar is relative to torch's fp32 error)
+    assert rel_l2(bh, br) <= max(2e-6, 2 * rel_l2(b32, br)), (rel_l2(bh, br), rel_l2(b32, br))
+    e_row = (bh - br).norm(dim=1) / br.norm(dim=1).clamp_min(1e-30)
+    e32 = (b32 - br).norm(dim=1) / br.norm(dim=1).clamp_min(1e-30)
+    assert bool((e_row <= 4 * e32 + 1e-6).all()), float((e_row - 4 * e32).max())
+
+
+def test_block_mlp_strided_output_and_cache(device):
+    """Writes into a column slice of a wider buffer (the last Block writes into the head input, ld 120), and the
+    packed weights are rebuilt when a weight changes in place."""
+    C, M = 96, 1000
+    ln, fc1, fc2 = [m.to(device) for m in _mods(C, 3)]
+    x = torch.randn(M, C, generator=torch.Generator().manual_seed(1)).to(device)
+    buf = torch.full((M, 120), 7.0, device=device)
+    ops.block_mlp(x, ln, fc1, fc2, out=buf[:, :C])
+    ref = _ref(x.cpu(), ln.cpu(), fc1.cpu(), fc2.cpu(), torch.float64)
+    assert rel_l2(buf[:, :C].cpu().double() - x.cpu().double(), ref - x.cpu().double()) < 2e-6
+    assert bool((buf[:, C:] == 7.0).all())
+    with torch.no_grad():
+        fc1.weight.mul_(0.5)  # in-place change: bumps the version, so the packed stream is rebuilt
+    y2 = ops.block_mlp(x, ln, fc1, fc2)
+    ref2 = _ref(x.cpu(), ln.cpu(), fc1.cpu(), fc2.cpu(), torch.float64)
+    assert rel_l2(y2.cpu().double() - x.cpu().double(), ref2 - x.cpu().double()) < 2e-6
+
+
+def test_block_fused_equals_unfused(device):
+    """Block.run with the fused tail vs the LayerNorm + two-GEMM form (SFX_MLP_FUSED=0 path)."""
+    C, M = 128, 3001
+    ln, fc1, fc2 = [m.to(device) for m in _mods(C, 5)]
+    x = torch.randn(M, C, generator=torch.Generator().manual_seed(2)).to(device)
+    y = ops.block_mlp(x, ln, fc1, fc2)
+    h = ops.layernorm(x, ln.weight, ln.bias, ln.eps)
+    m = ops.linear(h, fc1.weight, fc1.bias, act=ops.ACT_GELU)
+    y0 = ops.linear(m, fc2.weight, fc2.bias, residual=x)
+    assert rel_l2((y - x).cpu(), (y0 - x).cpu()) < 4e-6
