@@ -31,6 +31,8 @@
 // ([2 halves][2 terms][32 channels][32 units, permuted]).  A phase = 2 slabs (16 KB) = 12 MFMAs per wave; the ring
 // holds RING phases, RING-1 in flight; one barrier per phase (RAW for the arriving slabs, WAR for the refilled
 // slot), counted vmcnt, raw s_barrier (no __syncthreads: its fence would drain the DMA queue).
+#include <cstdlib>
+
 #include "gemm_common.h"
 
 namespace {
@@ -40,7 +42,6 @@ using namespace sfxg;
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int MLP_BM = 64;          // points per workgroup
 constexpr int SLAB_BYTES = 8192;    // one streamed weight slab
 constexpr int PHASE_BYTES = 2 * SLAB_BYTES;
 
@@ -50,8 +51,6 @@ struct MlpGeom {
   static constexpr int NCH = C / 16;          // hidden chunks of 64 units (4C / 64)
   static constexpr int PPC = NB;              // phases per chunk (2 * NB slabs, 2 per phase)
   static constexpr int NP = NCH * PPC;        // phases per tile
-  static constexpr int RS = 2 * C + 16;       // LN2 image row stride in bytes (pad: conflict-free b128 reads)
-  static constexpr int IMG = 2 * MLP_BM * RS; // two term images
   static constexpr int PAR = 12 * C + 4;      // parameter table floats
 };
 
@@ -67,42 +66,78 @@ __device__ __forceinline__ int slab_off(int r, int q) {
   return r * 64 + ((((q >> 3) ^ (r >> 2)) & 3) << 4) + ((q & 7) << 1);
 }
 
-template <int RING>
-__device__ __forceinline__ void wait_vm_pipeline() {
-  // this wave's DMAs of the phase about to be read have landed: RING-2 younger phases (4 pieces each) may fly
-  if constexpr (RING == 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else if constexpr (RING == 3) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+// Before each phase's barrier: (RAW) this wave's DMAs of the phase about to be read have landed -- the younger
+// phases in flight (PIECES each) may still fly; (WAR) its LDS reads of the previous phase have returned
+// (lgkmcnt(0)), so the slot the phase refills after the barrier is no longer being read (cdna_hip_programming.md
+// §5, "Read a staged buffer one phase AFTER the wait that retires it": a slot restaged one phase after its last
+// read needs that lgkmcnt before the barrier).
+// erf GELU (torch approximate='none') with a branch-free erf: the two argument ranges of the device library's
+// erff (|x| < 1: odd polynomial; |x| >= 1: 1 - exp(-(|x| + |x| P(|x|))), same coefficients) are both evaluated
+// and selected, so the compiler can interleave the epilogue with the MFMA stream (the library form branches per
+// lane and splits the loop into ~30 basic blocks).
+__device__ __forceinline__ float erf_nb(float x) {
+  const float ax = fabsf(x);
+  const float t = ax * ax;
+  float p1 = __builtin_fmaf(t, -0x1.268bc2p-11f, 0x1.420828p-8f);
+  p1 = __builtin_fmaf(t, p1, -0x1.b5937p-6f);
+  p1 = __builtin_fmaf(t, p1, 0x1.ce077cp-4f);
+  p1 = __builtin_fmaf(t, p1, -0x1.81266p-2f);
+  p1 = __builtin_fmaf(t, p1, 0x1.06eba0p-3f);
+  const float r1 = __builtin_fmaf(ax, p1, ax);
+  float p2 = __builtin_fmaf(ax, 0x1.1d3156p-16f, -0x1.8d129p-12f);
+  p2 = __builtin_fmaf(ax, p2, 0x1.f9a6d2p-9f);
+  p2 = __builtin_fmaf(ax, p2, -0x1.8c3164p-6f);
+  p2 = __builtin_fmaf(ax, p2, 0x1.b4e9c8p-4f);
+  p2 = __builtin_fmaf(ax, p2, 0x1.4515fap-1f);
+  p2 = __builtin_fmaf(ax, p2, 0x1.078e50p-3f);
+  p2 = __builtin_fmaf(ax, p2, ax);
+  const float r2 = 1.0f - expf(-p2);
+  return __builtin_copysignf(ax < 1.0f ? r1 : r2, x);
+}
+__device__ __forceinline__ float gelu_nb(float x) { return 0.5f * x * (1.f + erf_nb(x * 0.70710678118654752f)); }
+
+template <int N>
+__device__ __forceinline__ void wait_vm_lgkm() {
+  static_assert(N >= 0 && N <= 63, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(N) : "memory");
 }
 
-template <int C, int RING>
-__global__ void __launch_bounds__(256, C <= 96 ? 2 : 1) mlp_kernel(int M, const float* __restrict__ X, long long ldx,
-                                                     const float* __restrict__ stream, const float* __restrict__ par,
-                                                     float eps, float* __restrict__ Y, long long ldy) {
+// One workgroup = WAVES x 32 points; wave w owns points [32 w, 32 w + 32) of the tile and computes every hidden
+// unit and every output channel for them, so nothing but the weights is shared: the LN2 output of a wave's points
+// lives in its registers as the fc1 B fragments (lane (r, h) holds point r's channels 16 t + 8 h .. + 7 for every
+// k-step t -- half a row per lane, LayerNorm statistics completed with the partner lane r + 32), and the weights
+// are read from the LDS ring by all WAVES waves (WAVES-fold reuse per DMA'd byte).
+template <int C, int WAVES, int RING>
+__global__ void __launch_bounds__(WAVES * 64, (WAVES == 4 && C > 128) ? 1 : 2)
+    mlp_kernel(int M, const float* __restrict__ X, long long ldx, const float* __restrict__ stream,
+               const float* __restrict__ par, float eps, float* __restrict__ Y, long long ldy, int rot) {
   using G = MlpGeom<C>;
-  constexpr int NB = G::NB, NP = G::NP, PPC = G::PPC, RS = G::RS;
-  constexpr int RING_OFF = G::IMG;
-  constexpr int PAR_OFF = RING_OFF + RING * PHASE_BYTES;
-  constexpr int PT_OFF = PAR_OFF + G::PAR * 4;
-  constexpr int LDS_BYTES = PT_OFF + MLP_BM * 16;
-  static_assert(LDS_BYTES <= 163840, "LDS budget");
-  static_assert(2 * NB * 4096 <= G::IMG, "the tile-end exchange reuses the LN2 image");
+  constexpr int NB = G::NB, NP = G::NP, PPC = G::PPC, NT = C / 16;  // NT: fc1 k-steps
+  constexpr int NTH = WAVES * 64;
+  constexpr int PIECES = 16 / WAVES;  // 1 KB LDS-DMA pieces per wave per phase
+  constexpr int PAR_OFF = RING * PHASE_BYTES;
+  constexpr int LDS_BYTES = PAR_OFF + G::PAR * 4;
+  static_assert(16 % WAVES == 0 && LDS_BYTES <= 163840, "geometry");
   __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
   float* s_par = reinterpret_cast<float*>(lds + PAR_OFF);
-  float* s_pt = reinterpret_cast<float*>(lds + PT_OFF);  // per point: 1/s (LN2 split), t (hidden scale), 1/t
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int pm = wid >> 1, cn = wid & 1;
   const int h = lane >> 5, r32 = lane & 31;
-  const int m0 = (int)blockIdx.x * MLP_BM;
+  const int prow = (int)blockIdx.x * (WAVES * 32) + wid * 32 + r32;  // this lane's point
+  const bool pok = prow < M;
 
-  // ---- weight stream: phase q -> ring slot q % RING; 16 pieces of 1 KB, 4 per wave ----
+  // ---- weight stream: logical phase q -> ring slot q % RING; rot: each workgroup starts at its own hidden
+  // chunk j0 and wraps, so the workgroups of an XCD read different parts of the stream at any moment
+  const int j0 = rot ? (int)(blockIdx.x % G::NCH) : 0;
   const char* gstream = reinterpret_cast<const char*>(stream);
   auto issue = [&](int q) {
-    const char* src = gstream + (size_t)q * PHASE_BYTES + wid * 4096 + lane * 16;
-    char* dst = lds + RING_OFF + (q % RING) * PHASE_BYTES + wid * 4096;
+    int jq = q / PPC + j0;
+    jq -= jq >= G::NCH ? G::NCH : 0;
+    const int sq = jq * PPC + (q - (q / PPC) * PPC);  // stream phase of logical phase q
+    const char* src = gstream + (size_t)sq * PHASE_BYTES + wid * (PIECES * 1024) + lane * 16;
+    char* dst = lds + (q % RING) * PHASE_BYTES + wid * (PIECES * 1024);
 #pragma unroll
-    for (int pc = 0; pc < 4; ++pc)
+    for (int pc = 0; pc < PIECES; ++pc)
       __builtin_amdgcn_global_load_lds(src + pc * 1024, (__attribute__((address_space(3))) void*)(dst + pc * 1024),
                                        16, 0, 0);
   };
@@ -110,83 +145,72 @@ __global__ void __launch_bounds__(256, C <= 96 ? 2 : 1) mlp_kernel(int M, const 
   for (int q = 0; q < RING - 1; ++q)
     if (q < NP) issue(q);
 
-  // ---- prologue: parameter table, X2 tile, LayerNorm, LN2 term images, per-point scales ----
-  for (int i = tid; i < G::PAR; i += 256) s_par[i] = par[i];
-  const int pt = tid >> 2, qd = tid & 3;  // 4 threads per point, float4 f = qd + 4 i
-  constexpr int NV = C / 16;
-  const unsigned Mu = (unsigned)M;
-  const __amdgpu_buffer_rsrc_t rX = rsrc_ext(X, Mu * (unsigned)ldx * 4u);
-  float4 v[NV];
-  const unsigned xrow = (unsigned)(m0 + pt) * (unsigned)ldx;
+  // ---- prologue: parameter table; this lane's half row of X2, LayerNorm, fc1 B fragments, scales ----
+  for (int i = tid; i < G::PAR; i += NTH) s_par[i] = par[i];
+  const __amdgpu_buffer_rsrc_t rX = rsrc_ext(X, (unsigned)M * (unsigned)ldx * 4u);
+  const unsigned xr = (unsigned)prow * (unsigned)ldx;
+  float4 v[2 * NT];  // channels 16 t + 8 h + 0..3 (v[2t]) and + 4..7 (v[2t+1])
 #pragma unroll
-  for (int i = 0; i < NV; ++i) v[i] = bload4(rX, (m0 + pt < M) ? (xrow + 4u * (unsigned)(qd + 4 * i)) * 4u : OOB);
-  float s = 0.f;
+  for (int t = 0; t < NT; ++t) {
+    const unsigned c = (unsigned)(16 * t + 8 * h);
+    v[2 * t] = bload4(rX, pok ? (xr + c) * 4u : OOB);
+    v[2 * t + 1] = bload4(rX, pok ? (xr + c + 4u) * 4u : OOB);
+  }
+  float sm = 0.f;
 #pragma unroll
-  for (int i = 0; i < NV; ++i) s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
-  s += __shfl_xor(s, 1, 64);
-  s += __shfl_xor(s, 2, 64);
-  const float mean = s / (float)C;
+  for (int i = 0; i < 2 * NT; ++i) sm += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+  sm += __shfl_xor(sm, 32, 64);
+  const float mean = sm / (float)C;
   float q2 = 0.f;
 #pragma unroll
-  for (int i = 0; i < NV; ++i) {
+  for (int i = 0; i < 2 * NT; ++i) {
     const float a = v[i].x - mean, b = v[i].y - mean, c = v[i].z - mean, d = v[i].w - mean;
     q2 += (a * a + b * b) + (c * c + d * d);
   }
-  q2 += __shfl_xor(q2, 1, 64);
-  q2 += __shfl_xor(q2, 2, 64);
+  q2 += __shfl_xor(q2, 32, 64);
   const float rstd = 1.f / sqrtf(q2 / (float)C + eps);
   __syncthreads();  // s_par visible (no DMA is waited for here: only plain stores precede it)
   float mx = 0.f, nrm = 0.f;
 #pragma unroll
-  for (int i = 0; i < NV; ++i) {
-    const int c = 4 * (qd + 4 * i);
-    const float4 g = *reinterpret_cast<const float4*>(s_par + c);
-    const float4 b = *reinterpret_cast<const float4*>(s_par + C + c);
-    v[i] = make_float4((v[i].x - mean) * rstd * g.x + b.x, (v[i].y - mean) * rstd * g.y + b.y,
-                       (v[i].z - mean) * rstd * g.z + b.z, (v[i].w - mean) * rstd * g.w + b.w);
-    mx = fmaxf(mx, fmaxf(fmaxf(fabsf(v[i].x), fabsf(v[i].y)), fmaxf(fabsf(v[i].z), fabsf(v[i].w))));
-    nrm += (v[i].x * v[i].x + v[i].y * v[i].y) + (v[i].z * v[i].z + v[i].w * v[i].w);
-  }
-  mx = fmaxf(mx, __shfl_xor(mx, 1, 64));
-  mx = fmaxf(mx, __shfl_xor(mx, 2, 64));
-  nrm += __shfl_xor(nrm, 1, 64);
-  nrm += __shfl_xor(nrm, 2, 64);
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int c = 16 * t + 8 * h + 4 * u;
+      const float4 g = *reinterpret_cast<const float4*>(s_par + c);
+      const float4 b = *reinterpret_cast<const float4*>(s_par + C + c);
+      float4& w = v[2 * t + u];
+      w = make_float4((w.x - mean) * rstd * g.x + b.x, (w.y - mean) * rstd * g.y + b.y,
+                      (w.z - mean) * rstd * g.z + b.z, (w.w - mean) * rstd * g.w + b.w);
+      mx = fmaxf(mx, fmaxf(fmaxf(fabsf(w.x), fabsf(w.y)), fmaxf(fabsf(w.z), fabsf(w.w))));
+      nrm += (w.x * w.x + w.y * w.y) + (w.z * w.z + w.w * w.w);
+    }
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  nrm += __shfl_xor(nrm, 32, 64);
   int e = 0;
   if (mx > 0.f && mx <= 3.4028235e38f) e = row_exp(mx) + 1;  // row max in [2^13, 2^14)
-  const float sc = ldexpf(1.f, e);
+  const float sc = ldexpf(1.f, e), sinv = ldexpf(1.f, -e);
   // hidden bound: |GELU(z)| <= max(|z|, 0.17), |z| <= ||h2|| max||W1_u|| + max|b1| (1.001: the sums' rounding)
   const float U = fmaxf((sqrtf(nrm) * s_par[12 * C] + s_par[12 * C + 1]) * 1.001f, 0.17f);
   int et = 0;
   if (U <= 3.4028235e38f) et = row_exp(U) + 2;  // bound in [2^14, 2^15)
-  if (qd == 0) {
-    s_pt[4 * pt + 0] = ldexpf(1.f, -e);
-    s_pt[4 * pt + 1] = ldexpf(1.f, et);
-    s_pt[4 * pt + 2] = ldexpf(1.f, -et);
-  }
+  const float tsc = ldexpf(1.f, et), tinv = ldexpf(1.f, -et);
+  f16x8 hb[NT][2];  // fc1 B fragments [k-step][term]
 #pragma unroll
-  for (int i = 0; i < NV; ++i) {
-    uint2 t[2];
-    split2h(v[i], sc, t);
-    const int c = 4 * (qd + 4 * i);
-    *reinterpret_cast<uint2*>(lds + pt * RS + 2 * c) = t[0];
-    *reinterpret_cast<uint2*>(lds + MLP_BM * RS + pt * RS + 2 * c) = t[1];
+  for (int t = 0; t < NT; ++t) {
+    uint2 lo[2], hi[2];
+    split2h(v[2 * t], sc, lo);
+    split2h(v[2 * t + 1], sc, hi);
+    hb[t][0] = __builtin_bit_cast(f16x8, make_uint4(lo[0].x, lo[0].y, hi[0].x, hi[0].y));
+    hb[t][1] = __builtin_bit_cast(f16x8, make_uint4(lo[1].x, lo[1].y, hi[1].x, hi[1].y));
   }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  const int ptw = pm * 32 + r32;  // this lane's point within the tile
-  const float4 ps = *reinterpret_cast<const float4*>(s_pt + 4 * ptw);
-  const float sinv = ps.x, tsc = ps.y, tinv = ps.z;
 
   floatx16 acc2[NB];
 #pragma unroll
   for (int b = 0; b < NB; ++b)
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc2[b][i] = 0.f;
-  floatx16 acc1;
-  f16x8 hf[2][2];  // hidden fragments: [k-step][term]
-
-  const char* img_h = lds + ptw * RS + 16 * h;           // LN2 h term, this lane's point, lane-half offset
-  const char* img_l = img_h + MLP_BM * RS;
+  floatx16 acc1[2];
+  f16x8 hf[2][2][2];  // hidden fragments: [unit block][k-step][term]
 
   auto mfma3 = [](const f16x8& ah, const f16x8& al, const f16x8& bh, const f16x8& bl, floatx16 c) {
     c = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, c, 0, 0, 0);  // smallest terms first
@@ -194,107 +218,103 @@ __global__ void __launch_bounds__(256, C <= 96 ? 2 : 1) mlp_kernel(int M, const 
     return __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, c, 0, 0, 0);
   };
 
-  // one slab of the chunk body: sl < NB -> fc1 slab sl (k = 32 sl .. +32), else fc2 slab sl - NB (channels)
-  auto slab = [&](const char* base, int sl, int j) {
-    const char* half = base + cn * 4096;  // this wave's [2 terms][32 rows][64 B]
-    if (sl < NB) {
+  // the 8 fragment pairs of one slab (both 32-row halves x 2 k-steps x 2 terms), read in one batch so the LDS
+  // latency is paid once per slab, not once per MFMA triple
+  auto load_frags = [&](const char* base, f16x8 (&fa)[2][2][2]) {
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
-        const int q = 16 * t + 8 * h;
-        const f16x8 ah = *reinterpret_cast<const f16x8*>(half + slab_off(r32, q));
-        const f16x8 al = *reinterpret_cast<const f16x8*>(half + 2048 + slab_off(r32, q));
-        const int ko = 2 * (32 * sl + 16 * t);
-        const f16x8 bh = *reinterpret_cast<const f16x8*>(img_h + ko);
-        const f16x8 bl = *reinterpret_cast<const f16x8*>(img_l + ko);
-        acc1 = mfma3(ah, al, bh, bl, acc1);
+        const char* half = base + cb * 4096;
+        const int o = slab_off(r32, 16 * t + 8 * h);
+        fa[cb][t][0] = *reinterpret_cast<const f16x8*>(half + o);
+        fa[cb][t][1] = *reinterpret_cast<const f16x8*>(half + 2048 + o);
       }
+  };
+  // one slab: sl < NB -> fc1 slab sl (input channels 32 sl .. +32, both 32-unit blocks), else fc2 slab sl - NB
+  auto slab = [&](const f16x8 (&fa)[2][2][2], int sl, int j) {
+    if (sl < NB) {
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+          acc1[cb] = mfma3(fa[cb][t][0], fa[cb][t][1], hb[2 * sl + t][0], hb[2 * sl + t][1], acc1[cb]);
       if (sl == NB - 1) {  // hidden chunk complete: bias, GELU, split -> fc2 B fragments (registers)
-        const float4* pp = reinterpret_cast<const float4*>(s_par + 2 * C + 2 * fc1_par_index(j, cn, h, 0));
-        float g[16];
 #pragma unroll
-        for (int i2 = 0; i2 < 8; ++i2) {
-          const float4 wb = pp[i2];  // (1/s_u, b1_u) of registers 2 i2, 2 i2 + 1
-          g[2 * i2 + 0] = gelu_erf(acc1[2 * i2 + 0] * (sinv * wb.x) + wb.y) * tsc;
-          g[2 * i2 + 1] = gelu_erf(acc1[2 * i2 + 1] * (sinv * wb.z) + wb.w) * tsc;
-        }
+        for (int cb = 0; cb < 2; ++cb) {
+          const float4* pp = reinterpret_cast<const float4*>(s_par + 2 * C + 2 * fc1_par_index(j, cb, h, 0));
+          float g[16];
 #pragma unroll
-        for (int st = 0; st < 2; ++st) {
-          unsigned uh[4], ul[4];
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const float x0 = g[8 * st + 2 * k], x1 = g[8 * st + 2 * k + 1];
-            uh[k] = sfx::pk_f16(x0, x1);
-            const sfx::sfx_f16x2 hh = __builtin_bit_cast(sfx::sfx_f16x2, uh[k]);
-            ul[k] = sfx::pk_f16(x0 - (float)hh.x, x1 - (float)hh.y);
+          for (int i2 = 0; i2 < 8; ++i2) {
+            const float4 wb = pp[i2];  // (1/s_u, b1_u) of registers 2 i2, 2 i2 + 1
+            g[2 * i2 + 0] = gelu_nb(acc1[cb][2 * i2 + 0] * (sinv * wb.x) + wb.y) * tsc;
+            g[2 * i2 + 1] = gelu_nb(acc1[cb][2 * i2 + 1] * (sinv * wb.z) + wb.w) * tsc;
           }
-          hf[st][0] = __builtin_bit_cast(f16x8, make_uint4(uh[0], uh[1], uh[2], uh[3]));
-          hf[st][1] = __builtin_bit_cast(f16x8, make_uint4(ul[0], ul[1], ul[2], ul[3]));
+#pragma unroll
+          for (int st = 0; st < 2; ++st) {
+            unsigned uh[4], ul[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              const float x0 = g[8 * st + 2 * k], x1 = g[8 * st + 2 * k + 1];
+              uh[k] = sfx::pk_f16(x0, x1);
+              const sfx::sfx_f16x2 hh = __builtin_bit_cast(sfx::sfx_f16x2, uh[k]);
+              ul[k] = sfx::pk_f16(x0 - (float)hh.x, x1 - (float)hh.y);
+            }
+            hf[cb][st][0] = __builtin_bit_cast(f16x8, make_uint4(uh[0], uh[1], uh[2], uh[3]));
+            hf[cb][st][1] = __builtin_bit_cast(f16x8, make_uint4(ul[0], ul[1], ul[2], ul[3]));
+          }
         }
       }
     } else {
       const int b = sl - NB;
 #pragma unroll
-      for (int st = 0; st < 2; ++st) {
-        const int q = 16 * st + 8 * h;
-        const f16x8 ah = *reinterpret_cast<const f16x8*>(half + slab_off(r32, q));
-        const f16x8 al = *reinterpret_cast<const f16x8*>(half + 2048 + slab_off(r32, q));
-        acc2[b] = mfma3(ah, al, hf[st][0], hf[st][1], acc2[b]);
-      }
+      for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+        for (int st = 0; st < 2; ++st)
+          acc2[b] = mfma3(fa[cb][st][0], fa[cb][st][1], hf[cb][st][0], hf[cb][st][1], acc2[b]);
     }
   };
 
   int p = 0;
-  for (int j = 0; j < G::NCH; ++j) {
+  for (int jl = 0; jl < G::NCH; ++jl) {
+    const int j = jl + j0 - (jl + j0 >= G::NCH ? G::NCH : 0);  // the hidden chunk of this logical chunk
 #pragma unroll
-    for (int i = 0; i < 16; ++i) acc1[i] = 0.f;
+    for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc1[cb][i] = 0.f;
 #pragma unroll
     for (int pi = 0; pi < PPC; ++pi, ++p) {
-      if (p + RING - 1 < NP) wait_vm_pipeline<RING>();
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tail: nothing younger than this phase in flight
+      if (p + RING - 1 < NP) wait_vm_lgkm<(RING - 2) * PIECES>();
+      else wait_vm_lgkm<0>();  // tail: nothing younger than this phase in flight
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");  // no LDS access moves across the barrier
       if (p + RING - 1 < NP) issue(p + RING - 1);  // refills the slot every wave finished before the barrier
-      const char* base = lds + RING_OFF + (p % RING) * PHASE_BYTES;
-      slab(base, 2 * pi, j);
-      slab(base + SLAB_BYTES, 2 * pi + 1, j);
+      const char* base = lds + (p % RING) * PHASE_BYTES;
+      f16x8 fa0[2][2][2], fa1[2][2][2];
+      load_frags(base, fa0);
+      load_frags(base + SLAB_BYTES, fa1);
+      slab(fa0, 2 * pi, j);
+      slab(fa1, 2 * pi + 1, j);
     }
   }
 
-  // ---- tile end: add the unit halves' partial sums (block b finishes on wave cn = b % 2), epilogue ----
-  __builtin_amdgcn_s_barrier();  // every wave is past its last LN2-image read: the image area is free
-  float* exch = reinterpret_cast<float*>(lds);
+  // ---- epilogue: Y = X2 + acc2 / (t s_c) + b2, 16-byte stores of 4 consecutive channels ----
+  const __amdgpu_buffer_rsrc_t rY = rsrc_ext(Y, (unsigned)M * (unsigned)ldy * 4u);
+  const unsigned yr = (unsigned)prow * (unsigned)ldy;
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
-    if ((b & 1) == cn) continue;
-    float4* d = reinterpret_cast<float4*>(exch + ((pm * NB + b) * 64 + lane) * 16);
-#pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4)
-      d[g4] = make_float4(acc2[b][4 * g4], acc2[b][4 * g4 + 1], acc2[b][4 * g4 + 2], acc2[b][4 * g4 + 3]);
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  const __amdgpu_buffer_rsrc_t rY = rsrc_ext(Y, Mu * (unsigned)ldy * 4u);
-  const int prow = m0 + ptw;
-  const bool pok = prow < M;
-  const unsigned yrow = (unsigned)prow * (unsigned)ldy, xr = (unsigned)prow * (unsigned)ldx;
-#pragma unroll
-  for (int b = 0; b < NB; ++b) {
-    if ((b & 1) != cn) continue;
-    const float4* o = reinterpret_cast<const float4*>(exch + ((pm * NB + b) * 64 + lane) * 16);
     const float4* pp = reinterpret_cast<const float4*>(s_par + 10 * C + 2 * fc2_par_index(b, h, 0));
 #pragma unroll
     for (int g4 = 0; g4 < 4; ++g4) {
-      const float4 ot = o[g4];
       const float4 w01 = pp[2 * g4], w23 = pp[2 * g4 + 1];  // (1/s_c, b2_c) of registers 4 g4 .. 4 g4 + 3
-      const int c0 = 32 * b + 8 * g4 + 4 * h;
-      const float4 xres = bload4(rX, pok ? (xr + (unsigned)c0) * 4u : OOB);
+      const unsigned c0 = (unsigned)(32 * b + 8 * g4 + 4 * h);
+      const float4 xres = bload4(rX, pok ? (xr + c0) * 4u : OOB);
       float4 y;
-      y.x = xres.x + ((acc2[b][4 * g4 + 0] + ot.x) * (tinv * w01.x) + w01.y);
-      y.y = xres.y + ((acc2[b][4 * g4 + 1] + ot.y) * (tinv * w01.z) + w01.w);
-      y.z = xres.z + ((acc2[b][4 * g4 + 2] + ot.z) * (tinv * w23.x) + w23.y);
-      y.w = xres.w + ((acc2[b][4 * g4 + 3] + ot.w) * (tinv * w23.z) + w23.w);
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, y), rY, pok ? (yrow + (unsigned)c0) * 4u : OOB,
-                                             0, 0);
+      y.x = xres.x + (acc2[b][4 * g4 + 0] * (tinv * w01.x) + w01.y);
+      y.y = xres.y + (acc2[b][4 * g4 + 1] * (tinv * w01.z) + w01.w);
+      y.z = xres.z + (acc2[b][4 * g4 + 2] * (tinv * w23.x) + w23.y);
+      y.w = xres.w + (acc2[b][4 * g4 + 3] * (tinv * w23.z) + w23.w);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, y), rY, pok ? (yr + c0) * 4u : OOB, 0, 0);
     }
   }
 }
@@ -406,10 +426,16 @@ int pack_impl(const float* w1, const float* b1, const float* w2, const float* b2
   return sfx::check_launch("sfx_mlp_pack");
 }
 
-template <int C, int RING>
+template <int C, int WAVES, int RING>
 int run_impl(int M, const float* x, long long ldx, const float* stream, const float* par, float eps, float* y,
              long long ldy, hipStream_t st) {
-  mlp_kernel<C, RING><<<sfx::ceil_div(M, MLP_BM), 256, 0, st>>>(M, x, ldx, stream, par, eps, y, ldy);
+  static int rot = -1;
+  if (rot < 0) {
+    const char* e = getenv("SFX_MLP_ROT");
+    rot = (e && *e) ? (atoi(e) != 0) : 1;
+  }
+  mlp_kernel<C, WAVES, RING><<<sfx::ceil_div(M, WAVES * 32), WAVES * 64, 0, st>>>(M, x, ldx, stream, par, eps, y, ldy,
+                                                                                 rot);
   return sfx::check_launch("sfx_block_mlp");
 }
 
@@ -449,10 +475,12 @@ int sfx_block_mlp(int M, int C, const float* x, long long ldx, const float* stre
   SFX_REQUIRE(x != y, "sfx_block_mlp: in-place output is not supported");
   hipStream_t st = sfx::as_stream(stream_);
   switch (C) {
-    case 64: return run_impl<64, 3>(M, x, ldx, stream, params, eps, y, ldy, st);
-    case 96: return run_impl<96, 3>(M, x, ldx, stream, params, eps, y, ldy, st);
-    case 128: return run_impl<128, 4>(M, x, ldx, stream, params, eps, y, ldy, st);
-    default: return run_impl<256, 4>(M, x, ldx, stream, params, eps, y, ldy, st);
+    // (waves, ring phases): 8 waves = 256 points per workgroup, 2 workgroups per CU for C <= 128 (64 KB ring);
+    // C = 256 needs 4 waves (its 128 point columns of LN2 fragments + output accumulators fill 512 registers)
+    case 64: return run_impl<64, 8, 4>(M, x, ldx, stream, params, eps, y, ldy, st);
+    case 96: return run_impl<96, 8, 4>(M, x, ldx, stream, params, eps, y, ldy, st);
+    case 128: return run_impl<128, 8, 4>(M, x, ldx, stream, params, eps, y, ldy, st);
+    default: return run_impl<256, 4, 8>(M, x, ldx, stream, params, eps, y, ldy, st);
   }
 }
 

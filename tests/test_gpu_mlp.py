@@ -2,6 +2,8 @@
 restated in calflops.py:72-82 (norm2 -> mlp -> + shortcut) -- against the fp64 torch reference of the same ops,
 at the bar of the GEMM family's tests (relative L2 <= 2e-6, each row's error within 4x that of torch's fp32 CPU
 evaluation of the unfused ops), for every channel count the kernel serves and ragged point counts."""
+import copy
+
 import pytest
 import torch
 import torch.nn.functional as F
@@ -25,6 +27,7 @@ def _mods(C, seed):
     return ln, fc1, fc2
 
 
+@torch.no_grad()
 def _ref(x, ln, fc1, fc2, dtype):
     x = x.to(dtype)
     h = F.layer_norm(x, (x.shape[1],), ln.weight.to(dtype), ln.bias.to(dtype), ln.eps)
@@ -62,13 +65,14 @@ def test_block_mlp_strided_output_and_cache(device):
     x = torch.randn(M, C, generator=torch.Generator().manual_seed(1)).to(device)
     buf = torch.full((M, 120), 7.0, device=device)
     ops.block_mlp(x, ln, fc1, fc2, out=buf[:, :C])
-    ref = _ref(x.cpu(), ln.cpu(), fc1.cpu(), fc2.cpu(), torch.float64)
+    cpu = lambda m: copy.deepcopy(m).cpu()  # (Module.cpu() moves in place)
+    ref = _ref(x.cpu(), cpu(ln), cpu(fc1), cpu(fc2), torch.float64)
     assert rel_l2(buf[:, :C].cpu().double() - x.cpu().double(), ref - x.cpu().double()) < 2e-6
     assert bool((buf[:, C:] == 7.0).all())
     with torch.no_grad():
         fc1.weight.mul_(0.5)  # in-place change: bumps the version, so the packed stream is rebuilt
     y2 = ops.block_mlp(x, ln, fc1, fc2)
-    ref2 = _ref(x.cpu(), ln.cpu(), fc1.cpu(), fc2.cpu(), torch.float64)
+    ref2 = _ref(x.cpu(), cpu(ln), cpu(fc1), cpu(fc2), torch.float64)
     assert rel_l2(y2.cpu().double() - x.cpu().double(), ref2 - x.cpu().double()) < 2e-6
 
 
