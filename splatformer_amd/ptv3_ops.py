@@ -50,8 +50,9 @@ _lib.register("sfx_mlp_params_floats", [I], Z)
 _lib.register("sfx_mlp_pack", [I, P, P, P, P, P, P, P, P, P, P])
 _lib.register("sfx_block_mlp", [I, I, P, L, P, P, F, P, L, P])
 _lib.register("sfx_split_planes", [I, I, I, P, L, P, L, P, P])
-_lib.register("sfx_gemm2", [I, I, I, I, P, L, P, P, I, P, L, P, P, P, P, I, I, P, L, P, P, L, P, I, P])
-_lib.register("sfx_gemm2_pairs", [I, I, P, L, P, P, P, P, P, L, P, I, P, L, P])
+_lib.register("sfx_gemm2", [I, I, I, I, P, L, P, I, P, I, P, L, P, P, P, P, I, I, P, L, P, P, L, P, I, P])
+_lib.register("sfx_gemm2_pairs", [I, I, P, L, P, I, P, P, P, L, P, P, L, P])
+_lib.register("sfx_gemm2_ok", [I, I, P, P, P, P, P, L, P, L])
 
 ACT_NONE, ACT_GELU, ACT_RELU, ACT_TANH = 0, 1, 2, 3
 # gemm.hip kCfgs: 128x128, 128x96, 128x64, 64x128, 64x64 (4 waves, 2 per CU), 256x128, 128x256 (8 waves)
@@ -276,7 +277,7 @@ def linear2(x, weight: Tensor, bias: Optional[Tensor] = None, *, act: int = ACT_
     pr, ldr = _rows(residual) if residual is not None else (None, 0)
     ys = new_amax(out.device) if y_amax else None
     gs = gather_idx.stride(0) if gather_idx is not None else 1
-    call("sfx_gemm2", 1 if gather_idx is not None else 0, M, N, xp.Kp, ptr(xp.buf), xp.plane, ptr(xp.inv),
+    call("sfx_gemm2", 1 if gather_idx is not None else 0, M, N, xp.Kp, ptr(xp.buf), xp.plane, ptr(xp.inv), xp.rows,
          ptr(gather_idx), gs, ptr(wp.buf), wp.plane, ptr(wp.inv), ptr(bias), ptr(scale), ptr(shift), act, act_ncols,
          pr, ldr, ptr(residual_idx), py, ldy, *_slot_args(ys), stream())
     return (out, ys) if y_amax else out
