@@ -55,7 +55,7 @@ F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense fp16 / bf16 MFMA (no
 # fp32-equivalent ceiling is the dense fp16 peak / 3.
 SPLIT_PEAK_TFLOPS = round(F16_MFMA_PEAK_TFLOPS / 3, 1)
 HBM_PEAK_GBS = 8000.0
-GEMM_FAMILY = ("gemm_kernel", "wgrad_kernel")  # kernel-name prefixes of the dominant family
+GEMM_FAMILY = ("gemm_kernel", "wgrad_kernel", "mlp_kernel")  # kernel-name prefixes of the dominant family
 
 
 def in_family(kernel_name: str) -> bool:
@@ -166,6 +166,10 @@ def _gemm_cost(kind, args, kw, res):
         cin = dx.shape[1]
         fl = 2.0 * (n + smap.num_pairs) * cin * cout
         return fl, (n * cout + 27 * cin * cout + 2 * n * cin + 27 * n) * f4, (n, cin, cout)
+    if kind == "block_mlp":  # fused LN2 + fc1 + GELU + fc2 + residual (csrc/mlp.hip): the two GEMMs' FLOPs
+        x = args[0]
+        M, C = x.shape
+        return 16.0 * M * C * C, (2 * M * C + 8 * C * C + 12 * C) * f4, (M, 4 * C, C)
     if kind == "cpe_residual_ln":  # timed only with SubM pair partials: the conv's own pair summation
         return 0.0, 0, tuple(args[1].shape)
     raise KeyError(kind)
@@ -187,7 +191,8 @@ class GemmTimer:
         self._saved = []
         for mod, name in [(ptv3_ops, "linear"), (ptv3_ops, "subm_conv"), (ptv3_ops, "grouped_linear"),
                           (train_ops, "linear_bwd_data"), (train_ops, "linear_wgrad"),
-                          (train_ops, "subm_conv_bwd_data"), (ptv3_ops, "cpe_residual_ln")]:
+                          (train_ops, "subm_conv_bwd_data"), (ptv3_ops, "cpe_residual_ln"),
+                          (ptv3_ops, "block_mlp")]:
             fn = getattr(mod, name)
             self._saved.append((mod, name, fn))
             setattr(mod, name, self._wrap(name, fn))

@@ -548,7 +548,7 @@ __global__ void __launch_bounds__(256) split_planes_kernel(int rows, int K, int 
     }
     m = sfx::wave_max(m);
     int e = 0;
-    if (m > 0.f && m <= 3.4028235e38f) e = row_exp(m) + 2;
+    if (m > 0.f && m <= 3.4028235e38f) e = min(row_exp(m) + 2, 126);
     const float sc = ldexpf(1.f, e);
     typedef _Float16 h4 __attribute__((ext_vector_type(4)));
 #pragma unroll
@@ -570,7 +570,7 @@ __global__ void __launch_bounds__(256) split_planes_kernel(int rows, int K, int 
     for (int c = lane; c < K; c += 64) m = fmaxf(m, fabsf(s[c]));
     m = sfx::wave_max(m);
     int e = 0;
-    if (m > 0.f && m <= 3.4028235e38f) e = row_exp(m) + 2;
+    if (m > 0.f && m <= 3.4028235e38f) e = min(row_exp(m) + 2, 126);
     const float sc = ldexpf(1.f, e);
     for (int c = lane; c < Kp; c += 64) {
       const float x = c < K ? s[c] * sc : 0.f;

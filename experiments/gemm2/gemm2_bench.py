@@ -10,6 +10,8 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from splatformer_amd import _lib  # noqa: E402
 from splatformer_amd import ptv3_ops as ops  # noqa: E402
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import gemm2_ops as g2  # noqa: E402
 
 SHAPES = [(37759, 256, 768), (37759, 256, 1024), (37759, 1024, 256), (37759, 256, 256), (70349, 128, 512),
           (70349, 512, 128), (90434, 384, 96), (16000, 512, 2048), (14764, 512, 1536)]
@@ -44,8 +46,8 @@ def quick():
     for M, K, N in SHAPES[:4]:
         x = torch.randn(M, K, device=dev)
         w, b = torch.randn(N, K, device=dev), torch.randn(N, device=dev)
-        xp = ops.split_planes(x)
-        out.append(f"{M}x{K}x{N} {timeit(lambda: ops.linear2(xp, w, b)):7.1f}")
+        xp = g2.split_planes(x)
+        out.append(f"{M}x{K}x{N} {timeit(lambda: g2.linear2(xp, w, b)):7.1f}")
     print(os.path.basename(os.environ.get("SFX_LIB", "libsfx.so")) + ": " + " | ".join(out), flush=True)
 
 
@@ -62,10 +64,10 @@ def main():
         fl = 2.0 * M * N * K
         y_ref = (x.double() @ w.double().t() + b.double())
         t_old = timeit(lambda: ops.linear(x, w, b))
-        xp = ops.split_planes(x)
-        t_split = timeit(lambda: ops.split_planes(x))
-        t_g2 = timeit(lambda: ops.linear2(xp, w, b))
-        y_old, y_new = ops.linear(x, w, b), ops.linear2(xp, w, b)
+        xp = g2.split_planes(x)
+        t_split = timeit(lambda: g2.split_planes(x))
+        t_g2 = timeit(lambda: g2.linear2(xp, w, b))
+        y_old, y_new = ops.linear(x, w, b), g2.linear2(xp, w, b)
         den = y_ref.norm()
         e_old = float((y_old.double() - y_ref).norm() / den)
         e_new = float((y_new.double() - y_ref).norm() / den)
@@ -77,7 +79,7 @@ def main():
         # gathered rows (centre tap of a SubM conv): every other row, a few -1
         idx = torch.arange(0, M, 2, device=dev, dtype=torch.int32)
         idx[::97] = -1
-        yg = ops.linear2(xp, w, b, gather_idx=idx)
+        yg = g2.linear2(xp, w, b, gather_idx=idx)
         xg = torch.where((idx >= 0)[:, None], x[idx.long().clamp(min=0)], torch.zeros((), device=dev))
         yg_ref = xg.double() @ w.double().t() + b.double()
         print(f"    gather: rel err {float((yg.double() - yg_ref).norm() / yg_ref.norm()):.1e}", flush=True)

@@ -7,6 +7,8 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from splatformer_amd import _lib  # noqa: E402
 from splatformer_amd import ptv3_ops as ops  # noqa: E402
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import gemm2_ops as g2  # noqa: E402
 
 
 def main():
@@ -33,7 +35,7 @@ def main():
         for name, (kw, ref) in cases.items():
             kw = dict(kw)
             bias = kw.pop("bias", None)
-            y = ops.linear2(x, w, bias, **kw)
+            y = g2.linear2(x, w, bias, **kw)
             e = (y.double() - ref).abs()
             bad = (e > 1e-4 * ref.abs().max()).nonzero()
             print(f"M={M} {name:8s} rel {float(e.norm() / ref.norm()):.2e} bad {bad.shape[0]} first {bad[:4].tolist()}",

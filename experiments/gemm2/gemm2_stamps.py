@@ -9,6 +9,8 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from splatformer_amd import _lib  # noqa: E402
 from splatformer_amd import ptv3_ops as ops  # noqa: E402
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import gemm2_ops as g2  # noqa: E402
 
 SHAPES = [(37759, 256, 768), (37759, 256, 1024), (37759, 1024, 256), (37759, 256, 256)]
 
@@ -21,10 +23,10 @@ def main():
     for M, K, N in SHAPES:
         x = torch.randn(M, K, device=dev)
         w, b = torch.randn(N, K, device=dev), torch.randn(N, device=dev)
-        xp = ops.split_planes(x)
+        xp = g2.split_planes(x)
         for _ in range(5):
             buf.zero_()
-            ops.linear2(xp, w, b)
+            g2.linear2(xp, w, b)
         torch.cuda.synchronize()
         st = buf.view(-1, 4).cpu()
         st = st[st[:, 0] > 0].double()

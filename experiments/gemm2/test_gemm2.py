@@ -5,15 +5,24 @@ bias / BN-affine / GELU / residual epilogue."""
 import pytest
 import torch
 
+import os
+import sys
+
 pytestmark = pytest.mark.gpu
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 
 @pytest.fixture(scope="module")
 def ops():
+    """The experiment's ops; needs SFX_LIB=experiments/gemm2/libsfx_gemm2.so (bash experiments/gemm2/build.sh)."""
+    if "gemm2" not in os.environ.get("SFX_LIB", ""):
+        pytest.skip("set SFX_LIB=experiments/gemm2/libsfx_gemm2.so")
     from splatformer_amd import _lib
+    import gemm2_ops
     from splatformer_amd import ptv3_ops
     _lib.load()
-    return ptv3_ops
+    gemm2_ops.ACT_GELU = ptv3_ops.ACT_GELU
+    return gemm2_ops
 
 
 def _err(y, ref):
@@ -28,7 +37,7 @@ def test_dense(ops, M, K, N):
     x = torch.randn(M, K, device=dev) * torch.rand(M, 1, device=dev).mul(8).exp2()
     w = torch.randn(N, K, device=dev) / K ** 0.5
     b = torch.randn(N, device=dev)
-    y = ops.linear2(x, w, b)
+    y = g2.linear2(x, w, b)
     ref = x.double() @ w.double().t() + b.double()
     assert _err(y, ref) < 2e-6  # fp32 arithmetic error (~1e-7 at these K)
 
@@ -43,11 +52,11 @@ def test_epilogue(ops):
         w = torch.randn(N, K, device=dev) / K ** 0.5
         b, sc, sh = torch.randn(N, device=dev), torch.rand(N, device=dev) + 0.5, torch.randn(N, device=dev)
         r = torch.randn(M, N, device=dev)
-        y = ops.linear2(x, w, b, scale=sc, shift=sh, act=ops.ACT_GELU, act_ncols=256)
+        y = g2.linear2(x, w, b, scale=sc, shift=sh, act=ops.ACT_GELU, act_ncols=256)
         z = (x.double() @ w.double().t() + b.double()) * sc.double() + sh.double()
         z[:, :256] = torch.nn.functional.gelu(z[:, :256])
         assert _err(y, z) < 2e-6
-        y = ops.linear2(x, w, b, residual=r)
+        y = g2.linear2(x, w, b, residual=r)
         ref = x.double() @ w.double().t() + b.double() + r.double()
         assert _err(y, ref) < 2e-6
 
@@ -60,7 +69,7 @@ def test_gather(ops):
     w = torch.randn(N, K, device=dev) / K ** 0.5
     idx = torch.randint(0, M, (5003,), device=dev, dtype=torch.int32)
     idx[::13] = -1
-    y = ops.linear2(x, w, None, gather_idx=idx)
+    y = g2.linear2(x, w, None, gather_idx=idx)
     xg = torch.where((idx >= 0)[:, None], x[idx.long().clamp(min=0)], torch.zeros((), device=dev))
     ref = xg.double() @ w.double().t()
     assert _err(y, ref) < 2e-6

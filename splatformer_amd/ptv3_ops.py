@@ -49,10 +49,6 @@ _lib.register("sfx_mlp_stream_floats", [I], Z)
 _lib.register("sfx_mlp_params_floats", [I], Z)
 _lib.register("sfx_mlp_pack", [I, P, P, P, P, P, P, P, P, P, P])
 _lib.register("sfx_block_mlp", [I, I, P, L, P, P, F, P, L, P])
-_lib.register("sfx_split_planes", [I, I, I, P, L, P, L, P, P])
-_lib.register("sfx_gemm2", [I, I, I, I, P, L, P, I, P, I, P, L, P, P, P, P, I, I, P, L, P, P, L, P, I, P])
-_lib.register("sfx_gemm2_pairs", [I, I, P, L, P, I, P, P, P, L, P, P, L, P])
-_lib.register("sfx_gemm2_ok", [I, I, P, P, P, P, P, L, P, L])
 
 ACT_NONE, ACT_GELU, ACT_RELU, ACT_TANH = 0, 1, 2, 3
 # gemm.hip kCfgs: 128x128, 128x96, 128x64, 64x128, 64x64 (4 waves, 2 per CU), 256x128, 128x256 (8 waves)
@@ -217,69 +213,6 @@ def grouped_linear(x: Tensor, weight: Tensor, bias: Tensor, groups: int, *, act:
     call("sfx_linear", M, N, K, pa, lda, None, 1, ptr(weight), K, ptr(bias), None, None, act, -1, None, 0, None, py,
          ldy, None, 0, G, K, N * K, N, N, None, None, 0, *_slot_args(a_amax), *_slot_args(w_amax),
          *_slot_args(ys), *weight_split(weight, G * N), stream())
-    return (out, ys) if y_amax else out
-
-
-# ---- pre-split operand planes + the LDS-DMA GEMM (csrc/gemm2.hip) ---------------------------------------------
-class Planes:
-    """fp16x2 planes of a fp32 matrix [rows, K]: buf = [2][rows][Kp] fp16 (h then l terms of X * 2^e_r, K padded
-    to Kp = ceil32(K) with zeros), inv[r] = 2^-e_r (sfx_split_planes)."""
-    __slots__ = ("buf", "inv", "rows", "K", "Kp")
-
-    def __init__(self, buf: Tensor, inv: Tensor, rows: int, K: int, Kp: int):
-        self.buf, self.inv, self.rows, self.K, self.Kp = buf, inv, rows, K, Kp
-
-    @property
-    def plane(self) -> int:
-        return self.rows * self.Kp
-
-
-def split_planes(x: Tensor, rows: Optional[int] = None) -> Planes:
-    rows = x.shape[0] if rows is None else rows
-    K = x.shape[1]
-    Kp = (K + 31) // 32 * 32
-    pa, lda = _rows(x)
-    buf = torch.empty(2 * max(rows, 1) * Kp, device=x.device, dtype=torch.float16)
-    inv = torch.empty(max(rows, 1), device=x.device, dtype=torch.float32)
-    call("sfx_split_planes", rows, K, Kp, pa, lda, ptr(buf), max(rows, 1) * Kp, ptr(inv), stream())
-    return Planes(buf, inv, max(rows, 1), K, Kp)
-
-
-def weight_planes(w: Tensor) -> Planes:
-    """Planes of a weight [N, K], cached on the tensor until its storage or version changes."""
-    key = (w.data_ptr(), w._version, tuple(w.shape))
-    c = w.__dict__.get("_sfx_wplanes")
-    if c is not None and c[0] == key:
-        return c[1]
-    p = split_planes(w.reshape(w.shape[0], -1))
-    w.__dict__["_sfx_wplanes"] = (key, p)
-    return p
-
-
-GEMM2_MIN = int(os.environ.get("SFX_GEMM2_MIN", "128"))  # N and K from which `linear` takes the gemm2 path
-
-
-def linear2(x, weight: Tensor, bias: Optional[Tensor] = None, *, act: int = ACT_NONE, act_ncols: int = -1,
-            scale: Optional[Tensor] = None, shift: Optional[Tensor] = None, residual: Optional[Tensor] = None,
-            residual_idx: Optional[Tensor] = None, out: Optional[Tensor] = None,
-            gather_idx: Optional[Tensor] = None, rows: Optional[int] = None, y_amax: bool = False):
-    """`linear` on pre-split planes (sfx_gemm2): x is a Tensor (split here) or Planes; gather_idx [M] / [M, 1]
-    selects A rows (-1 = zero row)."""
-    wp = weight_planes(weight)
-    xp = x if isinstance(x, Planes) else split_planes(x)
-    if xp.Kp != wp.Kp:
-        raise RuntimeError(f"linear2: x has {xp.K} features, weight expects {wp.K}")
-    N = weight.shape[0]
-    M = (gather_idx.shape[0] if gather_idx is not None else (xp.rows if rows is None else rows))
-    if out is None:
-        out = torch.empty(M, N, device=weight.device, dtype=torch.float32)
-    py, ldy = _rows(out)
-    pr, ldr = _rows(residual) if residual is not None else (None, 0)
-    ys = new_amax(out.device) if y_amax else None
-    gs = gather_idx.stride(0) if gather_idx is not None else 1
-    call("sfx_gemm2", 1 if gather_idx is not None else 0, M, N, xp.Kp, ptr(xp.buf), xp.plane, ptr(xp.inv), xp.rows,
-         ptr(gather_idx), gs, ptr(wp.buf), wp.plane, ptr(wp.inv), ptr(bias), ptr(scale), ptr(shift), act, act_ncols,
-         pr, ldr, ptr(residual_idx), py, ldy, *_slot_args(ys), stream())
     return (out, ys) if y_amax else out
 
 

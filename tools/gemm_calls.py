@@ -44,7 +44,9 @@ def main():
         k[2] += fl
     tot = sum(v[1] for v in agg.values())
     for k, (c, ms, fl) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
-        print(f"{k[0]:15s} M={k[1]:6d} N={k[2]:5d} K={k[3]:5d} calls={c:3d} {ms:7.3f} ms {fl / ms / 1e9:6.1f} TF/s")
+        dims = tuple(k[1:]) + (0,) * (3 - len(k[1:]))  # cpe_residual_ln (pair sums) has (rows, C)
+        print(f"{k[0]:15s} M={dims[0]:6d} N={dims[1]:5d} K={dims[2]:5d} calls={c:3d} {ms:7.3f} ms "
+              f"{fl / ms / 1e9:6.1f} TF/s")
     fl = sum(p[3] for p in per)
     print(f"total {tot:.2f} ms / scene, {fl / tot / 1e9:.1f} TF/s")
 
