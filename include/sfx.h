@@ -356,6 +356,27 @@ int sfx_rasterize_fwd_views(int views, int tiles_x, int tiles_y, int block_width
                             const int32_t* gids_sorted, const int* tile_bins, const float* xys, const float* conics,
                             const float* colors, const float* opacity, const float* background, int clamp_max1,
                             float* final_Ts, int* final_idx, float* out_img, float* out_alpha, void* stream);
+/* (ABI v9) exact contribution culling for the eval path (replaces sfx_isect_emit_views + the tile counts of
+ * sfx_render_prep_project_views; same reference call site gs_utils.py:96-109 -> gsplat bin_and_sort_gaussians):
+ * a (Gaussian, tile) pair of gsplat's 3-sigma square is kept unless alpha < 1/255 at every pixel centre of the
+ * tile (minimum of the conic over the tile, double precision, with a margin for the fp32 per-pixel rounding).
+ * sfx_isect_count_cull_views writes the surviving tile count of every projected Gaussian into num_tiles_kept
+ * (gsplat's own counts stay in sfx_render_prep_project_views' num_tiles_hit: its per-view emptiness decides the
+ * empty-image branch); sfx_isect_emit_cull_views, over the inclusive scan of num_tiles_kept, writes the
+ * survivors (a subsequence of gsplat's list).  sfx_rasterize_fwd_views_quad = sfx_rasterize_fwd_views_packed with one
+ * 8x8 quadrant per wave and per-wave record lists (block_width 16); images / alphas / final T bit-identical to
+ * the unculled path, final_idx indexes the culled list. */
+int sfx_isect_count_cull_views(int n_total, int n_per_view, const float* xys, const float* conics,
+                               const float* opacities, const int* radii, int tiles_x, int tiles_y, int block_width,
+                               int img_h, int img_w, int* num_tiles_kept, void* stream);
+int sfx_isect_emit_cull_views(int n_total, int n_per_view, const float* xys, const float* conics,
+                              const float* opacities, const float* depths, const int* radii, const int* cum_tiles_hit,
+                              int tiles_x, int tiles_y, int block_width, int img_h, int img_w, int64_t* isect_ids,
+                              int32_t* gaussian_ids, void* stream);
+int sfx_rasterize_fwd_views_quad(int views, int tiles_x, int tiles_y, int block_width, int img_h, int img_w,
+                                 const int32_t* gids_sorted, const int* tile_bins, const float* records,
+                                 const float* background, int clamp_max1, float* final_Ts, int* final_idx,
+                                 float* out_img, float* out_alpha, void* stream);
 
 /* ---- evaluation post-processing ------------------------------------------------------------------
  * Replaces train.py:104-113 `(x*255).to(torch.uint8)` of prediction (after the gs_utils.py:111

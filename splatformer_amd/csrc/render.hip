@@ -790,6 +790,311 @@ rasterize_fwd_packed_kernel(int tiles_x, int tiles_y, int bw, int img_h, int img
   }
 }
 
+// ---- exact contribution culling (eval path, ABI v9) ---------------------------------------------------------
+// gsplat bins a Gaussian into every tile of its 3-sigma square (get_tile_bbox) and the per-pixel loop then skips
+// it wherever alpha = min(0.999, o exp(-sigma)) < 1/255.  A (Gaussian, pixel box) pair can be dropped without
+// changing any output bit when no pixel centre in the box can pass that test: sigma is a positive-definite
+// quadratic in d = (x, y) - pixel, so its minimum over the box of d is 0 (centre inside) or on an edge (a 1-D
+// quadratic clamped to the edge).  The minimum is evaluated in fp32 and compared against a limit raised by
+// margins far above every rounding involved: the kernel's own fp32 sigma (relative error <= a few ulp *
+// (1 + rho) / (1 - rho), rho = |b| / sqrt(ac) <= 0.99 here), this evaluation, __expf / __logf (absolute 1e-4 on
+// the log threshold).  Near-degenerate (rho > 0.99), non-PD and non-finite conics or positions are never
+// dropped.  Dropped pairs are exactly ones the rasterizer would `continue` past for every pixel of the box, so
+// images, alphas and final T are bit-identical; only final_idx (a list position) refers to the shorter list.
+struct CullG {
+  float gx, gy, a, b, c, ia, ic, lim;  // lim: box minimum of sigma above which the box is dropped
+  bool never, always;                  // never: o < 1/255 everywhere; always: never drop (degenerate input)
+};
+
+__device__ __forceinline__ CullG cull_setup(float x, float y, float ca, float cb, float cc, float opac) {
+  CullG g;
+  g.gx = x; g.gy = y; g.a = ca; g.b = cb; g.c = cc;
+  g.ia = 0.f; g.ic = 0.f; g.lim = 0.f;
+  g.always = false; g.never = false;
+  const float ac = ca * cc;
+  if (!(ca > 0.f) || !(cc > 0.f) || !(cb * cb < 0.9801f * ac) || !isfinite(x) || !isfinite(y) || !isfinite(ac)) {
+    g.always = true;  // rho > 0.99, not positive definite, or non-finite
+    return g;
+  }
+  if (!(opac * 255.f >= 0.999f)) {  // o < 1/255 (minus 1e-3): alpha < 1/255 at every pixel; NaN: keep
+    if (opac * 255.f < 0.999f) g.never = true; else g.always = true;
+    return g;
+  }
+  const float rho = sqrtf(cb * cb / ac);
+  g.ia = 1.f / ca;
+  g.ic = 1.f / cc;
+  // may contribute iff sigma_min * (1 - 1e-4 / (1 - rho)) <= ln(255 o) + 2e-4
+  g.lim = (__logf(opac * 255.f) + 2e-4f) / (1.f - 1e-4f / (1.f - rho));
+  return g;
+}
+
+// May the Gaussian reach alpha >= 1/255 at a pixel centre of [px0, px1] x [py0, py1] (integer pixel bounds,
+// inclusive, already clipped to the image)?
+__device__ __forceinline__ bool cull_box_may_hit(const CullG& g, int px0, int px1, int py0, int py1) {
+  if (g.always) return true;
+  if (g.never || px0 > px1 || py0 > py1) return false;
+  // d = g - (p + 0.5) over the pixel centres
+  const float u0 = g.gx - ((float)px1 + 0.5f), u1 = g.gx - ((float)px0 + 0.5f);
+  const float v0 = g.gy - ((float)py1 + 0.5f), v1 = g.gy - ((float)py0 + 0.5f);
+  if (u0 <= 0.f && u1 >= 0.f && v0 <= 0.f && v1 >= 0.f) return true;
+  float m = 3.0e38f;
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    const float dx = e ? u1 : u0;
+    const float dy = fminf(fmaxf(-g.b * dx * g.ic, v0), v1);
+    m = fminf(m, 0.5f * (g.a * dx * dx + g.c * dy * dy) + g.b * dx * dy);
+    const float ey = e ? v1 : v0;
+    const float ex = fminf(fmaxf(-g.b * ey * g.ia, u0), u1);
+    m = fminf(m, 0.5f * (g.a * ex * ex + g.c * ey * ey) + g.b * ex * ey);
+  }
+  return m <= g.lim;
+}
+
+// Tiles of a Gaussian's gsplat square are visited in gsplat's order (row-major over the square).  Squares of up
+// to SMALL_AREA tiles are walked by their own lane; bigger ones (a few needles and near-camera Gaussians can
+// cover thousands of tiles) by the whole wave, 64 tiles per step, so no lane serialises a long walk.
+constexpr int CULL_SMALL_AREA = 16;
+
+struct CullWalk {
+  int x0, y0, x1, y1, area;
+  CullG g;
+};
+
+__device__ __forceinline__ CullWalk cull_walk_setup(int i, const float* __restrict__ xys,
+                                                    const float* __restrict__ conics, const float* __restrict__ opac,
+                                                    const int* __restrict__ radii, int tiles_x, int tiles_y, int bw) {
+  CullWalk w;
+  w.x0 = w.y0 = w.x1 = w.y1 = 0;
+  w.area = 0;
+  if (radii[i] > 0) {
+    get_tile_bbox(xys[2 * i], xys[2 * i + 1], (float)radii[i], tiles_x, tiles_y, bw, w.x0, w.y0, w.x1, w.y1);
+    w.area = max(0, (w.x1 - w.x0) * (w.y1 - w.y0));
+  }
+  if (w.area > 0)
+    w.g = cull_setup(xys[2 * i], xys[2 * i + 1], conics[3 * i], conics[3 * i + 1], conics[3 * i + 2], opac[i]);
+  return w;
+}
+
+__device__ __forceinline__ CullG cull_bcast(const CullG& g, int l) {
+  CullG o;
+  o.gx = __shfl(g.gx, l); o.gy = __shfl(g.gy, l); o.a = __shfl(g.a, l); o.b = __shfl(g.b, l);
+  o.c = __shfl(g.c, l); o.ia = __shfl(g.ia, l); o.ic = __shfl(g.ic, l); o.lim = __shfl(g.lim, l);
+  o.never = __shfl((int)g.never, l) != 0;
+  o.always = __shfl((int)g.always, l) != 0;
+  return o;
+}
+
+// tiles of the gsplat 3-sigma square that survive the culling test.  256 threads, one Gaussian per lane.
+__global__ void __launch_bounds__(256)
+isect_count_cull_kernel(int n, int n_per_view, const float* __restrict__ xys, const float* __restrict__ conics,
+                        const float* __restrict__ opac, const int* __restrict__ radii, int tiles_x, int tiles_y,
+                        int bw, int img_h, int img_w, int* __restrict__ num_tiles_kept) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  CullWalk w;
+  w.x0 = w.y0 = w.x1 = w.y1 = 0;  // empty walk for lanes without a Gaussian (or without surviving tiles)
+  w.area = 0;
+  w.g = cull_setup(0.f, 0.f, 0.f, 0.f, 0.f, 0.f);
+  if (i < n) w = cull_walk_setup(i, xys, conics, opac, radii, tiles_x, tiles_y, bw);
+  int cnt = 0;
+  if (w.area <= CULL_SMALL_AREA) {
+    for (int ty = w.y0; ty < w.y1; ++ty)
+      for (int tx = w.x0; tx < w.x1; ++tx)
+        cnt += cull_box_may_hit(w.g, tx * bw, min(tx * bw + bw, img_w) - 1, ty * bw, min(ty * bw + bw, img_h) - 1);
+  }
+  unsigned long long big = __ballot(w.area > CULL_SMALL_AREA);
+  while (big) {
+    const int l = __ffsll((long long)big) - 1;
+    big &= big - 1;
+    const CullG g = cull_bcast(w.g, l);
+    const int x0 = __shfl(w.x0, l), y0 = __shfl(w.y0, l), wx = __shfl(w.x1, l) - x0, area = __shfl(w.area, l);
+    int c = 0;
+    for (int base = 0; base < area; base += 64) {
+      const int k = base + lane;
+      const int tx = x0 + k % wx, ty = y0 + k / wx;
+      const bool hit = k < area &&
+                       cull_box_may_hit(g, tx * bw, min(tx * bw + bw, img_w) - 1, ty * bw, min(ty * bw + bw, img_h) - 1);
+      c += __popcll(__ballot(hit));
+    }
+    if (lane == l) cnt = c;
+  }
+  if (i < n) num_tiles_kept[i] = cnt;
+}
+
+// isect_emit_kernel over the surviving tiles only (same walk order: the list is a subsequence of gsplat's)
+__global__ void __launch_bounds__(256)
+isect_emit_cull_kernel(int n, int n_per_view, const float* __restrict__ xys, const float* __restrict__ conics,
+                       const float* __restrict__ opac, const float* __restrict__ depths,
+                       const int* __restrict__ radii, const int* __restrict__ cum_tiles_hit, int tiles_x,
+                       int tiles_y, int bw, int img_h, int img_w, int64_t* __restrict__ isect_ids,
+                       int32_t* __restrict__ gaussian_ids) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  CullWalk w;
+  w.x0 = w.y0 = w.x1 = w.y1 = 0;  // empty walk for lanes without a Gaussian (or without surviving tiles)
+  w.area = 0;
+  w.g = cull_setup(0.f, 0.f, 0.f, 0.f, 0.f, 0.f);
+  int cur = 0, end = 0;
+  if (i < n) {
+    cur = (i == 0) ? 0 : cum_tiles_hit[i - 1];
+    end = cum_tiles_hit[i];
+    if (end > cur) w = cull_walk_setup(i, xys, conics, opac, radii, tiles_x, tiles_y, bw);
+  }
+  const int64_t depth_id = i < n ? (int64_t)__float_as_int(depths[i]) & 0xffffffffll : 0;
+  const int64_t tile_base = (int64_t)(i / n_per_view) * tiles_x * tiles_y;
+  if (w.area <= CULL_SMALL_AREA) {
+    for (int ty = w.y0; ty < w.y1; ++ty)
+      for (int tx = w.x0; tx < w.x1; ++tx) {
+        if (!cull_box_may_hit(w.g, tx * bw, min(tx * bw + bw, img_w) - 1, ty * bw, min(ty * bw + bw, img_h) - 1))
+          continue;
+        if (cur >= end) break;  // never taken: the count kernel ran the same test on the same inputs
+        isect_ids[cur] = ((tile_base + (int64_t)ty * tiles_x + tx) << 32) | depth_id;
+        gaussian_ids[cur] = i;
+        ++cur;
+      }
+  }
+  const unsigned long long lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  unsigned long long big = __ballot(w.area > CULL_SMALL_AREA);
+  while (big) {
+    const int l = __ffsll((long long)big) - 1;
+    big &= big - 1;
+    const CullG g = cull_bcast(w.g, l);
+    const int x0 = __shfl(w.x0, l), y0 = __shfl(w.y0, l), wx = __shfl(w.x1, l) - x0, area = __shfl(w.area, l);
+    int pos = __shfl(cur, l);
+    const int stop = __shfl(end, l);
+    const int gi = __shfl(i, l);
+    const int64_t d = (int64_t)__shfl((long long)depth_id, l);
+    const int64_t tb = (int64_t)__shfl((long long)tile_base, l);
+    for (int base = 0; base < area; base += 64) {
+      const int k = base + lane;
+      const int tx = x0 + k % wx, ty = y0 + k / wx;
+      const bool hit = k < area &&
+                       cull_box_may_hit(g, tx * bw, min(tx * bw + bw, img_w) - 1, ty * bw, min(ty * bw + bw, img_h) - 1);
+      const unsigned long long bal = __ballot(hit);
+      const int p = pos + __popcll(bal & lt_mask);
+      if (hit && p < stop) {
+        isect_ids[p] = ((tb + (int64_t)ty * tiles_x + tx) << 32) | d;
+        gaussian_ids[p] = gi;
+      }
+      pos += __popcll(bal);
+    }
+  }
+}
+
+// rasterize_fwd_packed_kernel with per-wave Gaussian lists: the 16x16 tile is split into four 8x8 quadrants, one
+// per wave; while a batch is staged each lane tests its record against the four quadrants (cull_box_may_hit)
+// and every wave compacts the batch to the records that can reach its quadrant.  Each pixel still visits its
+// tile's Gaussians in list order and runs the identical arithmetic; it only skips records whose alpha is below
+// 1/255 at all of its quadrant's pixel centres -- the ones the per-pixel test would `continue` past -- so every
+// output is bit-identical to rasterize_fwd_packed_kernel over the same list.  bw must be 16.
+__global__ void __launch_bounds__(MAX_BLOCK)
+rasterize_fwd_quad_kernel(int tiles_x, int tiles_y, int img_h, int img_w, const int32_t* __restrict__ gids_sorted,
+                          const int* __restrict__ tile_bins, const float4* __restrict__ rec,
+                          const float* __restrict__ background, float* __restrict__ final_Ts,
+                          int* __restrict__ final_idx, float* __restrict__ out_img, float* __restrict__ out_alpha,
+                          int clamp_max1) {
+  // the per-pixel arithmetic spelled out with the exact contractions the compiler gives
+  // rasterize_fwd_packed_kernel / rasterize_fwd_kernel (their ISA: sigma = fma(dy, qx dx, 0.5 fma(dx, aw dx,
+  // dy (qy dy))), colour += vis c as fma, out = fma(T, bg, colour)), so the outputs match them bit for bit
+#pragma clang fp contract(off)
+  constexpr int BW = 16, BS = BW * BW;
+  __shared__ float4 r0_batch[BS];
+  __shared__ float4 r1_batch[BS];
+  __shared__ float r2_batch[BS];
+  __shared__ unsigned char mask_batch[BS];
+  __shared__ unsigned char wlist[4][BS];
+
+  const int tile_id = blockIdx.z * tiles_x * tiles_y + blockIdx.y * tiles_x + blockIdx.x;
+  if (blockIdx.z > 0) {
+    const long long po = (long long)blockIdx.z * img_h * img_w;
+    final_Ts += po; final_idx += po; out_img += 3 * po;
+    if (out_alpha) out_alpha += po;
+  }
+  const int tr = threadIdx.x;
+  const int lane = tr & 63, w = tr >> 6;
+  const int qx = (w & 1) * 8, qy = (w >> 1) * 8;
+  const unsigned pi = blockIdx.y * BW + qy + (lane >> 3), pj = blockIdx.x * BW + qx + (lane & 7);
+  const float px = (float)pj + 0.5f, py = (float)pi + 0.5f;
+  const bool inside = (pi < (unsigned)img_h && pj < (unsigned)img_w);
+  bool done = !inside;
+  // quadrant pixel boxes (clipped to the image) for the mask test
+  const int tx0 = blockIdx.x * BW, ty0 = blockIdx.y * BW;
+
+  const int range_x = tile_bins[2 * tile_id], range_y = tile_bins[2 * tile_id + 1];
+  const int num_batches = (range_y - range_x + BS - 1) / BS;
+  const unsigned long long lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+
+  float T = 1.f;
+  int cur_idx = 0;
+  float c0 = 0.f, c1 = 0.f, c2 = 0.f;
+  for (int b = 0; b < num_batches; ++b) {
+    if (__syncthreads_count(done) >= BS) break;
+    const int batch_start = range_x + BS * b;
+    const int idx = batch_start + tr;
+    unsigned m = 0;
+    if (idx < range_y) {
+      const long long g = gids_sorted[idx];
+      const float4 a = rec[3 * g];
+      const float4 q = rec[3 * g + 1];
+      r0_batch[tr] = a;
+      r1_batch[tr] = q;
+      r2_batch[tr] = reinterpret_cast<const float*>(rec + 3 * g + 2)[0];
+      const CullG cg = cull_setup(a.x, a.y, a.w, q.x, q.y, a.z);
+#pragma unroll
+      for (int qd = 0; qd < 4; ++qd) {
+        const int bx0 = tx0 + (qd & 1) * 8, by0 = ty0 + (qd >> 1) * 8;
+        m |= (unsigned)cull_box_may_hit(cg, bx0, min(bx0 + 8, img_w) - 1, by0, min(by0 + 8, img_h) - 1) << qd;
+      }
+    }
+    mask_batch[tr] = (unsigned char)m;
+    __syncthreads();
+    // this wave's list: batch positions whose record may reach the quadrant, in batch order
+    int cnt = 0;
+#pragma unroll
+    for (int ch = 0; ch < BS / 64; ++ch) {
+      const bool hit = (mask_batch[ch * 64 + lane] >> w) & 1;
+      const unsigned long long bal = __ballot(hit);
+      if (hit) wlist[w][cnt + __popcll(bal & lt_mask)] = (unsigned char)(ch * 64 + lane);
+      cnt += __popcll(bal);
+    }
+    __syncthreads();
+    for (int j = 0; (j < cnt) && !done; ++j) {
+      const int t = wlist[w][j];
+      const float4 a = r0_batch[t];
+      const float4 q = r1_batch[t];
+      const float dx = a.x - px, dy = a.y - py;
+      const float sigma = __builtin_fmaf(dy, q.x * dx, 0.5f * __builtin_fmaf(dx, a.w * dx, dy * (q.y * dy)));
+      const float alpha = fminf(0.999f, a.z * __expf(-sigma));
+      if (sigma < 0.f || alpha < 1.f / 255.f) continue;
+      const float next_T = T * (1.f - alpha);
+      if (next_T <= 1e-4f) {
+        done = true;
+        break;
+      }
+      const float vis = alpha * T;
+      c0 = __builtin_fmaf(vis, q.z, c0);
+      c1 = __builtin_fmaf(vis, q.w, c1);
+      c2 = __builtin_fmaf(vis, r2_batch[t], c2);
+      T = next_T;
+      cur_idx = batch_start + t;
+    }
+  }
+  if (inside) {
+    const int pix = pi * img_w + pj;
+    final_Ts[pix] = T;
+    final_idx[pix] = cur_idx;
+    float o0 = __builtin_fmaf(T, background[0], c0), o1 = __builtin_fmaf(T, background[1], c1),
+          o2 = __builtin_fmaf(T, background[2], c2);
+    if (clamp_max1) {
+      o0 = fminf(o0, 1.f); o1 = fminf(o1, 1.f); o2 = fminf(o2, 1.f);
+    }
+    out_img[3 * pix + 0] = o0;
+    out_img[3 * pix + 1] = o1;
+    out_img[3 * pix + 2] = o2;
+    if (out_alpha) out_alpha[pix] = 1.f - T;
+  }
+}
+
 // ---- rasterize backward -----------------------------------------------------
 __global__ void __launch_bounds__(MAX_BLOCK)
 rasterize_bwd_kernel(int tiles_x, int tiles_y, int bw, int img_h, int img_w,
@@ -1150,6 +1455,55 @@ int sfx_rasterize_fwd_views_packed(int views, int tiles_x, int tiles_y, int bloc
       tiles_x, tiles_y, block_width, img_h, img_w, gids_sorted, tile_bins, reinterpret_cast<const float4*>(records),
       background, final_Ts, final_idx, out_img, out_alpha, clamp_max1);
   return sfx::check_launch("sfx_rasterize_fwd_views_packed");
+}
+
+int sfx_isect_count_cull_views(int n_total, int n_per_view, const float* xys, const float* conics,
+                               const float* opacities, const int* radii, int tiles_x, int tiles_y, int block_width,
+                               int img_h, int img_w, int* num_tiles_kept, void* stream) {
+  SFX_REQUIRE(n_total >= 0 && n_per_view > 0 && n_total % n_per_view == 0, "sfx_isect_count_cull_views: bad sizes");
+  SFX_REQUIRE(block_width > 1 && block_width <= 16, "sfx_isect_count_cull_views: block_width must be in (1,16]");
+  SFX_REQUIRE(tiles_x == (img_w + block_width - 1) / block_width && tiles_y == (img_h + block_width - 1) / block_width,
+              "sfx_isect_count_cull_views: tile bounds do not match the image size");
+  if (n_total == 0) return SFX_OK;
+  SFX_REQUIRE(xys && conics && opacities && radii && num_tiles_kept, "sfx_isect_count_cull_views: null buffer");
+  isect_count_cull_kernel<<<sfx::ceil_div(n_total, 256), 256, 0, sfx::as_stream(stream)>>>(
+      n_total, n_per_view, xys, conics, opacities, radii, tiles_x, tiles_y, block_width, img_h, img_w, num_tiles_kept);
+  return sfx::check_launch("sfx_isect_count_cull_views");
+}
+
+int sfx_isect_emit_cull_views(int n_total, int n_per_view, const float* xys, const float* conics,
+                              const float* opacities, const float* depths, const int* radii, const int* cum_tiles_hit,
+                              int tiles_x, int tiles_y, int block_width, int img_h, int img_w, int64_t* isect_ids,
+                              int32_t* gaussian_ids, void* stream) {
+  SFX_REQUIRE(n_total >= 0 && n_per_view > 0 && n_total % n_per_view == 0, "sfx_isect_emit_cull_views: bad sizes");
+  SFX_REQUIRE(block_width > 1 && block_width <= 16, "sfx_isect_emit_cull_views: block_width must be in (1,16]");
+  SFX_REQUIRE(tiles_x == (img_w + block_width - 1) / block_width && tiles_y == (img_h + block_width - 1) / block_width,
+              "sfx_isect_emit_cull_views: tile bounds do not match the image size");
+  if (n_total == 0) return SFX_OK;
+  SFX_REQUIRE(xys && conics && opacities && depths && radii && cum_tiles_hit && isect_ids && gaussian_ids,
+              "sfx_isect_emit_cull_views: null buffer");
+  isect_emit_cull_kernel<<<sfx::ceil_div(n_total, 256), 256, 0, sfx::as_stream(stream)>>>(
+      n_total, n_per_view, xys, conics, opacities, depths, radii, cum_tiles_hit, tiles_x, tiles_y, block_width, img_h,
+      img_w, isect_ids, gaussian_ids);
+  return sfx::check_launch("sfx_isect_emit_cull_views");
+}
+
+int sfx_rasterize_fwd_views_quad(int views, int tiles_x, int tiles_y, int block_width, int img_h, int img_w,
+                                 const int32_t* gids_sorted, const int* tile_bins, const float* records,
+                                 const float* background, int clamp_max1, float* final_Ts, int* final_idx,
+                                 float* out_img, float* out_alpha, void* stream) {
+  SFX_REQUIRE(views >= 1 && views <= 65535, "sfx_rasterize_fwd_views_quad: bad view count");
+  SFX_REQUIRE(block_width == 16, "sfx_rasterize_fwd_views_quad: block_width must be 16");
+  SFX_REQUIRE(tiles_x == (img_w + 15) / 16 && tiles_y == (img_h + 15) / 16,
+              "sfx_rasterize_fwd_views_quad: tile bounds do not match the image size");
+  SFX_REQUIRE(tile_bins && records && background && final_Ts && final_idx && out_img,
+              "sfx_rasterize_fwd_views_quad: null buffer");
+  SFX_REQUIRE((reinterpret_cast<uintptr_t>(records) & 15) == 0, "sfx_rasterize_fwd_views_quad: records alignment");
+  dim3 grid(tiles_x, tiles_y, views);
+  rasterize_fwd_quad_kernel<<<grid, 256, 0, sfx::as_stream(stream)>>>(
+      tiles_x, tiles_y, img_h, img_w, gids_sorted, tile_bins, reinterpret_cast<const float4*>(records), background,
+      final_Ts, final_idx, out_img, out_alpha, clamp_max1);
+  return sfx::check_launch("sfx_rasterize_fwd_views_quad");
 }
 
 }  // extern "C"

@@ -25,6 +25,11 @@ from .gsplat_compat import (_RasterizeGaussians, bin_and_sort_gaussians, compute
                             project_gaussians, rasterize_gaussians, spherical_harmonics)
 
 BLOCK_WIDTH = 16
+# eval path: exact contribution culling + per-wave quadrant lists (ABI v9).  Images, alphas and final T are
+# bit-identical either way; SFX_RENDER_CULL=0 restores gsplat's full 3-sigma intersection list (the list the
+# intersection-level parity tests compare key for key).
+import os as _os
+RENDER_CULL = _os.environ.get("SFX_RENDER_CULL", "1") != "0"
 C0 = 0.28209479177387814
 
 
@@ -46,6 +51,9 @@ _lib.register("sfx_isect_emit_views", [I, I, P, P, P, P, I, I, I, P, P, P])
 _lib.register("sfx_rasterize_fwd_views", [I, I, I, I, I, I, P, P, P, P, P, P, P, I, P, P, P, P, P])
 _lib.register("sfx_pack_raster_records", [I, P, P, P, P, P, P])
 _lib.register("sfx_rasterize_fwd_views_packed", [I, I, I, I, I, I, P, P, P, P, I, P, P, P, P, P])
+_lib.register("sfx_isect_count_cull_views", [I, I, P, P, P, P, I, I, I, I, I, P, P])
+_lib.register("sfx_isect_emit_cull_views", [I, I, P, P, P, P, P, P, I, I, I, I, I, P, P, P])
+_lib.register("sfx_rasterize_fwd_views_quad", [I, I, I, I, I, I, P, P, P, P, I, P, P, P, P, P])
 
 
 def rasterize_gaussians_to_multiimgs(gs_params: Dict[str, Tensor], cameras: Dict) -> Tuple[List[Tensor], List[Tensor]]:
@@ -167,10 +175,19 @@ def _render_fused_views(gs, c2ws, cameras, meta=None):
     # asynchronous read, with the count-independent record packing enqueued in front of the wait
     cum = torch.empty(V * n, device=dev, dtype=torch.int32)
     rec = f(V * n, 12)  # packed 48-byte records: one gather per Gaussian in the rasterizer's batch fetch
+    bw = BLOCK_WIDTH
+    tiles_x, tiles_y = (W + bw - 1) // bw, (H + bw - 1) // bw
+    T = tiles_x * tiles_y
+    cull = RENDER_CULL and bw == 16
+    kept = tiles
     if n:
+        if cull:  # surviving tile counts (gsplat's 3-sigma counts stay in `tiles`)
+            kept = torch.empty(V * n, device=dev, dtype=torch.int32)
+            call("sfx_isect_count_cull_views", V * n, n, ptr(xys), ptr(conics), ptr(opac), ptr(radii), tiles_x,
+                 tiles_y, bw, H, W, ptr(kept), stream())
         tot_dev = torch.zeros(1, device=dev, dtype=torch.int32)
         ws = _lib.workspace(_lib.fn("sfx_scan_workspace_bytes")(V * n), dev)
-        call("sfx_scan_i32", V * n, ptr(tiles), ptr(cum), 1, ptr(ws), ws.numel(), ptr(tot_dev), stream())
+        call("sfx_scan_i32", V * n, ptr(kept), ptr(cum), 1, ptr(ws), ws.numel(), ptr(tot_dev), stream())
         ends_rd = _lib.HostRead(cum.view(V, n)[:, -1])
         call("sfx_pack_raster_records", V * n, ptr(xys), ptr(conics), ptr(rgbs), ptr(opac), ptr(rec), stream())
         ends = ends_rd.get()
@@ -179,16 +196,20 @@ def _render_fused_views(gs, c2ws, cameras, meta=None):
     total = ends[-1]
     # per-view intersection counts (gsplat's empty-image branch is per call: alpha = 1 there)
     per_view = [ends[0]] + [ends[v] - ends[v - 1] for v in range(1, V)]
-    bw = BLOCK_WIDTH
-    tiles_x, tiles_y = (W + bw - 1) // bw, (H + bw - 1) // bw
-    T = tiles_x * tiles_y
+    if cull and n and not all(per_view):  # rare: a view kept nothing -- is gsplat's own list empty too?
+        full = tiles.view(V, n).sum(1, dtype=torch.int64).tolist()
+        per_view = [max(c, int(f)) for c, f in zip(per_view, full)]
     out = f(V, H, W, 3)
     alpha = f(V, H, W)
     if total > 0:
         isect = f(total, dt=torch.int64)
         gids = f(total, dt=torch.int32)
-        call("sfx_isect_emit_views", V * n, n, ptr(xys), ptr(depths), ptr(radii), ptr(cum), tiles_x, tiles_y, bw,
-             ptr(isect), ptr(gids), stream())
+        if cull:
+            call("sfx_isect_emit_cull_views", V * n, n, ptr(xys), ptr(conics), ptr(opac), ptr(depths), ptr(radii),
+                 ptr(cum), tiles_x, tiles_y, bw, H, W, ptr(isect), ptr(gids), stream())
+        else:
+            call("sfx_isect_emit_views", V * n, n, ptr(xys), ptr(depths), ptr(radii), ptr(cum), tiles_x, tiles_y, bw,
+                 ptr(isect), ptr(gids), stream())
         isect_s, gids_s = torch.empty_like(isect), torch.empty_like(gids)
         key_bits = 32 + max(1, int(V * T - 1).bit_length())
         ws = _lib.workspace(_lib.fn("sfx_sort_workspace_bytes")(total), dev)
@@ -198,15 +219,20 @@ def _render_fused_views(gs, c2ws, cameras, meta=None):
         bins = f(V * T, 2, dt=torch.int32)
         call("sfx_tile_bins", total, ptr(isect_s), V * T, ptr(bins), stream())
         final_Ts, final_idx = f(V, H, W), f(V, H, W, dt=torch.int32)
-        call("sfx_rasterize_fwd_views_packed", V, tiles_x, tiles_y, bw, H, W, ptr(gids_s), ptr(bins), ptr(rec),
-             ptr(bg), 1, ptr(final_Ts), ptr(final_idx), ptr(out), ptr(alpha), stream())
+        call("sfx_rasterize_fwd_views_quad" if cull else "sfx_rasterize_fwd_views_packed", V, tiles_x, tiles_y, bw,
+             H, W, ptr(gids_s), ptr(bins), ptr(rec), ptr(bg), 1, ptr(final_Ts), ptr(final_idx), ptr(out),
+             ptr(alpha), stream())
+    elif any(c > 0 for c in per_view):  # every gsplat intersection culled: T = 1 at every pixel of those views
+        out[:] = torch.clamp(bg, max=1.0)
+        alpha.zero_()
     for v in range(V):
         if per_view[v] < 1:
             out[v] = torch.clamp(bg, max=1.0).expand(H, W, 3)
             alpha[v] = 1.0
     if meta is not None:
         meta.update(rgbs=rgbs, opacities=opac, xys=xys, depths=depths, radii=radii, conics=conics,
-                    num_tiles_hit=tiles.view(V, n), per_view=per_view, tiles_x=tiles_x, tiles_y=tiles_y)
+                    num_tiles_hit=tiles.view(V, n), num_tiles_kept=kept.view(V, n), per_view=per_view, tiles_x=tiles_x,
+                    tiles_y=tiles_y, culled=cull)
         if total > 0:
             meta.update(isect_sorted=isect_s, gids_sorted=gids_s, tile_bins=bins.view(V, T, 2), final_Ts=final_Ts,
                         final_idx=final_idx)

@@ -143,8 +143,8 @@ class Block(nn.Module):
         t = ops.subm_conv(xc, point.nbr, wf, bf, partials=ops.subm_partials_ok(xc, point.nbr, C))
         ln1 = self.norm1[0]
         x1, h = ops.cpe_residual_ln(t, x, ln_c.weight, ln_c.bias, ln1.weight, ln1.bias, ln1.eps)
-        qkv, q_amax = ops.linear(h, self.attn.qkv.weight, self.attn.qkv.bias, y_amax=True)
         oi = point.order_type[self.attn.order_index]
+        qkv, q_amax = ops.linear(h, self.attn.qkv.weight, self.attn.qkv.bias, y_amax=True)
         if self.attn.enable_flash:
             K, win3, nw = point_windows_flash(point, self.attn.patch_size_max)
             a = ops.window_attention_varlen(qkv, point.order_phys[oi], win3, nw, K, self.attn.num_heads, C,
@@ -153,9 +153,13 @@ class Block(nn.Module):
             K, win, nw = point_windows(point, self.attn.patch_size_max)
             a = ops.window_attention(qkv, point.order_phys[oi], win, nw, K, self.attn.num_heads, C, qkv_amax=q_amax)
         x2 = ops.linear(a, self.attn.proj.weight, self.attn.proj.bias, residual=x1)
+        return self._mlp_tail(point, x2, out)
+
+    def _mlp_tail(self, point: Point, x2: Tensor, out: Optional[Tensor]) -> Point:
+        """x += MLP(LN2 x) (calflops.py:72-82)."""
         ln2 = self.norm2[0]
         mlp = self.mlp[0]
-        if ops.block_mlp_ok(x2, C):  # norm2 -> fc1 -> GELU -> fc2 -> + shortcut in one launch (csrc/mlp.hip)
+        if ops.block_mlp_ok(x2, self.channels):  # norm2 -> fc1 -> GELU -> fc2 -> + shortcut in one launch (mlp.hip)
             point.feat = ops.block_mlp(x2, ln2, mlp.fc1, mlp.fc2, out=out)
             return point
         h2 = ops.layernorm(x2, ln2.weight, ln2.bias, ln2.eps)

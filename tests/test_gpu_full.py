@@ -45,6 +45,14 @@ class Workload:
             self.out_d = self.model([scene_d], [0])[0]
             self.perms = [list(p) for p in self.model.backbone.backbone.last_perms]
             self.rgbs, self.alphas, self.meta = gs_render.render_views_meta(self.out_d, self.cams_d)
+            # the same render without contribution culling (gsplat's full 3-sigma list): culling must not change
+            # a single output bit
+            cull0 = gs_render.RENDER_CULL
+            gs_render.RENDER_CULL = False
+            try:
+                self.rgbs_full, self.alphas_full, self.meta_full = gs_render.render_views_meta(self.out_d, self.cams_d)
+            finally:
+                gs_render.RENDER_CULL = cull0
             gt, _ = gs_render.rasterize_gaussians_to_multiimgs(scene_d, self.cams_d)
         torch.cuda.synchronize()
         self.out = {k: v.detach().cpu().contiguous() for k, v in self.out_d.items()}
@@ -74,11 +82,52 @@ def check_refine(w: Workload):
         assert err <= 1e-5, f"refined {k}: residual rel L2 {err:.3e}"
 
 
+def _view_list(M, v, n):
+    """View v's slice of a batched meta: (keys, gids, tile bins) in single-view numbering."""
+    T = M["tiles_x"] * M["tiles_y"]
+    keys = M["isect_sorted"].cpu()
+    view_of = keys >> 32
+    sel = (view_of >= v * T) & (view_of < (v + 1) * T)
+    start = int(sel.nonzero()[0]) if bool(sel.any()) else 0
+    bins = M["tile_bins"][v].cpu().clone()
+    nz = bins[:, 1] > bins[:, 0]
+    bins[nz] -= start
+    return keys[sel] - ((v * T) << 32), M["gids_sorted"].cpu()[sel] - v * n, bins
+
+
+def check_cull_view(w: Workload, v: int, m):
+    """The culled eval path (default) vs gsplat's full list: its (key, Gaussian) list is a subsequence of the
+    oracle's, its tile counts are <= gsplat's, and images / alphas / final T are bit-identical to the HIP render
+    of the full list (culling drops only Gaussians below 1/255 at every pixel of a tile or quadrant)."""
+    M, F = w.meta, w.meta_full
+    n = w.out["means"].shape[0]
+    assert M["culled"] and not F["culled"]
+    assert torch.equal(M["num_tiles_hit"][v].cpu(), m["num_tiles_hit"]), f"view {v}: gsplat tile counts differ"
+    got_t, exp_t = M["num_tiles_kept"][v].cpu(), m["num_tiles_hit"]
+    assert bool((got_t <= exp_t).all()), f"view {v}: culled tile count above gsplat's"
+    assert (M["per_view"][v] > 0) == (int(exp_t.sum()) > 0)
+    if int(got_t.sum()) > 0:
+        keys, gids, _ = _view_list(M, v, n)
+        assert keys.numel() == int(got_t.sum())
+        # subsequence: every (tile, Gaussian) pair is in the oracle's list, at increasing positions
+        ek, eg = m["isect_sorted"], m["gids_sorted"]
+        pos = {(int(t), int(g)): i for i, (t, g) in enumerate(zip((ek >> 32).tolist(), eg.tolist()))}
+        p = [pos[(int(t), int(g))] for t, g in zip((keys >> 32).tolist(), gids.tolist())]
+        assert all(b > a for a, b in zip(p, p[1:])), f"view {v}: culled list is not a subsequence of gsplat's"
+        assert torch.equal(keys, ek[torch.tensor(p, dtype=torch.long)]), f"view {v}: culled keys differ"
+    assert torch.equal(w.rgbs[v].cpu(), w.rgbs_full[v].cpu()), f"view {v}: culling changed the image"
+    assert torch.equal(w.alphas[v].cpu(), w.alphas_full[v].cpu()), f"view {v}: culling changed alpha"
+    if "final_Ts" in M:
+        assert torch.equal(M["final_Ts"][v].cpu(), F["final_Ts"][v].cpu()), f"view {v}: culling changed final T"
+
+
 def check_render_view(w: Workload, v: int):
-    """HIP eval render vs the oracle render of the same (HIP-refined) Gaussians, view v."""
+    """HIP eval render vs the oracle render of the same (HIP-refined) Gaussians, view v: the full (unculled)
+    list key for key, and the culled default path through check_cull_view."""
     c2w = w.cams["camera_to_worlds"][v]
     rr, ar, m = render_ref.rasterize_gaussians_to_singleimg(w.out, c2w, return_meta=True, **w.cams)
-    M = w.meta
+    check_cull_view(w, v, m)
+    M = w.meta_full
     n = w.out["means"].shape[0]
     for k in ["radii", "num_tiles_hit"]:
         got, exp = M[k][v].cpu(), m[k]

@@ -224,3 +224,69 @@ def test_batched_views_equal_per_view(device):
             assert torch.equal(rgbs[v], r1), v
             assert torch.equal(alphas[v], a1), v
     assert float(alphas[5].min()) == 1.0  # empty-branch quirk reproduced per view
+
+
+def _render_both(sd, cams):
+    """Eval render with and without exact contribution culling (ABI v9)."""
+    cull0 = gs_render.RENDER_CULL
+    try:
+        gs_render.RENDER_CULL = True
+        rc, ac, mc = gs_render.render_views_meta(sd, cams)
+        gs_render.RENDER_CULL = False
+        rf, af, mf = gs_render.render_views_meta(sd, cams)
+    finally:
+        gs_render.RENDER_CULL = cull0
+    return (rc, ac, mc), (rf, af, mf)
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_render_cull_bit_identical_adversarial(device, seed):
+    """Culling near its thresholds: opacities around 1/255, needle-thin and near-degenerate (rho -> 1)
+    conics, Gaussians sitting on tile and quadrant borders, image sizes that are not multiples of 16.  Images,
+    alphas and final T must be bit-identical to the full gsplat list; the culled list must be shorter."""
+    n = 6000
+    g = torch.Generator().manual_seed(100 + seed)
+    s = make_scene(n, 1, seed=seed)
+    logit = lambda p: math.log(p / (1.0 - p))
+    k = torch.randint(0, 4, (n,), generator=g)
+    op = s["opacities"].clone()
+    near = torch.tensor([logit(1 / 255.0)]) + 1e-4 * torch.randn(n, 1, generator=g)
+    op[k == 0] = near[k == 0]  # opacity at the 1/255 threshold
+    op[k == 1] = logit(0.999)
+    s["opacities"] = op
+    sc = s["scales"].clone()
+    sc[k == 2, 0] = sc[k == 2, 0] + 3.0   # needles: one axis 20x, another 1/20
+    sc[k == 2, 1] = sc[k == 2, 1] - 3.0
+    s["scales"] = sc
+    cams = make_cameras(200, 136, n_views=3)
+    sd, cd = to_device(s, device), to_device(cams, device)
+    with torch.no_grad():
+        (rc, ac, mc), (rf, af, mf) = _render_both(sd, cd)
+    torch.cuda.synchronize()
+    assert mc["culled"] and not mf["culled"]
+    assert mc["isect_sorted"].numel() < mf["isect_sorted"].numel()
+    for v in range(3):
+        assert torch.equal(rc[v], rf[v]), v
+        assert torch.equal(ac[v], af[v]), v
+        assert torch.equal(mc["final_Ts"][v], mf["final_Ts"][v]), v
+    # every kept (tile, Gaussian) pair is one of gsplat's, in gsplat's order
+    kf = zip((mf["isect_sorted"].cpu() >> 32).tolist(), mf["gids_sorted"].cpu().tolist())
+    pos = {tg: i for i, tg in enumerate(kf)}
+    p = [pos[tg] for tg in zip((mc["isect_sorted"].cpu() >> 32).tolist(), mc["gids_sorted"].cpu().tolist())]
+    assert all(b > a for a, b in zip(p, p[1:]))
+
+
+def test_render_cull_all_culled_view(device):
+    """A view whose every gsplat intersection is culled (opacities below 1/255) renders background with alpha 0
+    (gsplat's normal path), not the empty-list branch (alpha 1)."""
+    s = make_scene(500, 1, seed=3)
+    s["opacities"] = torch.full_like(s["opacities"], math.log((0.5 / 255) / (1 - 0.5 / 255)))
+    cams = to_device(make_cameras(64, 48, n_views=2), device)
+    sd = to_device(s, device)
+    with torch.no_grad():
+        (rc, ac, mc), (rf, af, mf) = _render_both(sd, cams)
+    assert mf["isect_sorted"].numel() > 0
+    for v in range(2):
+        assert torch.equal(rc[v], rf[v]), v
+        assert torch.equal(ac[v], af[v]), v
+        assert float(ac[v].max()) == 0.0
