@@ -377,6 +377,14 @@ int sfx_rasterize_fwd_views_quad(int views, int tiles_x, int tiles_y, int block_
                                  const int32_t* gids_sorted, const int* tile_bins, const float* records,
                                  const float* background, int clamp_max1, float* final_Ts, int* final_idx,
                                  float* out_img, float* out_alpha, void* stream);
+/* (ABI v9) sfx_rasterize_bwd over a culled list (sfx_isect_emit_cull_views, single view) and the final_idx of
+ * sfx_rasterize_fwd_views_quad: one 8x8 quadrant per wave with per-wave record lists; block_width 16.  Same
+ * contract as sfx_rasterize_bwd (outputs accumulated with float atomics: zero them first). */
+int sfx_rasterize_bwd_quad(int tiles_x, int tiles_y, int block_width, int img_h, int img_w, const int32_t* gids_sorted,
+                           const int* tile_bins, const float* xys, const float* conics, const float* colors,
+                           const float* opacity, const float* background, const float* final_Ts, const int* final_idx,
+                           const float* v_out, const float* v_out_alpha, float* v_xy, float* v_xy_abs, float* v_conic,
+                           float* v_rgb, float* v_opacity, void* stream);
 
 /* ---- evaluation post-processing ------------------------------------------------------------------
  * Replaces train.py:104-113 `(x*255).to(torch.uint8)` of prediction (after the gs_utils.py:111

@@ -1225,6 +1225,164 @@ rasterize_bwd_kernel(int tiles_x, int tiles_y, int bw, int img_h, int img_w,
   }
 }
 
+// rasterize_bwd_kernel over a culled list with rasterize_fwd_quad_kernel's layout: one 8x8 quadrant per wave
+// and, per batch, per-wave lists of the records that can reach the quadrant (cull_box_may_hit) and lie at or
+// before the wave's last contributing position (final_idx).  Every skipped record has alpha < 1/255 at each
+// pixel of the quadrant -- the per-pixel `valid` test would be false for all lanes -- so each pixel sees the same
+// contributions in the same back-to-front order; per-Gaussian sums per wave as before (one atomic per wave and
+// Gaussian that any lane of the wave touches).  bw = 16.
+__global__ void __launch_bounds__(MAX_BLOCK)
+rasterize_bwd_quad_kernel(int tiles_x, int tiles_y, int img_h, int img_w, const int32_t* __restrict__ gids_sorted,
+                          const int* __restrict__ tile_bins, const float* __restrict__ xys,
+                          const float* __restrict__ conics, const float* __restrict__ colors,
+                          const float* __restrict__ opacity, const float* __restrict__ background,
+                          const float* __restrict__ final_Ts, const int* __restrict__ final_idx,
+                          const float* __restrict__ v_out, const float* __restrict__ v_out_alpha,
+                          float* __restrict__ v_xy, float* __restrict__ v_xy_abs, float* __restrict__ v_conic,
+                          float* __restrict__ v_rgb, float* __restrict__ v_opacity) {
+  constexpr int BW = 16, BS = BW * BW;
+  __shared__ int id_batch[BS];
+  __shared__ float4 xyo_batch[BS];
+  __shared__ float4 conic_batch[BS];
+  __shared__ float4 rgb_batch[BS];
+  __shared__ unsigned char mask_batch[BS];
+  __shared__ unsigned char wlist[4][BS];
+
+  const int tile_id = blockIdx.y * tiles_x + blockIdx.x;
+  const int tr = threadIdx.x;
+  const int lane = tr & 63, w = tr >> 6;
+  const int qx = (w & 1) * 8, qy = (w >> 1) * 8;
+  const unsigned pi = blockIdx.y * BW + qy + (lane >> 3), pj = blockIdx.x * BW + qx + (lane & 7);
+  const float px = (float)pj + 0.5f, py = (float)pi + 0.5f;
+  const bool inside = (pi < (unsigned)img_h && pj < (unsigned)img_w);
+  const int pix = min((int)(pi * img_w + pj), img_w * img_h - 1);
+  const int tx0 = blockIdx.x * BW, ty0 = blockIdx.y * BW;
+
+  const float T_final = final_Ts[pix];
+  float T = T_final;
+  float buf0 = 0.f, buf1 = 0.f, buf2 = 0.f;
+  const int bin_final = inside ? final_idx[pix] : 0;
+  const int range_x = tile_bins[2 * tile_id], range_y = tile_bins[2 * tile_id + 1];
+  const int num_batches = (range_y - range_x + BS - 1) / BS;
+  const float vo0 = v_out[3 * pix], vo1 = v_out[3 * pix + 1], vo2 = v_out[3 * pix + 2];
+  const float voa = v_out_alpha ? v_out_alpha[pix] : 0.f;
+  const float bg0 = background[0], bg1 = background[1], bg2 = background[2];
+  const int wave_bin_final = sfx::wave_max_i(inside ? bin_final : -1);
+  const unsigned long long lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+
+  for (int b = 0; b < num_batches; ++b) {
+    __syncthreads();
+    const int batch_end = range_y - 1 - BS * b;
+    const int idx = batch_end - tr;
+    unsigned m = 0;
+    if (idx >= range_x) {
+      const int g = gids_sorted[idx];
+      const float4 xyo = make_float4(xys[2 * g], xys[2 * g + 1], opacity[g], 0.f);
+      const float4 con = make_float4(conics[3 * g], conics[3 * g + 1], conics[3 * g + 2], 0.f);
+      id_batch[tr] = g;
+      xyo_batch[tr] = xyo;
+      conic_batch[tr] = con;
+      rgb_batch[tr] = make_float4(colors[3 * g], colors[3 * g + 1], colors[3 * g + 2], 0.f);
+      const CullG cg = cull_setup(xyo.x, xyo.y, con.x, con.y, con.z, xyo.z);
+#pragma unroll
+      for (int qd = 0; qd < 4; ++qd) {
+        const int bx0 = tx0 + (qd & 1) * 8, by0 = ty0 + (qd >> 1) * 8;
+        m |= (unsigned)cull_box_may_hit(cg, bx0, min(bx0 + 8, img_w) - 1, by0, min(by0 + 8, img_h) - 1) << qd;
+      }
+    }
+    mask_batch[tr] = (unsigned char)m;
+    __syncthreads();
+    int cnt = 0;
+#pragma unroll
+    for (int ch = 0; ch < BS / 64; ++ch) {
+      const int t = ch * 64 + lane;
+      const bool hit = ((mask_batch[t] >> w) & 1) && (batch_end - t <= wave_bin_final);
+      const unsigned long long bal = __ballot(hit);
+      if (hit) wlist[w][cnt + __popcll(bal & lt_mask)] = (unsigned char)t;
+      cnt += __popcll(bal);
+    }
+    __syncthreads();
+    for (int j = 0; j < cnt; ++j) {
+      const int t = wlist[w][j];
+      bool valid = inside && (batch_end - t <= bin_final);
+      float alpha = 0.f, opac = 0.f, vis = 0.f, dx = 0.f, dy = 0.f;
+      float4 con = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (valid) {
+        con = conic_batch[t];
+        const float4 xyo = xyo_batch[t];
+        opac = xyo.z;
+        dx = xyo.x - px;
+        dy = xyo.y - py;
+        const float sigma = 0.5f * (con.x * dx * dx + con.z * dy * dy) + con.y * dx * dy;
+        vis = __expf(-sigma);
+        alpha = fminf(0.99f, opac * vis);
+        if (sigma < 0.f || alpha < 1.f / 255.f) valid = false;
+      }
+      if (!__any(valid)) continue;
+      float g_rgb0 = 0.f, g_rgb1 = 0.f, g_rgb2 = 0.f, g_c0 = 0.f, g_c1 = 0.f, g_c2 = 0.f;
+      float g_xy0 = 0.f, g_xy1 = 0.f, g_ax = 0.f, g_ay = 0.f, g_o = 0.f;
+      if (valid) {
+        const float ra = 1.f / (1.f - alpha);
+        T *= ra;
+        const float fac = alpha * T;
+        g_rgb0 = fac * vo0;
+        g_rgb1 = fac * vo1;
+        g_rgb2 = fac * vo2;
+        const float4 rgb = rgb_batch[t];
+        float v_alpha = 0.f;
+        v_alpha += (rgb.x * T - buf0 * ra) * vo0;
+        v_alpha += (rgb.y * T - buf1 * ra) * vo1;
+        v_alpha += (rgb.z * T - buf2 * ra) * vo2;
+        v_alpha += T_final * ra * voa;
+        v_alpha += -T_final * ra * bg0 * vo0;
+        v_alpha += -T_final * ra * bg1 * vo1;
+        v_alpha += -T_final * ra * bg2 * vo2;
+        buf0 += rgb.x * fac;
+        buf1 += rgb.y * fac;
+        buf2 += rgb.z * fac;
+        const float v_sigma = -opac * vis * v_alpha;
+        g_c0 = 0.5f * v_sigma * dx * dx;
+        g_c1 = v_sigma * dx * dy;
+        g_c2 = 0.5f * v_sigma * dy * dy;
+        g_xy0 = v_sigma * (con.x * dx + con.y * dy);
+        g_xy1 = v_sigma * (con.y * dx + con.z * dy);
+        g_ax = fabsf(g_xy0);
+        g_ay = fabsf(g_xy1);
+        g_o = vis * v_alpha;
+      }
+      g_rgb0 = sfx::wave_sum_dpp(g_rgb0);
+      g_rgb1 = sfx::wave_sum_dpp(g_rgb1);
+      g_rgb2 = sfx::wave_sum_dpp(g_rgb2);
+      g_c0 = sfx::wave_sum_dpp(g_c0);
+      g_c1 = sfx::wave_sum_dpp(g_c1);
+      g_c2 = sfx::wave_sum_dpp(g_c2);
+      g_xy0 = sfx::wave_sum_dpp(g_xy0);
+      g_xy1 = sfx::wave_sum_dpp(g_xy1);
+      g_o = sfx::wave_sum_dpp(g_o);
+      if (v_xy_abs) {
+        g_ax = sfx::wave_sum_dpp(g_ax);
+        g_ay = sfx::wave_sum_dpp(g_ay);
+      }
+      if (lane == 0) {
+        const int g = id_batch[t];
+        atomicAdd(v_rgb + 3 * g + 0, g_rgb0);
+        atomicAdd(v_rgb + 3 * g + 1, g_rgb1);
+        atomicAdd(v_rgb + 3 * g + 2, g_rgb2);
+        atomicAdd(v_conic + 3 * g + 0, g_c0);
+        atomicAdd(v_conic + 3 * g + 1, g_c1);
+        atomicAdd(v_conic + 3 * g + 2, g_c2);
+        atomicAdd(v_xy + 2 * g + 0, g_xy0);
+        atomicAdd(v_xy + 2 * g + 1, g_xy1);
+        if (v_xy_abs) {
+          atomicAdd(v_xy_abs + 2 * g + 0, g_ax);
+          atomicAdd(v_xy_abs + 2 * g + 1, g_ay);
+        }
+        atomicAdd(v_opacity + g, g_o);
+      }
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -1504,6 +1662,24 @@ int sfx_rasterize_fwd_views_quad(int views, int tiles_x, int tiles_y, int block_
       tiles_x, tiles_y, img_h, img_w, gids_sorted, tile_bins, reinterpret_cast<const float4*>(records), background,
       final_Ts, final_idx, out_img, out_alpha, clamp_max1);
   return sfx::check_launch("sfx_rasterize_fwd_views_quad");
+}
+
+int sfx_rasterize_bwd_quad(int tiles_x, int tiles_y, int block_width, int img_h, int img_w, const int32_t* gids_sorted,
+                           const int* tile_bins, const float* xys, const float* conics, const float* colors,
+                           const float* opacity, const float* background, const float* final_Ts, const int* final_idx,
+                           const float* v_out, const float* v_out_alpha, float* v_xy, float* v_xy_abs, float* v_conic,
+                           float* v_rgb, float* v_opacity, void* stream) {
+  SFX_REQUIRE(block_width == 16, "sfx_rasterize_bwd_quad: block_width must be 16");
+  SFX_REQUIRE(tiles_x == (img_w + 15) / 16 && tiles_y == (img_h + 15) / 16,
+              "sfx_rasterize_bwd_quad: tile bounds do not match the image size");
+  SFX_REQUIRE(tile_bins && xys && conics && colors && opacity && background && final_Ts && final_idx && v_out &&
+                  v_xy && v_conic && v_rgb && v_opacity,
+              "sfx_rasterize_bwd_quad: null buffer");
+  dim3 grid(tiles_x, tiles_y);
+  rasterize_bwd_quad_kernel<<<grid, 256, 0, sfx::as_stream(stream)>>>(
+      tiles_x, tiles_y, img_h, img_w, gids_sorted, tile_bins, xys, conics, colors, opacity, background, final_Ts,
+      final_idx, v_out, v_out_alpha, v_xy, v_xy_abs, v_conic, v_rgb, v_opacity);
+  return sfx::check_launch("sfx_rasterize_bwd_quad");
 }
 
 }  // extern "C"

@@ -8,6 +8,7 @@ Same names, argument order, return tuples and autograd behaviour as
 """
 from __future__ import annotations
 
+import os
 from typing import Optional, Tuple
 
 import torch
@@ -29,6 +30,19 @@ def deg_from_sh(num_bases: int) -> int:
     if num_bases not in d:
         raise ValueError(f"invalid number of SH bases: {num_bases}")
     return d[num_bases]
+
+
+# exact contribution culling (ABI v9, csrc/render.hip): the rasterizer runs over the (Gaussian, tile) pairs that
+# can reach alpha >= 1/255 -- forward outputs bit-identical, gradients the same sums in another atomic order.
+# SFX_RENDER_CULL=0 restores gsplat's full 3-sigma lists.
+CULL = os.environ.get("SFX_RENDER_CULL", "1") != "0"
+_I, _P = _lib.I, _lib.P
+_lib.register("sfx_isect_count_cull_views", [_I, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P])
+_lib.register("sfx_isect_emit_cull_views", [_I, _I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P])
+_lib.register("sfx_pack_raster_records", [_I, _P, _P, _P, _P, _P, _P])
+_lib.register("sfx_rasterize_fwd_views_quad", [_I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _I, _P, _P, _P, _P, _P])
+_lib.register("sfx_rasterize_bwd_quad", [_I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
+                                         _P, _P, _P])
 
 
 def _f32(t: Tensor) -> Tensor:
@@ -170,6 +184,11 @@ class _RasterizeGaussians(torch.autograd.Function):
             final_Ts = torch.zeros(H, W, device=dev)  # gsplat v0.1.11 empty-branch quirk (alpha == 1)
             final_idx = torch.zeros(H, W, device=dev, dtype=torch.int32)
             alpha = 1 - final_Ts
+        elif CULL and bw == 16:
+            out, alpha, final_Ts, final_idx, gids_sorted, tile_bins = _culled_forward(
+                n, xys, _f32(depths), radii.to(torch.int32).contiguous(), conics, colors, opacity, background, H, W,
+                tiles_x, tiles_y)
+            ctx.quad = True
         else:
             _, _, _, gids_sorted, tile_bins = bin_and_sort_gaussians(
                 n, num_isect, _f32(xys), _f32(depths), radii.to(torch.int32).contiguous(), cum,
@@ -181,6 +200,7 @@ class _RasterizeGaussians(torch.autograd.Function):
             call("sfx_rasterize_fwd", tiles_x, tiles_y, bw, H, W, ptr(gids_sorted), ptr(tile_bins), ptr(xys),
                  ptr(conics), ptr(colors), ptr(opacity), ptr(background), ptr(final_Ts), ptr(final_idx), ptr(out),
                  ptr(alpha), stream())
+        ctx.quad = getattr(ctx, "quad", False)
         ctx.img = (H, W, bw, tiles_x, tiles_y)
         ctx.save_for_backward(gids_sorted, tile_bins, xys, conics, colors, opacity, background, final_Ts, final_idx)
         if return_alpha:
@@ -201,12 +221,49 @@ class _RasterizeGaussians(torch.autograd.Function):
             v_out_img = _f32(v_out_img)
             v_out_alpha = _f32(v_out_alpha) if v_out_alpha is not None else None
             v_xy_abs = torch.zeros(n, 2, device=dev)
-            call("sfx_rasterize_bwd", tiles_x, tiles_y, bw, H, W, ptr(gids_sorted), ptr(tile_bins), ptr(xys),
+            call("sfx_rasterize_bwd_quad" if ctx.quad else "sfx_rasterize_bwd", tiles_x, tiles_y, bw, H, W,
+                 ptr(gids_sorted), ptr(tile_bins), ptr(xys),
                  ptr(conics), ptr(colors), ptr(opacity), ptr(background), ptr(final_Ts), ptr(final_idx),
                  ptr(v_out_img), ptr(v_out_alpha), ptr(v_xy), ptr(v_xy_abs), ptr(v_conic), ptr(v_rgb), ptr(v_op),
                  stream())
             xys.absgrad = v_xy_abs
         return (v_xy, None, None, v_conic, None, v_rgb, v_op) + (None,) * 5
+
+
+def _culled_forward(n, xys, depths, radii, conics, colors, opacity, background, H, W, tiles_x, tiles_y):
+    """The forward over the culled list (single view): surviving tile counts -> scan -> culled emission -> the
+    same stable sort and bins -> rasterize_fwd_views_quad.  Called when gsplat's own list is non-empty."""
+    dev = xys.device
+    kept = torch.empty(n, device=dev, dtype=torch.int32)
+    call("sfx_isect_count_cull_views", n, n, ptr(xys), ptr(conics), ptr(opacity), ptr(radii), tiles_x, tiles_y, 16, H,
+         W, ptr(kept), stream())
+    total, cum = compute_cumulative_intersects(kept)
+    num_tiles = tiles_x * tiles_y
+    final_Ts = torch.empty(H, W, device=dev, dtype=torch.float32)
+    final_idx = torch.empty(H, W, device=dev, dtype=torch.int32)
+    if total < 1:  # nothing reaches 1/255 anywhere: T = 1 at every pixel (gsplat's normal path, alpha 0)
+        out = background.reshape(1, 1, -1).expand(H, W, background.shape[0]).contiguous()
+        final_Ts.fill_(1.0)
+        final_idx.zero_()
+        return (out, torch.zeros(H, W, device=dev), final_Ts, final_idx,
+                torch.zeros(0, device=dev, dtype=torch.int32), torch.zeros(num_tiles, 2, device=dev, dtype=torch.int32))
+    isect = torch.empty(total, device=dev, dtype=torch.int64)
+    gids = torch.empty(total, device=dev, dtype=torch.int32)
+    call("sfx_isect_emit_cull_views", n, n, ptr(xys), ptr(conics), ptr(opacity), ptr(depths), ptr(radii), ptr(cum),
+         tiles_x, tiles_y, 16, H, W, ptr(isect), ptr(gids), stream())
+    isect_s, gids_s = torch.empty_like(isect), torch.empty_like(gids)
+    ws = _lib.workspace(_lib.fn("sfx_sort_workspace_bytes")(total), dev)
+    call("sfx_sort_pairs_u64", total, ptr(isect), ptr(gids), ptr(isect_s), ptr(gids_s), 0,
+         32 + max(1, int(num_tiles - 1).bit_length()), ptr(ws), ws.numel(), stream())
+    tile_bins = torch.empty(num_tiles, 2, device=dev, dtype=torch.int32)
+    call("sfx_tile_bins", total, ptr(isect_s), num_tiles, ptr(tile_bins), stream())
+    rec = torch.empty(n, 12, device=dev, dtype=torch.float32)
+    call("sfx_pack_raster_records", n, ptr(xys), ptr(conics), ptr(colors), ptr(opacity), ptr(rec), stream())
+    out = torch.empty(H, W, 3, device=dev, dtype=torch.float32)
+    alpha = torch.empty(H, W, device=dev, dtype=torch.float32)
+    call("sfx_rasterize_fwd_views_quad", 1, tiles_x, tiles_y, 16, H, W, ptr(gids_s), ptr(tile_bins), ptr(rec),
+         ptr(background), 0, ptr(final_Ts), ptr(final_idx), ptr(out), ptr(alpha), stream())
+    return out, alpha, final_Ts, final_idx, gids_s, tile_bins
 
 
 def rasterize_gaussians(xys: Tensor, depths: Tensor, radii: Tensor, conics: Tensor, num_tiles_hit: Tensor,

@@ -48,5 +48,39 @@ def main():
                   f"(min {min(ts):7.3f})", flush=True)
 
 
+def train_main(reps=5):
+    """Training render (autograd glue, gs_utils.py:32-113) of the bench scene's 4 training views at 800x800:
+    forward + backward per view, cull on / off; per-kernel times come from a rocprofv3 kernel trace."""
+    n, W, H, sh = CFG["B"]
+    dev = torch.device("cuda", 0)
+    _lib.load()
+    from splatformer_amd import gsplat_compat
+    scene = to_device(make_scene(n, sh_degree=sh, seed=0), dev)
+    cams = to_device(make_cameras(W, H, n_views=4), dev)
+    params = {k: v.clone().requires_grad_(True) for k, v in scene.items()}
+    for cull in (False, True, False, True):
+        gsplat_compat.CULL = cull
+        ts = []
+        for it in range(reps + 1):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            rgbs, _ = gs_render.rasterize_gaussians_to_multiimgs(params, cams)
+            loss = sum(r.sum() for r in rgbs)
+            loss.backward()
+            torch.cuda.synchronize()
+            if it:
+                ts.append(1e3 * (time.perf_counter() - t0))
+        g = params["means"].grad.norm().item()
+        for p in params.values():
+            p.grad = None
+        print(f"train render 4 views fwd+bwd cull={int(cull)} median {statistics.median(ts):7.3f} ms "
+              f"(min {min(ts):7.3f}) |grad means| {g:.6e}", flush=True)
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "train":
+    train_main()
+    sys.exit(0)
+
+
 if __name__ == "__main__":
     main()
