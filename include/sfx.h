@@ -327,6 +327,12 @@ int sfx_subm_conv_partials(int n, int cin, int cout, const float* x, long long l
                            const float* weight, const float* bias, const int* pair_in, const int* pair_out,
                            const int* pair_off_host, float* out, long long ldo, float* partials, long long ldp,
                            const float* w_split, const float* w_inv, void* stream);
+/* (ABI v10) the pair launch of sfx_subm_conv_partials alone, for a caller that made the centre launch first (an
+ * sfx_subm_conv_partials call with pair_in = NULL and 28 zero offsets) and only then waits for pair_off_host. */
+int sfx_subm_conv_partials_pairs(int n, int cin, int cout, const float* x, long long ldx, const int* nbr,
+                                 const float* weight, const float* bias, const int* pair_in, const int* pair_out,
+                                 const int* pair_off_host, float* out, long long ldo, float* partials, long long ldp,
+                                 const float* w_split, const float* w_inv, void* stream);
 
 /* FeaturePredictor batchify (feature_predictor.py:134-156): strided attribute rows -> feat rows
  * [means,scales,opacities,quats,dc,rest], grid_coord = floor(means*res), optional atomic grid max. */

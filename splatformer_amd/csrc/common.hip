@@ -133,7 +133,7 @@ extern "C" {
 
 const char* sfx_last_error(void) { return sfx::g_err; }
 
-int sfx_abi_version(void) { return 9; }
+int sfx_abi_version(void) { return 10; }
 
 size_t sfx_scan_workspace_bytes(long long n) {
   const long long tiles = (n + SCAN_TILE - 1) / SCAN_TILE;

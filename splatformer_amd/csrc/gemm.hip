@@ -1422,7 +1422,8 @@ static int subm_conv_impl(int n, int cin, int cout, const float* x, long long ld
                           const float* weight, const float* bias, const int* pair_in, const int* pair_out,
                           const int* pair_off_host, float* out, long long ldo, const unsigned long long* x_amax,
                           unsigned x_tag, const unsigned long long* w_amax, unsigned w_tag, const float* w_split,
-                          const float* w_inv, float* partials, long long ldp, void* stream) {
+                          const float* w_inv, float* partials, long long ldp, void* stream,
+                          bool skip_centre = false) {
   SFX_REQUIRE(n >= 0 && cin > 0 && cout > 0, "sfx_subm_conv: bad sizes");
   if (n == 0) return SFX_OK;
   SFX_REQUIRE(x && nbr && weight && out && pair_off_host, "sfx_subm_conv: null buffer");
@@ -1454,9 +1455,11 @@ static int subm_conv_impl(int n, int cin, int cout, const float* x, long long ld
                     AmaxJob{weight, 27ll * cin, 0, cout, 27 * cin, 1, nullptr, 0, 1}, st)) {
     a.a_amax = a.w_amax = nullptr;  // (dispatch falls back to bf16x3 for the pair launch)
   }
-  dispatch(a, 1, vec, st);
-  int rc = sfx::check_launch("sfx_subm_conv(centre)");
-  if (rc) return rc;
+  if (!skip_centre) {
+    dispatch(a, 1, vec, st);
+    int rc = sfx::check_launch("sfx_subm_conv(centre)");
+    if (rc) return rc;
+  }
   if (!pair_in || pair_off_host[27] == 0) return SFX_OK;
   // 2) the other 26 offsets as one flat tile list
   GemmArgs b = a;
@@ -1494,6 +1497,19 @@ int sfx_subm_conv_partials(int n, int cin, int cout, const float* x, long long l
               "sfx_subm_conv_partials: null partials / pair lists");
   return subm_conv_impl(n, cin, cout, x, ldx, nbr, weight, bias, pair_in, pair_out, pair_off_host, out, ldo, nullptr,
                         0, nullptr, 0, w_split, w_inv, partials, ldp, stream);
+}
+
+// The pair launch of sfx_subm_conv_partials alone (its centre launch made by an earlier sfx_subm_conv_partials call
+// with pair_in = NULL): the host can enqueue the centre GEMM before it waits for the pair offsets, so the GPU has
+// work while the offsets travel to the host.
+int sfx_subm_conv_partials_pairs(int n, int cin, int cout, const float* x, long long ldx, const int* nbr,
+                                 const float* weight, const float* bias, const int* pair_in, const int* pair_out,
+                                 const int* pair_off_host, float* out, long long ldo, float* partials, long long ldp,
+                                 const float* w_split, const float* w_inv, void* stream) {
+  SFX_REQUIRE(n == 0 || pair_off_host[27] == 0 || (partials && pair_in && pair_out),
+              "sfx_subm_conv_partials_pairs: null partials / pair lists");
+  return subm_conv_impl(n, cin, cout, x, ldx, nbr, weight, bias, pair_in, pair_out, pair_off_host, out, ldo, nullptr,
+                        0, nullptr, 0, w_split, w_inv, partials, ldp, stream, true);
 }
 
 // SubMConv3d backward w.r.t. its input: dX[in] += dY[out] W_k for every pair (in, out, k), centre included.

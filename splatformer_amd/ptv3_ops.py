@@ -6,6 +6,7 @@ fallback: a missing library or a CPU tensor raises.
 """
 from __future__ import annotations
 
+import ctypes
 import os
 from typing import List, Optional, Sequence, Tuple
 
@@ -41,6 +42,7 @@ _lib.register("sfx_subm_pairs_workspace_bytes", [I], Z)
 _lib.register("sfx_subm_pairs", [I, P, P, Z, P, P, P, P])
 _lib.register("sfx_subm_conv", [I, I, I, P, L, P, P, P, P, P, P, P, L, P, I, P, I, P, P, P])
 _lib.register("sfx_subm_conv_partials", [I, I, I, P, L, P, P, P, P, P, P, P, L, P, L, P, P, P])
+_lib.register("sfx_subm_conv_partials_pairs", [I, I, I, P, L, P, P, P, P, P, P, P, L, P, L, P, P, P])
 _lib.register("sfx_subm_pair_pos", [I, L, P, P, P, P])
 _lib.register("sfx_gs_pack", [I, P, L, P, L, P, L, P, L, P, L, P, L, I, F, P, L, P, P, P])
 _lib.register("sfx_offsets_to_batch", [I, I, P, P, P])
@@ -530,6 +532,10 @@ class SubmMap:
             self._pos = pos
         return self._pos
 
+    def pair_off_ready(self) -> bool:
+        """Whether the pair offsets are already on the host (reading them costs no wait)."""
+        return self._off is not None or isinstance(self._off_src, list)
+
     @property
     def pair_off(self) -> List[int]:
         if self._off is None:
@@ -576,6 +582,8 @@ def subm_neighbors(grid_coord: Tensor, batch: Optional[Tensor], with_pairs: bool
 
 # eval-path SubM convs: store per-pair partials and sum them in the consumer (default), or add them atomically
 SUBM_PARTIALS = os.environ.get("SFX_SUBM_ATOMIC", "0") != "1"
+# the first conv of a new SubM map enqueues its centre GEMM before waiting for the pair offsets
+SUBM_CENTRE_FIRST = os.environ.get("SFX_SUBM_CENTRE_FIRST", "1") != "0"
 PAIRS_LN_CHANNELS = (64, 96, 128, 256, 512)  # the channel counts sfx_cpe_residual_ln_pairs has kernels for
 
 
@@ -583,8 +591,13 @@ def subm_partials_ok(x: Tensor, smap: "SubmMap", cout: int) -> bool:
     """Whether the atomic-free SubM form can run for this launch: its consumer (sfx_cpe_residual_ln_pairs) needs
     C in PAIRS_LN_CHANNELS, 16-byte aligned contiguous rows and partials below the 2 GiB buffer range; other
     launches (e.g. enc_dim=32's C=32 stage 0, reference pointtransformer_v3.py:113) take the atomic form."""
+    # the 2 GiB partials bound from 26 n (no host wait for the pair count) unless that bound is too coarse
     return (SUBM_PARTIALS and cout in PAIRS_LN_CHANNELS and x.shape[1] == cout and x.is_contiguous()
-            and x.data_ptr() % 16 == 0 and smap.num_pairs * cout * 4 + 64 < 0x7ffffff0)
+            and x.data_ptr() % 16 == 0 and (26 * smap.nbr.shape[0] * cout * 4 + 64 < 0x7ffffff0
+                                            or smap.num_pairs * cout * 4 + 64 < 0x7ffffff0))
+
+
+_ZERO_OFFS = (ctypes.c_int * 28)()  # pair offsets of a centre-only sfx_subm_conv_partials call
 
 
 class SubmPartials:
@@ -618,11 +631,19 @@ def subm_conv(x: Tensor, smap: "SubmMap", weight: Tensor, bias: Optional[Tensor]
     px, ldx = _rows(x)
     po, ldo = _rows(out)
     if partials:
+        wsp = weight_split(weight)
+        if SUBM_CENTRE_FIRST and not smap.pair_off_ready():  # centre GEMM first, then wait for the pair offsets
+            call("sfx_subm_conv_partials", n, cin, cout, px, ldx, ptr(smap.nbr), ptr(weight), ptr(bias), None, None,
+                 _ZERO_OFFS, po, ldo, None, cout, *wsp, stream())
+            npairs = smap.num_pairs
+            part = torch.empty(max(1, npairs), cout, device=x.device, dtype=torch.float32)
+            call("sfx_subm_conv_partials_pairs", n, cin, cout, px, ldx, ptr(smap.nbr), ptr(weight), ptr(bias),
+                 ptr(smap.pair_in), ptr(smap.pair_out), smap._off_host, po, ldo, ptr(part), cout, *wsp, stream())
+            return SubmPartials(out, part, smap.pair_pos, npairs)
         npairs = smap.num_pairs
         part = torch.empty(max(1, npairs), cout, device=x.device, dtype=torch.float32)
         call("sfx_subm_conv_partials", n, cin, cout, px, ldx, ptr(smap.nbr), ptr(weight), ptr(bias),
-             ptr(smap.pair_in), ptr(smap.pair_out), smap._off_host, po, ldo, ptr(part), cout, *weight_split(weight),
-             stream())
+             ptr(smap.pair_in), ptr(smap.pair_out), smap._off_host, po, ldo, ptr(part), cout, *wsp, stream())
         return SubmPartials(out, part, smap.pair_pos, npairs)
     call("sfx_subm_conv", n, cin, cout, px, ldx, ptr(smap.nbr), ptr(weight), ptr(bias), ptr(smap.pair_in),
          ptr(smap.pair_out), smap._off_host, po, ldo, *_slot_args(x_amax), *_slot_args(w_amax),
