@@ -1269,6 +1269,32 @@ rasterize_bwd_quad_kernel(int tiles_x, int tiles_y, int img_h, int img_w, const 
   const float bg0 = background[0], bg1 = background[1], bg2 = background[2];
   const int wave_bin_final = sfx::wave_max_i(inside ? bin_final : -1);
   const unsigned long long lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  constexpr int RING = 8;
+  __shared__ float ring[4][RING][11][4];
+  __shared__ int ring_g[4][RING];
+  int nring = 0;  // records parked in this wave's ring (wave-uniform)
+  auto flush_ring = [&]() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int nv = v_xy_abs ? 11 : 9;
+    for (int e = lane; e < nring * nv; e += 64) {
+      const int jj = e / nv, c = e - jj * nv;
+      const float* q = ring[w][jj][c];
+      const float sum = (q[0] + q[1]) + (q[2] + q[3]);
+      const int g = ring_g[w][jj];
+      float* dst = c < 3 ? v_rgb + 3 * g + c
+                 : c < 6 ? v_conic + 3 * g + (c - 3)
+                 : c < 8 ? v_xy + 2 * g + (c - 6)
+                 : c == 8 ? v_opacity + g
+                          : v_xy_abs + 2 * g + (c - 9);
+      atomicAdd(dst, sum);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    nring = 0;
+  };
 
   for (int b = 0; b < num_batches; ++b) {
     __syncthreads();
@@ -1350,37 +1376,26 @@ rasterize_bwd_quad_kernel(int tiles_x, int tiles_y, int img_h, int img_w, const 
         g_ay = fabsf(g_xy1);
         g_o = vis * v_alpha;
       }
-      g_rgb0 = sfx::wave_sum_dpp(g_rgb0);
-      g_rgb1 = sfx::wave_sum_dpp(g_rgb1);
-      g_rgb2 = sfx::wave_sum_dpp(g_rgb2);
-      g_c0 = sfx::wave_sum_dpp(g_c0);
-      g_c1 = sfx::wave_sum_dpp(g_c1);
-      g_c2 = sfx::wave_sum_dpp(g_c2);
-      g_xy0 = sfx::wave_sum_dpp(g_xy0);
-      g_xy1 = sfx::wave_sum_dpp(g_xy1);
-      g_o = sfx::wave_sum_dpp(g_o);
-      if (v_xy_abs) {
-        g_ax = sfx::wave_sum_dpp(g_ax);
-        g_ay = sfx::wave_sum_dpp(g_ay);
-      }
-      if (lane == 0) {
-        const int g = id_batch[t];
-        atomicAdd(v_rgb + 3 * g + 0, g_rgb0);
-        atomicAdd(v_rgb + 3 * g + 1, g_rgb1);
-        atomicAdd(v_rgb + 3 * g + 2, g_rgb2);
-        atomicAdd(v_conic + 3 * g + 0, g_c0);
-        atomicAdd(v_conic + 3 * g + 1, g_c1);
-        atomicAdd(v_conic + 3 * g + 2, g_c2);
-        atomicAdd(v_xy + 2 * g + 0, g_xy0);
-        atomicAdd(v_xy + 2 * g + 1, g_xy1);
-        if (v_xy_abs) {
-          atomicAdd(v_xy_abs + 2 * g + 0, g_ax);
-          atomicAdd(v_xy_abs + 2 * g + 1, g_ay);
+      // row sums (4 DPP butterflies per value) parked in this wave's LDS ring; the 4 row partials of 8 records
+      // are added and sent with one atomic per (record, value) by the wave's lanes in parallel (flush below)
+      float vals[11] = {g_rgb0, g_rgb1, g_rgb2, g_c0, g_c1, g_c2, g_xy0, g_xy1, g_o, g_ax, g_ay};
+      const int nvals = v_xy_abs ? 11 : 9;
+#pragma unroll
+      for (int c = 0; c < 11; ++c) {
+        if (c < nvals) {
+          float x = vals[c];
+          x = sfx::dpp_add(x, 0);
+          x = sfx::dpp_add(x, 1);
+          x = sfx::dpp_add(x, 2);
+          x = sfx::dpp_add(x, 3);
+          if ((lane & 15) == 0) ring[w][nring][c][lane >> 4] = x;
         }
-        atomicAdd(v_opacity + g, g_o);
       }
+      if (lane == 0) ring_g[w][nring] = id_batch[t];
+      if (++nring == RING) flush_ring();
     }
   }
+  flush_ring();
 }
 
 }  // namespace
