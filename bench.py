@@ -250,7 +250,9 @@ def roofline_probe(unit_fn, passes=3):
         "frac_of_fp32_mfma_peak": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
         "kernel": ("GEMM family (gemm_kernel: sfx_linear / sfx_subm_conv / training data-gradient GEMMs, fp32 "
                    "operands as power-of-two-scaled fp16x2 terms, 3 x v_mfma_f32_32x32x16_f16 per block, fp32 "
-                   "accumulation; wgrad_kernel), every launch of one unit of work incl. operand-maxima passes"),
+                   "accumulation; wgrad_kernel; mlp_kernel, the fused LN2 + fc1 + GELU + fc2 Block tail; and "
+                   "cpe_residual_ln4_kernel<.., true>, the SubM conv's per-row sum of its stored pair products), "
+                   "every launch of one unit of work incl. operand-maxima passes"),
         "timing": "HIP events around each launch on its stream, in the real launch sequence; median of "
                   f"{passes} passes",
         "launches": len(per), "gemm_ms_per_unit": round(ms, 3), "algorithmic_gflop_per_unit": round(fl / 1e9, 1),
