@@ -807,6 +807,10 @@ struct CullG {
 };
 
 __device__ __forceinline__ CullG cull_setup(float x, float y, float ca, float cb, float cc, float opac) {
+  // no contraction here or in cull_box_may_hit: the count and emit kernels must take the same decision for every
+  // (Gaussian, tile) (the emit walk fills exactly the slots the count reserved), whatever FMAs the compiler
+  // would pick in each inlined copy
+#pragma clang fp contract(off)
   CullG g;
   g.gx = x; g.gy = y; g.a = ca; g.b = cb; g.c = cc;
   g.ia = 0.f; g.ic = 0.f; g.lim = 0.f;
@@ -831,6 +835,7 @@ __device__ __forceinline__ CullG cull_setup(float x, float y, float ca, float cb
 // May the Gaussian reach alpha >= 1/255 at a pixel centre of [px0, px1] x [py0, py1] (integer pixel bounds,
 // inclusive, already clipped to the image)?
 __device__ __forceinline__ bool cull_box_may_hit(const CullG& g, int px0, int px1, int py0, int py1) {
+#pragma clang fp contract(off)
   if (g.always) return true;
   if (g.never || px0 > px1 || py0 > py1) return false;
   // d = g - (p + 0.5) over the pixel centres

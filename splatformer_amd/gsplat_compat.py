@@ -175,7 +175,14 @@ class _RasterizeGaussians(torch.autograd.Function):
         H, W, bw = int(img_height), int(img_width), int(block_width)
         tiles_x, tiles_y = (W + bw - 1) // bw, (H + bw - 1) // bw
         xys, conics, colors, opacity, background = map(_f32, (xys, conics, colors, opacity, background))
-        num_isect, cum = compute_cumulative_intersects(num_tiles_hit) if n else (0, None)
+        culled = CULL and bw == 16 and n > 0
+        if culled:
+            # gsplat's own list only decides the empty-image branch: one device flag, read back together with the
+            # culled list's total (one host sync per view, as gsplat's num_intersects read)
+            num_isect, kept_total, kept_cum = _culled_counts(n, num_tiles_hit, xys, radii.to(torch.int32).contiguous(),
+                                                             conics, opacity, H, W, tiles_x, tiles_y)
+        else:
+            num_isect, cum = compute_cumulative_intersects(num_tiles_hit) if n else (0, None)
         ctx.num_isect = num_isect
         if num_isect < 1:
             out = torch.ones(H, W, colors.shape[-1], device=dev) * background
@@ -184,10 +191,10 @@ class _RasterizeGaussians(torch.autograd.Function):
             final_Ts = torch.zeros(H, W, device=dev)  # gsplat v0.1.11 empty-branch quirk (alpha == 1)
             final_idx = torch.zeros(H, W, device=dev, dtype=torch.int32)
             alpha = 1 - final_Ts
-        elif CULL and bw == 16:
+        elif culled:
             out, alpha, final_Ts, final_idx, gids_sorted, tile_bins = _culled_forward(
                 n, xys, _f32(depths), radii.to(torch.int32).contiguous(), conics, colors, opacity, background, H, W,
-                tiles_x, tiles_y)
+                tiles_x, tiles_y, kept_total, kept_cum)
             ctx.quad = True
         else:
             _, _, _, gids_sorted, tile_bins = bin_and_sort_gaussians(
@@ -230,14 +237,27 @@ class _RasterizeGaussians(torch.autograd.Function):
         return (v_xy, None, None, v_conic, None, v_rgb, v_op) + (None,) * 5
 
 
-def _culled_forward(n, xys, depths, radii, conics, colors, opacity, background, H, W, tiles_x, tiles_y):
-    """The forward over the culled list (single view): surviving tile counts -> scan -> culled emission -> the
-    same stable sort and bins -> rasterize_fwd_views_quad.  Called when gsplat's own list is non-empty."""
+def _culled_counts(n, num_tiles_hit, xys, radii, conics, opacity, H, W, tiles_x, tiles_y):
+    """-> (1 if gsplat's 3-sigma list is non-empty else 0, culled list length, its inclusive scan): the surviving
+    tile counts and their scan on device, then ONE host read of [max(num_tiles_hit) > 0, culled total]."""
     dev = xys.device
     kept = torch.empty(n, device=dev, dtype=torch.int32)
     call("sfx_isect_count_cull_views", n, n, ptr(xys), ptr(conics), ptr(opacity), ptr(radii), tiles_x, tiles_y, 16, H,
          W, ptr(kept), stream())
-    total, cum = compute_cumulative_intersects(kept)
+    cum = torch.empty(n, device=dev, dtype=torch.int32)
+    flags = torch.zeros(2, device=dev, dtype=torch.int32)  # [gsplat non-empty, culled total]
+    ws = _lib.workspace(_lib.fn("sfx_scan_workspace_bytes")(n), dev)
+    call("sfx_scan_i32", n, ptr(kept), ptr(cum), 1, ptr(ws), ws.numel(), ptr(flags[1:]), stream())
+    flags[0] = (num_tiles_hit.max() > 0).to(torch.int32)
+    nonempty, total = flags.tolist()
+    return nonempty, total, cum
+
+
+def _culled_forward(n, xys, depths, radii, conics, colors, opacity, background, H, W, tiles_x, tiles_y, total, cum):
+    """The forward over the culled list (single view): culled emission over the surviving tile counts' scan (from
+    _culled_counts) -> the same stable sort and bins -> rasterize_fwd_views_quad.  Called when gsplat's own list is
+    non-empty."""
+    dev = xys.device
     num_tiles = tiles_x * tiles_y
     final_Ts = torch.empty(H, W, device=dev, dtype=torch.float32)
     final_idx = torch.empty(H, W, device=dev, dtype=torch.int32)

@@ -183,8 +183,13 @@ def bn_train_forward(x: Tensor, bn: torch.nn.BatchNorm1d, act: int, residual: Op
     rv = bn.running_var if update_running else None
     call("sfx_bn_finalize", Cc, count, sums.data_ptr(), ptr(bn.weight.detach()), ptr(bn.bias.detach()), float(bn.eps),
          float(bn.momentum), ptr(rm), ptr(rv), ptr(mean), ptr(rstd), ptr(scale), ptr(shift), stream())
-    if update_running and bn.num_batches_tracked is not None:
-        bn.num_batches_tracked.add_(1)
+    if update_running:
+        # the kernel wrote the running stats through raw pointers: bump their versions so caches keyed
+        # on (data_ptr, _version) -- ptv3.bn_affine's eval scale/shift -- see the new statistics
+        torch.autograd.graph.increment_version(bn.running_mean)
+        torch.autograd.graph.increment_version(bn.running_var)
+        if bn.num_batches_tracked is not None:
+            bn.num_batches_tracked.add_(1)
     if out is None:
         out = torch.empty(M, Cc, device=dev, dtype=torch.float32)
     po, ldo = _rows(out)

@@ -213,3 +213,32 @@ def test_trainer_second_step_uses_updated_weights(device):
         assert rel_l2(got, ref) < 1e-6, f"step {step}: qkv GEMM does not use the updated weight"
         wt_ref = qkv.weight.detach().reshape(qkv.weight.shape[0], -1).T.cpu()
         assert torch.equal(pt.wt(qkv.weight).cpu(), wt_ref), f"step {step}: stale cached W^T"
+
+
+def test_eval_after_trainer_step_sees_new_running_stats(device):
+    """eval -> Trainer.step -> eval: the train-mode BatchNorms update running_mean / running_var
+    through raw pointers, and the eval path caches each BN's (scale, shift) keyed on the buffers' versions, so
+    the step must bump them -- the second eval must equal a fresh model loaded with the stepped state dict."""
+    torch.manual_seed(0)
+    from splatformer_amd.feature_predictor import FeaturePredictor
+    from splatformer_amd.ptv3 import bn_affine
+    model = FeaturePredictor(sh_degree=1, zeroinit=False).to(device)
+    s = to_device(make_scene(2500, 1, seed=6), device)
+    cams = to_device(make_cameras(64, 64, n_views=2), device)
+    gt = [torch.rand(64, 64, 3, device=device) for _ in range(2)]
+    bns = [m for m in model.modules() if isinstance(m, torch.nn.BatchNorm1d)]
+    assert bns
+    perms = [[0, 1, 2, 3]] * 5
+    model.eval()
+    with torch.no_grad():
+        model([s], [0], perms=perms)
+    before = [tuple(t.clone() for t in bn_affine(b)) for b in bns]
+    tr = strain.Trainer(model, lr=1e-3, generator=torch.Generator(device=device).manual_seed(0))
+    tr.step([s], [cams], [gt])
+    model.eval()
+    after = [bn_affine(b) for b in bns]
+    for b, (sc0, sh0), (sc1, sh1) in zip(bns, before, after):
+        exp_sc = b.weight.detach() / torch.sqrt(b.running_var + b.eps)
+        exp_sh = b.bias.detach() - b.running_mean * exp_sc
+        assert torch.allclose(sc1, exp_sc, rtol=1e-6, atol=0) and torch.allclose(sh1, exp_sh, rtol=1e-6, atol=1e-7)
+        assert not torch.equal(sh0, sh1)  # the step moved the running statistics
