@@ -149,6 +149,80 @@ __device__ __forceinline__ int wave_max_i(int v) {
   return v;
 }
 
+// ---- decoupled look-back (single-pass scan, one-sweep radix passes) ----------------------------------------
+// A tile publishes one 8-byte status word per scanned quantity: tag (24 bits: which launch of the workspace it
+// belongs to; a zeroed workspace holds tag 0 = "nothing yet") | status (aggregate / inclusive prefix) | 32-bit
+// value.  The word is the whole hand-off (a data-tagged granule: written by ONE agent-scope store, `global_store
+// ... sc1`, polled by agent-scope loads, `global_load ... sc1` -- MI355X_MICROARCH.md, Workgroup dispatch,
+// "Valid forms"), so no fence orders anything else.  Tiles are numbered by a returning atomic ticket at
+// workgroup start, so a tile only ever waits on tiles that are already running: no dispatch-order assumption.
+constexpr unsigned kLbAgg = 1u, kLbPrefix = 2u;
+__device__ __forceinline__ unsigned long long lb_word(unsigned tag, unsigned status, int value) {
+  return ((unsigned long long)tag << 34) | ((unsigned long long)status << 32) | (unsigned)value;
+}
+__device__ __forceinline__ void lb_store(unsigned long long* p, unsigned long long w) {
+  __hip_atomic_store(p, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long lb_load(const unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned lb_tag(unsigned long long w) { return (unsigned)(w >> 34); }
+__device__ __forceinline__ unsigned lb_status(unsigned long long w) { return (unsigned)(w >> 32) & 3u; }
+__device__ __forceinline__ int lb_value(unsigned long long w) { return (int)(unsigned)w; }
+// Exclusive prefix of tile `tile` by one thread walking its predecessors' words (stride `stride` words apart):
+// adds aggregates until an inclusive prefix; spins (s_sleep) on words that do not carry `tag` yet.
+// Every wait is bounded (kLbSpinCap polls, far above any real wait): a broken hand-off ends the kernel with a
+// wrong prefix (the parity tests catch it) instead of hanging the GPU.
+constexpr int kLbSpinCap = 1 << 22;
+__device__ __forceinline__ int lb_lookback_thread(const unsigned long long* flags, long long stride, int tile,
+                                                  unsigned tag) {
+  int excl = 0;
+  int spins = 0;
+  for (int j = tile - 1; j >= 0;) {
+    const unsigned long long w = lb_load(flags + (long long)j * stride);
+    if (lb_tag(w) != tag && ++spins < kLbSpinCap) {
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    excl += lb_value(w);
+    if (lb_status(w) == kLbPrefix) break;
+    --j;
+  }
+  return excl;
+}
+// The same by a whole wave (uniform call): lanes read 64 predecessors at once, nearest first.
+__device__ __forceinline__ int lb_lookback_wave(const unsigned long long* flags, int tile, unsigned tag) {
+  const int lane = __lane_id();
+  int excl = 0;
+  int j = tile - 1;
+  int spins = 0;
+  while (j >= 0) {
+    const int idx = j - lane;
+    unsigned st = kLbPrefix;
+    int val = 0;
+    if (idx >= 0) {
+      const unsigned long long w = lb_load(flags + idx);
+      st = lb_tag(w) == tag ? lb_status(w) : 0u;
+      val = lb_value(w);
+    }
+    const unsigned long long pre = __ballot(st == kLbPrefix);
+    // nearest predecessor with a prefix (idx < 0 counts as one); none in this window: all 64 are aggregates
+    const int stop = pre ? __ffsll((long long)pre) - 1 : 63;
+    const unsigned long long need = (stop == 63) ? ~0ull : ((2ull << stop) - 1ull);
+    if ((__ballot(st == 0u) & need) && ++spins < kLbSpinCap) {  // a needed predecessor has not published yet
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    int v = (lane <= stop) ? val : 0;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    excl += v;
+    if (pre) break;
+    j -= 64;
+  }
+  return excl;
+}
+
 }  // namespace sfx
 
 #define SFX_REQUIRE(cond, ...)              \

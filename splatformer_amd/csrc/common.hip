@@ -18,10 +18,11 @@ void clear_error() { g_err[0] = 0; }
 }  // namespace sfx
 
 // ---------------------------------------------------------------------------
-// Inclusive / exclusive int32 scan, three launches: per-block scan (1024 items
-// per 256-thread block), a single-workgroup scan of the block totals, then an
-// offset add.  Used for cum_tiles_hit (gsplat's torch.cumsum(num_tiles_hit,
-// dtype=int32)) and every histogram/run-length offset in the library.
+// Inclusive / exclusive scans.  int32 (cum_tiles_hit = gsplat's
+// torch.cumsum(num_tiles_hit, dtype=int32), every run-length / pair offset in
+// the library): one single-pass launch with decoupled look-back (below).
+// int64: three launches -- per-block scan (1024 items per 256-thread block), a
+// single-workgroup scan of the block totals, then an offset add.
 // ---------------------------------------------------------------------------
 namespace {
 
@@ -127,24 +128,102 @@ int scan_impl(long long n, const T* in, T* out, int inclusive, void* ws, size_t 
   return sfx::check_launch("scan");
 }
 
+// ---- int32: single pass with decoupled look-back --------------------------------------------------------------
+// One launch after a memset of the (tile-word) workspace: each 2048-element tile takes a ticket, scans itself,
+// publishes its aggregate, gets its exclusive prefix from its predecessors' words (sfx::lb_lookback_wave), publishes
+// its inclusive prefix and writes.  The last tile writes the grand total.
+constexpr int LB_ITEMS = 8;
+constexpr int LB_TILE = SCAN_THREADS * LB_ITEMS;
+constexpr size_t LB_HEADER = 256;  // ticket counter, then the tile words
+
+__global__ void __launch_bounds__(SCAN_THREADS)
+scan_lookback_i32(const int32_t* __restrict__ in, int32_t* __restrict__ out, long long n, int inclusive, int tiles,
+                  unsigned* __restrict__ ticket, unsigned long long* __restrict__ flags, int32_t* __restrict__ total) {
+  __shared__ int32_t smem[SCAN_THREADS / 64];
+  __shared__ int s_tile, s_prefix;
+  if (threadIdx.x == 0) s_tile = (int)atomicAdd(ticket, 1u);
+  __syncthreads();
+  const int tile = s_tile;
+  const long long base = (long long)tile * LB_TILE + (long long)threadIdx.x * LB_ITEMS;
+  int32_t v[LB_ITEMS];
+  int32_t s = 0;
+  if (base + LB_ITEMS <= n && (((uintptr_t)(in + base)) & 15) == 0) {
+    const int4 a = *reinterpret_cast<const int4*>(in + base), b = *reinterpret_cast<const int4*>(in + base + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  } else {
+#pragma unroll
+    for (int i = 0; i < LB_ITEMS; ++i) v[i] = (base + i < n) ? in[base + i] : 0;
+  }
+#pragma unroll
+  for (int i = 0; i < LB_ITEMS; ++i) s += v[i];
+  int32_t agg;
+  const int32_t excl = block_exclusive_scan<int32_t>(s, smem, &agg);
+  if (threadIdx.x < 64) {  // wave 0: publish the aggregate, look back, publish the inclusive prefix
+    int32_t prefix = 0;
+    if (tile == 0) {
+      if (threadIdx.x == 0) sfx::lb_store(flags, sfx::lb_word(1u, sfx::kLbPrefix, agg));
+    } else {
+      if (threadIdx.x == 0) sfx::lb_store(flags + tile, sfx::lb_word(1u, sfx::kLbAgg, agg));
+      prefix = sfx::lb_lookback_wave(flags, tile, 1u);
+      if (threadIdx.x == 0) sfx::lb_store(flags + tile, sfx::lb_word(1u, sfx::kLbPrefix, prefix + agg));
+    }
+    if (threadIdx.x == 0) {
+      s_prefix = prefix;
+      if (tile == tiles - 1 && total) *total = prefix + agg;
+    }
+  }
+  __syncthreads();
+  int32_t run = s_prefix + excl;
+#pragma unroll
+  for (int i = 0; i < LB_ITEMS; ++i) {
+    const int32_t nv = run + v[i];
+    if (base + i < n) out[base + i] = inclusive ? nv : run;
+    run = nv;
+  }
+}
+
+int scan_lookback_impl(long long n, const int32_t* in, int32_t* out, int inclusive, void* ws, size_t ws_bytes,
+                       int32_t* total, hipStream_t st) {
+  if (n == 0) {
+    if (total) hipMemsetAsync(total, 0, sizeof(int32_t), st);
+    return sfx::check_launch("scan");
+  }
+  const long long tiles = (n + LB_TILE - 1) / LB_TILE;
+  const size_t need = LB_HEADER + (size_t)tiles * sizeof(unsigned long long);
+  if (ws_bytes < need || (reinterpret_cast<uintptr_t>(ws) & 7)) {
+    sfx::set_error("scan: workspace too small or misaligned (%zu < %zu)", ws_bytes, need);
+    return SFX_ERR_WORKSPACE;
+  }
+  char* p = reinterpret_cast<char*>(ws);
+  if (hipMemsetAsync(p, 0, need, st) != hipSuccess) return sfx::check_launch("scan (workspace reset)");
+  scan_lookback_i32<<<(unsigned)tiles, SCAN_THREADS, 0, st>>>(in, out, n, inclusive, (int)tiles,
+                                                              reinterpret_cast<unsigned*>(p),
+                                                              reinterpret_cast<unsigned long long*>(p + LB_HEADER),
+                                                              total);
+  return sfx::check_launch("scan");
+}
+
 }  // namespace
 
 extern "C" {
 
 const char* sfx_last_error(void) { return sfx::g_err; }
 
-int sfx_abi_version(void) { return 10; }
+int sfx_abi_version(void) { return 11; }
 
 size_t sfx_scan_workspace_bytes(long long n) {
+  // int64: one sum per 1024-element tile; int32: the look-back header + one word per 2048-element tile
   const long long tiles = (n + SCAN_TILE - 1) / SCAN_TILE;
-  return (size_t)(tiles > 0 ? tiles : 1) * sizeof(long long);
+  const size_t old = (size_t)(tiles > 0 ? tiles : 1) * sizeof(long long);
+  const size_t lb = LB_HEADER + (size_t)((n + LB_TILE - 1) / LB_TILE + 1) * sizeof(unsigned long long);
+  return old > lb ? old : lb;
 }
 
 int sfx_scan_i32(long long n, const int32_t* in, int32_t* out, int inclusive, void* ws, size_t ws_bytes,
                  int32_t* total, void* stream) {
   SFX_REQUIRE(n >= 0, "sfx_scan_i32: n < 0");
   SFX_REQUIRE(n == 0 || (in && out), "sfx_scan_i32: null buffer");
-  return scan_impl<int32_t>(n, in, out, inclusive, ws, ws_bytes, total, sfx::as_stream(stream));
+  return scan_lookback_impl(n, in, out, inclusive, ws, ws_bytes, total, sfx::as_stream(stream));
 }
 
 int sfx_scan_i64(long long n, const int64_t* in, int64_t* out, int inclusive, void* ws, size_t ws_bytes,

@@ -92,6 +92,51 @@ def test_scan_and_sort_exact(device):
         assert torch.equal(cum.cpu(), torch.cumsum(cnt, 0, dtype=torch.int32))
 
 
+def test_lookback_scan_and_onesweep_sort_cases(device):
+    """The single-pass scan and one-sweep sort (decoupled look-back, ABI v11) on the cases their hand-off has to
+    survive: thousands of tiles (long look-back chains, tiles finishing out of order), one workspace reused by
+    back-to-back calls of different sizes without a host sync, exclusive and in-place scans, a bit range that
+    does not start at 0, 64-bit keys using all passes, and negative values."""
+    from splatformer_amd import _lib
+    g = torch.Generator().manual_seed(11)
+    ws = _lib.workspace(_lib.fn("sfx_scan_workspace_bytes")(6_000_000), device)
+    outs = []
+    for n, incl in [(6_000_000, 1), (4097, 0), (1, 0), (3_000_001, 0), (2048 * 37, 1)]:
+        x = torch.randint(-5, 9, (n,), generator=g, dtype=torch.int32)
+        xd = x.to(device)
+        out = torch.empty_like(xd)
+        tot = torch.zeros(1, device=device, dtype=torch.int32)
+        _lib.call("sfx_scan_i32", n, xd.data_ptr(), out.data_ptr(), incl, ws.data_ptr(), ws.numel(), tot.data_ptr(),
+                  _lib.stream())
+        outs.append((x, incl, out, tot))
+    for x, incl, out, tot in outs:  # checked after all launches: no sync between the reuses of `ws`
+        ref = torch.cumsum(x, 0, dtype=torch.int32)
+        if not incl:
+            ref = ref - x
+        assert torch.equal(out.cpu(), ref) and int(tot) == int(x.sum())
+    x = torch.randint(0, 100, (777_777,), generator=g, dtype=torch.int32)
+    xd = x.to(device)
+    _lib.call("sfx_scan_i32", x.numel(), xd.data_ptr(), xd.data_ptr(), 1, ws.data_ptr(), ws.numel(), None,
+              _lib.stream())  # in place
+    assert torch.equal(xd.cpu(), torch.cumsum(x, 0, dtype=torch.int32))
+    for n, lo, hi in [(5_000_000, 0, 47), (300_000, 5, 61), (70_000, 0, 64)]:
+        keys = torch.randint(-(1 << 62), 1 << 62, (n,), generator=g, dtype=torch.int64)
+        keys[::3] = keys[1]
+        if hi - lo < 64:
+            keys &= (1 << hi) - 1
+        kd = keys.to(device)
+        ko, vo = torch.empty_like(kd), torch.empty(n, device=device, dtype=torch.int32)
+        wss = _lib.workspace(_lib.fn("sfx_sort_workspace_bytes")(n), device)
+        _lib.call("sfx_sort_pairs_u64", n, kd.data_ptr(), None, ko.data_ptr(), vo.data_ptr(), lo, hi,
+                  wss.data_ptr(), wss.numel(), _lib.stream())
+        ku = keys.cpu().numpy().view("uint64")
+        sk = (ku >> lo) if hi == 64 else ((ku >> lo) & ((1 << (hi - lo)) - 1) if hi - lo < 64 else ku)
+        import numpy as np
+        order = np.argsort(sk, kind="stable")
+        assert np.array_equal(vo.cpu().numpy(), order.astype(np.int32)), (n, lo, hi)
+        assert np.array_equal(ko.cpu().numpy().view("uint64"), ku[order]), (n, lo, hi)
+
+
 def test_bin_and_sort_exact(device):
     a, cams, W, H = _proj_inputs(4000, 2)
     ref = gsplat_ref.project_gaussians(a["means"], a["scales"], 1.0, a["quats"], a["viewmat"], cams["fx"],
