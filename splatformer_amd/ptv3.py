@@ -129,20 +129,39 @@ class Block(nn.Module):
         self.__dict__["_sfx_cpe"] = (key, wf.contiguous(), bf.contiguous())
         return wf, bf
 
+    def cpe_packed(self):
+        """cpe_fused() as the fused conv's fp16x2 fragment stream + inverse column scales (ops.subm_cpe_pack),
+        cached until one of the four CPE tensors changes."""
+        wf, bf = self.cpe_fused()
+        key = self.__dict__["_sfx_cpe"][0]
+        cache = self.__dict__.get("_sfx_cpe_pk")
+        if cache is None or cache[0] != key:
+            with torch.no_grad():
+                wpk, winv = ops.subm_cpe_pack(wf)
+            cache = (key, wpk, winv)
+            self.__dict__["_sfx_cpe_pk"] = cache
+        return cache[1], cache[2], bf
+
     def run(self, point: Point, conv_in: Optional[Tensor] = None, out: Optional[Tensor] = None) -> Point:
         """Block.forward (calflops.py:45-82): x += LN(Lin(SubMConv(x))); x += attn(LN1 x); x += MLP(LN2 x)."""
         x = point.feat
         C = self.channels
         ln_c = self.cpe[2]
-        wf, bf = self.cpe_fused()
+        ln1 = self.norm1[0]
+        xc = x if conv_in is None else conv_in
+        if ops.subm_fused_ok(C):
+            # conv + LN_cpe + shortcut + norm1 in one launch, pair products summed on chip (csrc/subm_fused.hip)
+            wpk, winv, bf = self.cpe_packed()
+            x1, h = ops.subm_cpe_ln(xc, x, point.nbr, wpk, winv, bf, ln_c.weight, ln_c.bias, ln1.weight, ln1.bias,
+                                    ln1.eps)
+        else:
+            wf, bf = self.cpe_fused()
+            # the conv's pair products go to per-pair rows that the LN kernel sums in a fixed order (no float
+            # atomics, reproducible); SFX_SUBM_ATOMIC=1 restores the atomic accumulation
+            t = ops.subm_conv(xc, point.nbr, wf, bf, partials=ops.subm_partials_ok(xc, point.nbr, C))
+            x1, h = ops.cpe_residual_ln(t, x, ln_c.weight, ln_c.bias, ln1.weight, ln1.bias, ln1.eps)
         # The GEMMs scale their fp16x2 operands per row themselves (no operand bounds needed); the qkv GEMM
         # publishes max |qkv| for the attention's fp16x2 q / k / v terms (ptv3_ops.new_amax)
-        # the conv's pair products go to per-pair rows that the LN kernel sums in a fixed order (no float atomics,
-        # reproducible); SFX_SUBM_ATOMIC=1 restores the atomic accumulation
-        xc = x if conv_in is None else conv_in
-        t = ops.subm_conv(xc, point.nbr, wf, bf, partials=ops.subm_partials_ok(xc, point.nbr, C))
-        ln1 = self.norm1[0]
-        x1, h = ops.cpe_residual_ln(t, x, ln_c.weight, ln_c.bias, ln1.weight, ln1.bias, ln1.eps)
         oi = point.order_type[self.attn.order_index]
         qkv, q_amax = ops.linear(h, self.attn.qkv.weight, self.attn.qkv.bias, y_amax=True)
         if self.attn.enable_flash:
@@ -204,7 +223,7 @@ class SerializedPooling(nn.Module):
         return ops.pool_geometry_begin(point.codes_phys, point.order_phys, self._pd(point))
 
     def geometry_end(self, point: Point, perm: Sequence[int], state, m: Optional[int] = None,
-                     deferred: Optional[list] = None):
+                     deferred: Optional[list] = None, pairs: bool = True):
         """The integer half of SerializedPooling.forward: clusters (code >> 3*pd, unique), their members
         (sidx / idx_ptr CSR), the pooled coords, codes, orders and neighbour map.  -> (new Point, sidx, idx_ptr, m)
         m: the cluster count when already known (PointTransformerV3.forward's pool_counts_begin)."""
@@ -223,17 +242,18 @@ class SerializedPooling(nn.Module):
             new.offset = torch.cumsum(torch.bincount(batch.long().cpu(), minlength=len(point.offset)), 0).tolist()
         else:
             new.offset = [m]
-        new.nbr = ops.subm_neighbors(grid, new.get("batch"))
+        new.nbr = ops.subm_neighbors(grid, new.get("batch"), with_pairs=pairs)
         return new, sidx, idx_ptr, m
 
     def geometry(self, point: Point, perm: Sequence[int]):
         return self.geometry_end(point, perm, self.geometry_begin(point))
 
-    def run(self, point: Point, perm: Sequence[int], m: Optional[int] = None, deferred: Optional[list] = None) -> Point:
+    def run(self, point: Point, perm: Sequence[int], m: Optional[int] = None, deferred: Optional[list] = None,
+            pairs: bool = True) -> Point:
         st = self.geometry_begin(point)
         # the projection does not depend on the clusters: enqueued while the host waits for the pooled count
         pf = ops.linear(point.feat, self.proj.weight, self.proj.bias)
-        new, sidx, idx_ptr, m = self.geometry_end(point, perm, st, m, deferred)
+        new, sidx, idx_ptr, m = self.geometry_end(point, perm, st, m, deferred, pairs=pairs)
         sc, sh = bn_affine(self.norm[0])
         new.feat = ops.segment_max_affine_act(pf, idx_ptr, sidx, m, sc, sh, ops.ACT_GELU)
         return new
@@ -353,7 +373,13 @@ class PointTransformerV3(nn.Module):
         self.last_perms.append(p)
         return p
 
-    def prepare(self, data_dict, perms: Optional[List[Sequence[int]]] = None) -> Point:
+    def stage_needs_pairs(self, s: int) -> bool:
+        """Whether an eval forward reads stage s's SubM pair lists: not when every Block on that map (encoder stage
+        s, decoder stage s) runs the fused conv, which reads the neighbour table only."""
+        chans = [self.enc_channels[s]] + ([self.dec_channels[s]] if s < len(self.dec_channels) else [])
+        return not all(ops.subm_fused_ok(c) for c in chans)
+
+    def prepare(self, data_dict, perms: Optional[List[Sequence[int]]] = None, pairs: bool = True) -> Point:
         """Point + serialization (randperm draw 0) + stage-0 neighbour map; `feat` is not embedded yet."""
         feat = data_dict["feat"]
         _lib.require_gpu(feat)
@@ -385,7 +411,7 @@ class PointTransformerV3(nn.Module):
                       code_bits=code_bits)
         if batch is not None:
             point.batch = batch
-        point.nbr = ops.subm_neighbors(grid, batch)
+        point.nbr = ops.subm_neighbors(grid, batch, with_pairs=pairs)
         return point
 
     @torch.no_grad()
@@ -396,7 +422,7 @@ class PointTransformerV3(nn.Module):
         sc, sh = bn_affine(bnm)
         # the embedding needs no geometry: enqueued first, it runs while prepare() waits for the grid depth
         emb_feat = ops.linear(feat, emb.weight, emb.bias, scale=sc, shift=sh, act=ops.ACT_GELU)
-        point = self.prepare(data_dict, perms)
+        point = self.prepare(data_dict, perms, pairs=self.stage_needs_pairs(0))
         point.feat = emb_feat
         # every pooling's cluster count from the stage-0 codes, read back while stage 0 runs: no pooling waits
         pools = [getattr(self.enc, f"enc{s}").down for s in range(1, self.num_stages)]
@@ -413,7 +439,8 @@ class PointTransformerV3(nn.Module):
             for name, mod in stage.named_children():
                 if name == "down":
                     m = counts_rd.get()[k - 1] if counts_rd is not None else None
-                    point = mod.run(point, self._draw_perm(perms, k), m=m, deferred=deferred)
+                    point = mod.run(point, self._draw_perm(perms, k), m=m, deferred=deferred,
+                                    pairs=self.stage_needs_pairs(s))
                     k += 1
                 else:
                     point = mod.run(point)

@@ -44,6 +44,9 @@ _lib.register("sfx_subm_conv", [I, I, I, P, L, P, P, P, P, P, P, P, L, P, I, P, 
 _lib.register("sfx_subm_conv_partials", [I, I, I, P, L, P, P, P, P, P, P, P, L, P, L, P, P, P])
 _lib.register("sfx_subm_conv_partials_pairs", [I, I, I, P, L, P, P, P, P, P, P, P, L, P, L, P, P, P])
 _lib.register("sfx_subm_pair_pos", [I, L, P, P, P, P])
+_lib.register("sfx_subm_cpe_pack_bytes", [I], Z)
+_lib.register("sfx_subm_cpe_pack", [I, P, P, P, P, P])
+_lib.register("sfx_subm_cpe_ln", [I, I, P, P, P, P, P, P, P, P, P, P, F, P, P, P])
 _lib.register("sfx_gs_pack", [I, P, L, P, L, P, L, P, L, P, L, P, L, I, F, P, L, P, P, P])
 _lib.register("sfx_offsets_to_batch", [I, I, P, P, P])
 _lib.register("sfx_gemm_force_config", [I, I])
@@ -507,26 +510,45 @@ def segment_mean(x: Tensor, idx_ptr: Tensor, sorted_idx: Tensor, m: int) -> Tens
 
 
 class SubmMap:
-    """Per-stage SubMConv3d indice map (indice_key=stage{s}): nbr [n,27] + offset-major pair lists.  The 28 pair
-    offsets reach the host asynchronously; the first conv that needs them waits for that copy only."""
+    """Per-stage SubMConv3d indice map (indice_key=stage{s}): nbr [n,27] + offset-major pair lists.  The pair
+    lists are built on first use (ensure_pairs; subm_neighbors(with_pairs=True) builds them right away): the fused
+    conv (subm_cpe_ln) reads nbr only.  The 28 pair offsets reach the host asynchronously; the first conv that
+    needs them waits for that copy only."""
 
-    def __init__(self, nbr: Tensor, mask: Tensor, pair_in: Tensor, pair_out: Tensor, pair_off,
-                 pair_off_dev: Optional[Tensor] = None):
-        self.nbr, self.mask, self.pair_in, self.pair_out = nbr, mask, pair_in, pair_out
-        self._off_src = pair_off  # list or _lib.HostRead
+    def __init__(self, nbr: Tensor, mask: Tensor):
+        self.nbr, self.mask = nbr, mask
+        self._pairs = None  # (pair_in, pair_out, offsets source: _lib.HostRead, device offsets)
         self._off = None
         self._off_c = None
-        self._off_dev = pair_off_dev
         self._pos = None
+
+    def ensure_pairs(self) -> "SubmMap":
+        if self._pairs is None:
+            n = self.nbr.shape[0]
+            dev = self.nbr.device
+            cap = max(1, 26 * n)
+            pin = torch.empty(cap, device=dev, dtype=torch.int32)
+            pout = torch.empty(cap, device=dev, dtype=torch.int32)
+            poff = torch.empty(28, device=dev, dtype=torch.int32)
+            ws = _lib.workspace(_lib.fn("sfx_subm_pairs_workspace_bytes")(n), dev)
+            call("sfx_subm_pairs", n, ptr(self.nbr), ptr(ws), ws.numel(), ptr(pin), ptr(pout), ptr(poff), stream())
+            self._pairs = (pin, pout, _lib.HostRead(poff), poff)
+        return self
+
+    @property
+    def pair_in(self) -> Tensor:
+        return self.ensure_pairs()._pairs[0]
+
+    @property
+    def pair_out(self) -> Tensor:
+        return self.ensure_pairs()._pairs[1]
 
     @property
     def pair_pos(self) -> Tensor:
         """[n, 27] inverted pair index (sfx_subm_pair_pos), built once per map."""
         if self._pos is None:
             n = self.nbr.shape[0]
-            off_dev = self._off_dev
-            if off_dev is None:
-                off_dev = torch.tensor(self.pair_off, dtype=torch.int32, device=self.nbr.device)
+            off_dev = self.ensure_pairs()._pairs[3]
             pos = torch.empty(n, 27, device=self.nbr.device, dtype=torch.int32)
             call("sfx_subm_pair_pos", n, self.num_pairs, ptr(self.pair_out), ptr(off_dev), ptr(pos), stream())
             self._pos = pos
@@ -534,12 +556,12 @@ class SubmMap:
 
     def pair_off_ready(self) -> bool:
         """Whether the pair offsets are already on the host (reading them costs no wait)."""
-        return self._off is not None or isinstance(self._off_src, list)
+        return self._off is not None
 
     @property
     def pair_off(self) -> List[int]:
         if self._off is None:
-            self._off = self._off_src if isinstance(self._off_src, list) else self._off_src.get()
+            self._off = self.ensure_pairs()._pairs[2].get()
         return self._off
 
     @property
@@ -569,15 +591,8 @@ def subm_neighbors(grid_coord: Tensor, batch: Optional[Tensor], with_pairs: bool
     mask = torch.empty(n, device=dev, dtype=torch.int32)
     call("sfx_subm_neighbors", n, ptr(grid_coord, torch.int32), ptr(batch), l2, ptr(tk), ptr(tv), ptr(nbr), ptr(mask),
          None, stream())
-    if not with_pairs:
-        return nbr
-    cap = max(1, 26 * n)
-    pin = torch.empty(cap, device=dev, dtype=torch.int32)
-    pout = torch.empty(cap, device=dev, dtype=torch.int32)
-    poff = torch.empty(28, device=dev, dtype=torch.int32)
-    ws = _lib.workspace(_lib.fn("sfx_subm_pairs_workspace_bytes")(n), dev)
-    call("sfx_subm_pairs", n, ptr(nbr), ptr(ws), ws.numel(), ptr(pin), ptr(pout), ptr(poff), stream())
-    return SubmMap(nbr, mask, pin, pout, _lib.HostRead(poff), poff)
+    smap = SubmMap(nbr, mask)
+    return smap.ensure_pairs() if with_pairs else smap
 
 
 # eval-path SubM convs: store per-pair partials and sum them in the consumer (default), or add them atomically
@@ -595,6 +610,42 @@ def subm_partials_ok(x: Tensor, smap: "SubmMap", cout: int) -> bool:
     return (SUBM_PARTIALS and cout in PAIRS_LN_CHANNELS and x.shape[1] == cout and x.is_contiguous()
             and x.data_ptr() % 16 == 0 and (26 * smap.nbr.shape[0] * cout * 4 + 64 < 0x7ffffff0
                                             or smap.num_pairs * cout * 4 + 64 < 0x7ffffff0))
+
+
+# Block.cpe + shortcut + norm1 of the eval forward in one launch with the pair products summed on chip
+# (csrc/subm_fused.hip) for these channel counts; SFX_SUBM_FUSED=0 restores the pair GEMM + pair-sum LayerNorm
+SUBM_FUSED = os.environ.get("SFX_SUBM_FUSED", "1") != "0"
+SUBM_FUSED_CHANNELS = (64, 96, 128)
+
+
+def subm_fused_ok(C: int) -> bool:
+    return SUBM_FUSED and C in SUBM_FUSED_CHANNELS
+
+
+def subm_cpe_pack(wf: Tensor) -> Tuple[Tensor, Tensor]:
+    """Folded CPE conv weight W' [C, 27*C] -> (fp16x2 fragment stream, inverse column scales) for subm_cpe_ln."""
+    C = wf.shape[0]
+    nb = int(_lib.fn("sfx_subm_cpe_pack_bytes")(C))
+    if nb == 0 or wf.shape[1] != 27 * C:
+        raise RuntimeError(f"subm_cpe_pack: no fused conv for C={C}")
+    wpk = torch.empty(nb // 4, device=wf.device, dtype=torch.float32)
+    winv = torch.empty(C, device=wf.device, dtype=torch.float32)
+    ws = torch.empty(C, device=wf.device, dtype=torch.float32)
+    call("sfx_subm_cpe_pack", C, ptr(wf.contiguous()), ptr(wpk), ptr(winv), ptr(ws), stream())
+    return wpk, winv
+
+
+def subm_cpe_ln(xc: Tensor, x: Tensor, smap: "SubmMap", wpk: Tensor, winv: Tensor, bias: Tensor, g_cpe: Tensor,
+                b_cpe: Tensor, g1: Tensor, b1: Tensor, eps: float) -> Tuple[Tensor, Tensor]:
+    """x1 = x + LN_cpe(SubMConv'(xc)), h = LN1(x1) in one launch (csrc/subm_fused.hip; C in SUBM_FUSED_CHANNELS)."""
+    n, C = x.shape
+    if xc.shape != x.shape or not (xc.is_contiguous() and x.is_contiguous()):
+        raise RuntimeError("subm_cpe_ln: contiguous [n, C] inputs expected")
+    x1 = torch.empty_like(x)
+    h = torch.empty_like(x)
+    call("sfx_subm_cpe_ln", n, C, ptr(xc), ptr(x), ptr(smap.nbr), ptr(wpk), ptr(winv), ptr(bias), ptr(g_cpe),
+         ptr(b_cpe), ptr(g1), ptr(b1), float(eps), ptr(x1), ptr(h), stream())
+    return x1, h
 
 
 _ZERO_OFFS = (ctypes.c_int * 28)()  # pair offsets of a centre-only sfx_subm_conv_partials call

@@ -150,6 +150,46 @@ def test_subm_conv_partials_atomic_free(device):
         assert torch.equal(xo, xo2) and torch.equal(h, h2)
 
 
+@pytest.mark.parametrize("C", [64, 96, 128])
+@pytest.mark.parametrize("n,unique,sep", [(6000, True, False), (4133, False, True), (1, True, False)])
+def test_subm_cpe_ln_fused(device, C, n, unique, sep):
+    """sfx_subm_cpe_ln (conv + LN_cpe + shortcut + norm1 in one launch, pair products summed on chip) against the
+    fp64 oracle (ptv3_ref.subm_conv then the two LayerNorms) -- relative L2 <= 2e-6 on x1 and h -- and against the
+    pair-GEMM path; duplicate voxels, a row count not a multiple of the 128-row block, a separate conv input (the
+    first decoder Block's stale skip feature), a single point; rows of very different magnitude (per-row fp16x2
+    scales); two runs bitwise equal."""
+    s = make_scene(n, 1, seed=n + C, unique_voxels=unique)
+    grid = torch.floor(s["means"] * 256).int()
+    n = grid.shape[0]
+    nbr_ref = ptv3_ref.subm_neighbors(grid, torch.zeros(n, dtype=torch.int64))
+    smap = ops.subm_neighbors(grid.to(device), None, with_pairs=False)
+    g = torch.Generator().manual_seed(C)
+    x = torch.randn(n, C, generator=g) * torch.exp2(torch.randint(-8, 9, (n, 1), generator=g).float())
+    xc = torch.randn(n, C, generator=g) if sep else x
+    wf = torch.randn(C, 27 * C, generator=g) * 0.05
+    bf = torch.randn(C, generator=g)
+    ga, be = torch.rand(C, generator=g) + 0.5, torch.randn(C, generator=g)
+    g1, b1 = torch.rand(C, generator=g) + 0.5, torch.randn(C, generator=g)
+    dev = lambda t: t.to(device).contiguous()
+    wpk, winv = ops.subm_cpe_pack(dev(wf))
+    args = (dev(bf), dev(ga), dev(be), dev(g1), dev(b1), 1e-5)
+    x1, h = ops.subm_cpe_ln(dev(xc), dev(x), smap, wpk, winv, *args)
+    x1b, hb = ops.subm_cpe_ln(dev(xc), dev(x), smap, wpk, winv, *args)
+    assert torch.equal(x1, x1b) and torch.equal(h, hb)
+    # fp64 reference: W' as [C, 27, C] = spconv [Cout, 3, 3, 3, Cin]
+    w5 = wf.double().view(C, 3, 3, 3, C)
+    t = ptv3_ref.subm_conv(xc.double(), nbr_ref, w5, bf.double())
+    ln = lambda v, gg, bb: torch.nn.functional.layer_norm(v, (C,), gg.double(), bb.double(), 1e-5)
+    x1r = x.double() + ln(t, ga, be)
+    hr = ln(x1r, g1, b1)
+    e1, e2 = rel_l2(x1.cpu().double(), x1r), rel_l2(h.cpu().double(), hr)
+    assert e1 < 2e-6 and e2 < 2e-6, (e1, e2)
+    # the pair-GEMM path on the same inputs
+    sp = ops.subm_conv(dev(xc), smap, dev(wf.view(C, 3, 3, 3, C)), dev(bf), partials=True)
+    xo, ho = ops.cpe_residual_ln(sp, dev(x), *args[1:])
+    assert rel_l2(x1.cpu(), xo.cpu()) < 2e-6 and rel_l2(h.cpu(), ho.cpu()) < 2e-6
+
+
 def test_subm_neighbors_duplicates_lowest_index(device):
     grid = torch.tensor([[5, 5, 5], [5, 5, 5], [6, 5, 5], [5, 5, 5], [0, 0, 0]], dtype=torch.int32)
     nbr = ops.subm_neighbors(grid.to(device), None, with_pairs=False).cpu()
