@@ -40,6 +40,60 @@ __global__ void gs_pack_kernel(int n, const float* __restrict__ means, long long
   }
 }
 
+// y[i, o] = GELU((sum_k x[i, k] W[o, k] + b[o]) * scale[o] + shift[o]) for K <= 64 input features: fp32 FMA
+// chains on the VALU (the MFMA GEMM's tiles are built for K >= 64; at K = 23 its launch ran at 7.6 TF/s).
+// 256 threads = 64 points x 4 threads, each thread N/4 outputs of its point; W^T, bias, scale, shift in LDS.
+template <int N>
+__global__ void __launch_bounds__(256) point_embed_kernel(int n, int K, const float* __restrict__ x, long long ldx,
+                                                          const float* __restrict__ w, const float* __restrict__ b,
+                                                          const float* __restrict__ scale,
+                                                          const float* __restrict__ shift, float* __restrict__ y,
+                                                          long long ldy) {
+  constexpr int NO = N / 4;  // outputs per thread
+  __shared__ __attribute__((aligned(16))) float wt[64 * N];  // [k][o]
+  __shared__ __attribute__((aligned(16))) float cst[3][N];
+  for (int e = threadIdx.x; e < K * N; e += 256) {
+    const int o = e / K, k = e - o * K;
+    wt[k * N + o] = w[(long long)o * K + k];
+  }
+  for (int o = threadIdx.x; o < N; o += 256) {
+    cst[0][o] = b ? b[o] : 0.f;
+    cst[1][o] = scale ? scale[o] : 1.f;
+    cst[2][o] = shift ? shift[o] : 0.f;
+  }
+  __syncthreads();
+  const int i = blockIdx.x * 64 + (threadIdx.x >> 2);
+  const int q = threadIdx.x & 3;
+  if (i >= n) return;
+  float acc[NO];
+#pragma unroll
+  for (int j = 0; j < NO; ++j) acc[j] = cst[0][q * NO + j];
+  const float* xr = x + (long long)i * ldx;
+  for (int k = 0; k < K; ++k) {
+    const float xv = xr[k];
+#pragma unroll
+    for (int j = 0; j < NO; j += 4) {
+      const float4 wv = *reinterpret_cast<const float4*>(&wt[k * N + q * NO + j]);
+      acc[j] = fmaf(xv, wv.x, acc[j]);
+      acc[j + 1] = fmaf(xv, wv.y, acc[j + 1]);
+      acc[j + 2] = fmaf(xv, wv.z, acc[j + 2]);
+      acc[j + 3] = fmaf(xv, wv.w, acc[j + 3]);
+    }
+  }
+  float* yr = y + (long long)i * ldy + q * NO;
+#pragma unroll
+  for (int j = 0; j < NO; j += 4) {
+    float4 o4;
+    float* ov = reinterpret_cast<float*>(&o4);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const float v = acc[j + t] * cst[1][q * NO + j + t] + cst[2][q * NO + j + t];
+      ov[t] = 0.5f * v * (1.f + erff(v * 0.70710678118654752f));
+    }
+    *reinterpret_cast<float4*>(yr + j) = o4;
+  }
+}
+
 __global__ void offsets_to_batch_kernel(int n, int B, const long long* __restrict__ offsets, int* __restrict__ batch) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -69,6 +123,22 @@ int sfx_gs_pack(int n, const float* means, long long ld_means, const float* scal
       n, means, ld_means, scales, ld_scales, opacities, ld_opacities, quats, ld_quats, features_dc, ld_dc,
       features_rest, ld_rest, rest_dim, grid_resolution, feat, ld_feat, grid_coord, grid_max);
   return sfx::check_launch("sfx_gs_pack");
+}
+
+// Embedding (reference pointtransformer_v3.py:273-278: Linear(Cin, C) -> BatchNorm1d (eval, as scale/shift) ->
+// GELU) for Cin <= 64 and C in {32, 64}: y [n, C] (ldy % 4 == 0, 16-byte aligned rows)
+int sfx_point_embed(int n, int K, int N, const float* x, long long ldx, const float* w, const float* b,
+                    const float* scale, const float* shift, float* y, long long ldy, void* stream) {
+  SFX_REQUIRE(n >= 0 && K >= 1 && K <= 64 && (N == 32 || N == 64), "sfx_point_embed: K <= 64, N in {32, 64}");
+  if (n == 0) return SFX_OK;
+  SFX_REQUIRE(x && w && y && ldy % 4 == 0 && (reinterpret_cast<uintptr_t>(y) & 15) == 0,
+              "sfx_point_embed: bad buffers");
+  hipStream_t st = sfx::as_stream(stream);
+  if (N == 64)
+    point_embed_kernel<64><<<sfx::ceil_div(n, 64), 256, 0, st>>>(n, K, x, ldx, w, b, scale, shift, y, ldy);
+  else
+    point_embed_kernel<32><<<sfx::ceil_div(n, 64), 256, 0, st>>>(n, K, x, ldx, w, b, scale, shift, y, ldy);
+  return sfx::check_launch("sfx_point_embed");
 }
 
 int sfx_offsets_to_batch(int n, int B, const long long* offsets, int* batch, void* stream) {

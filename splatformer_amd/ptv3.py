@@ -421,7 +421,10 @@ class PointTransformerV3(nn.Module):
         emb, bnm = self.embedding[0], self.embedding[1]
         sc, sh = bn_affine(bnm)
         # the embedding needs no geometry: enqueued first, it runs while prepare() waits for the grid depth
-        emb_feat = ops.linear(feat, emb.weight, emb.bias, scale=sc, shift=sh, act=ops.ACT_GELU)
+        if ops.point_embed_ok(feat, emb.weight):
+            emb_feat = ops.point_embed(feat, emb.weight, emb.bias, sc, sh)
+        else:
+            emb_feat = ops.linear(feat, emb.weight, emb.bias, scale=sc, shift=sh, act=ops.ACT_GELU)
         point = self.prepare(data_dict, perms, pairs=self.stage_needs_pairs(0))
         point.feat = emb_feat
         # every pooling's cluster count from the stage-0 codes, read back while stage 0 runs: no pooling waits

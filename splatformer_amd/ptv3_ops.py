@@ -49,6 +49,7 @@ _lib.register("sfx_subm_cpe_pack", [I, P, P, P, P, P])
 _lib.register("sfx_subm_cpe_ln", [I, I, P, P, P, P, P, P, P, P, P, P, F, P, P, P])
 _lib.register("sfx_gs_pack", [I, P, L, P, L, P, L, P, L, P, L, P, L, I, F, P, L, P, P, P])
 _lib.register("sfx_offsets_to_batch", [I, I, P, P, P])
+_lib.register("sfx_point_embed", [I, I, I, P, L, P, P, P, P, P, L, P])
 _lib.register("sfx_gemm_force_config", [I, I])
 _lib.register("sfx_mlp_stream_floats", [I], Z)
 _lib.register("sfx_mlp_params_floats", [I], Z)
@@ -201,6 +202,24 @@ def linear(x: Tensor, weight: Tensor, bias: Optional[Tensor] = None, *, act: int
          1 if pre_before_act else 0, *_slot_args(a_amax), *_slot_args(w_amax), *_slot_args(ys),
          *weight_split(weight), stream())
     return (out, ys) if y_amax else out
+
+
+def point_embed_ok(x: Tensor, weight: Tensor) -> bool:
+    N, K = weight.shape
+    return K <= 64 and N in (32, 64) and x.dim() == 2 and x.stride(1) == 1
+
+
+def point_embed(x: Tensor, weight: Tensor, bias: Optional[Tensor], scale: Optional[Tensor],
+                shift: Optional[Tensor]) -> Tensor:
+    """GELU((x W^T + b) * scale + shift) for K <= 64 inputs (the PTv3 embedding, pointtransformer_v3.py:273-278):
+    one fp32-VALU launch (csrc/misc.hip) instead of a K < 64 GEMM tile."""
+    N, K = weight.shape
+    M = x.shape[0]
+    out = torch.empty(M, N, device=x.device, dtype=torch.float32)
+    px, ldx = _rows(x)
+    call("sfx_point_embed", M, K, N, px, ldx, ptr(weight.detach().contiguous()), ptr(bias), ptr(scale), ptr(shift),
+         ptr(out), N, stream())
+    return out
 
 
 def grouped_linear(x: Tensor, weight: Tensor, bias: Tensor, groups: int, *, act: int = ACT_NONE,

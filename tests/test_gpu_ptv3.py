@@ -190,6 +190,22 @@ def test_subm_cpe_ln_fused(device, C, n, unique, sep):
     assert rel_l2(x1.cpu(), xo.cpu()) < 2e-6 and rel_l2(h.cpu(), ho.cpu()) < 2e-6
 
 
+@pytest.mark.parametrize("K,N", [(23, 64), (14, 64), (59, 64), (6, 32)])
+def test_point_embed(device, K, N):
+    """sfx_point_embed (the PTv3 embedding Linear -> eval BatchNorm -> GELU on the VALU, strided input rows as the
+    head buffer holds them) vs torch fp64: rel L2 <= 1e-6."""
+    g = torch.Generator().manual_seed(K)
+    n = 4099
+    buf = torch.randn(n, 120, generator=g)
+    x = buf[:, 96:96 + K]
+    w, b = torch.randn(N, K, generator=g) * 0.3, torch.randn(N, generator=g)
+    sc, sh = torch.rand(N, generator=g) + 0.5, torch.randn(N, generator=g)
+    bd = buf.to(device)
+    y = ops.point_embed(bd[:, 96:96 + K], w.to(device), b.to(device), sc.to(device), sh.to(device))
+    ref = torch.nn.functional.gelu((x.double() @ w.double().T + b.double()) * sc.double() + sh.double())
+    assert rel_l2(y.cpu().double(), ref) < 1e-6
+
+
 def test_subm_neighbors_duplicates_lowest_index(device):
     grid = torch.tensor([[5, 5, 5], [5, 5, 5], [6, 5, 5], [5, 5, 5], [0, 0, 0]], dtype=torch.int32)
     nbr = ops.subm_neighbors(grid.to(device), None, with_pairs=False).cpu()
