@@ -55,7 +55,9 @@ F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense fp16 / bf16 MFMA (no
 # fp32-equivalent ceiling is the dense fp16 peak / 3.
 SPLIT_PEAK_TFLOPS = round(F16_MFMA_PEAK_TFLOPS / 3, 1)
 HBM_PEAK_GBS = 8000.0
-GEMM_FAMILY = ("gemm_kernel", "wgrad_kernel", "mlp_kernel")  # kernel-name prefixes of the dominant family
+# kernel-name prefixes of the dominant family: the GEMMs, the fused Block MLP, the fused SubM conv + CPE
+# LayerNorm (subm_fused.hip) and the fused output heads (heads.hip)
+GEMM_FAMILY = ("gemm_kernel", "wgrad_kernel", "mlp_kernel", "subm_cpe_ln_kernel", "heads_kernel")
 
 
 def in_family(kernel_name: str) -> bool:
@@ -172,6 +174,20 @@ def _gemm_cost(kind, args, kw, res):
         return 16.0 * M * C * C, (2 * M * C + 8 * C * C + 12 * C) * f4, (M, 4 * C, C)
     if kind == "cpe_residual_ln":  # timed only with SubM pair partials: the conv's own pair summation
         return 0.0, 0, tuple(args[1].shape)
+    if kind == "subm_cpe_ln":  # fused conv (every active (out, in) pair incl. the centre) + its LayerNorm tail
+        xc, smap = args[0], args[2]
+        n, C = xc.shape
+        nbr = smap.nbr
+        # pair count read after the pass (a host read here would stall the launch sequence being timed)
+        fl = lambda: 2.0 * float((nbr >= 0).sum()) * C * C
+        return fl, (27 * n + 3 * n * C + 2 * n * C + 27 * C * C) * f4, (n, C, C)
+    if kind == "heads":  # 6 x (kin -> 128 -> 128 -> 128 -> c_f) MLPs + residual, one launch
+        x, kin, out_dim = args[0], args[1], args[3]
+        M = x.shape[0]
+        ng = len(args[5]) - 1
+        fl = 2.0 * M * (ng * (kin * 128 + 2 * 128 * 128) + 128 * out_dim)
+        return fl, (M * x.shape[1] + M * out_dim + ng * (kin * 128 + 2 * 128 * 128) + out_dim * 128) * f4, \
+            (M, ng * 128, kin)
     raise KeyError(kind)
 
 
@@ -192,7 +208,7 @@ class GemmTimer:
         for mod, name in [(ptv3_ops, "linear"), (ptv3_ops, "subm_conv"), (ptv3_ops, "grouped_linear"),
                           (train_ops, "linear_bwd_data"), (train_ops, "linear_wgrad"),
                           (train_ops, "subm_conv_bwd_data"), (ptv3_ops, "cpe_residual_ln"),
-                          (ptv3_ops, "block_mlp")]:
+                          (ptv3_ops, "block_mlp"), (ptv3_ops, "subm_cpe_ln"), (ptv3_ops, "heads")]:
             fn = getattr(mod, name)
             self._saved.append((mod, name, fn))
             setattr(mod, name, self._wrap(name, fn))
@@ -221,7 +237,8 @@ class GemmTimer:
 
     def summary(self):
         torch.cuda.synchronize()
-        per = [(e0.elapsed_time(e1), kind, shape, fl, by) for kind, fl, by, shape, e0, e1 in self.calls]
+        per = [(e0.elapsed_time(e1), kind, shape, fl() if callable(fl) else fl, by)
+               for kind, fl, by, shape, e0, e1 in self.calls]
         return per
 
 
@@ -243,7 +260,7 @@ def roofline_probe(unit_fn, passes=3):
     top = max(per)
     # the family grew (round 3: + the fused MLP and the pair-sum LayerNorm); the pure-GEMM subset
     # (gemm_kernel / wgrad_kernel launches only) is the figure comparable with rounds 1-2
-    pure = [p for p in per if p[1] not in ("block_mlp", "cpe_residual_ln")]
+    pure = [p for p in per if p[1] not in ("block_mlp", "cpe_residual_ln", "subm_cpe_ln", "heads")]
     pms, pfl = sum(p[0] for p in pure), sum(p[3] for p in pure)
     pure_tf = pfl / (pms * 1e-3) / 1e12 if pms > 0 else 0.0
     return {
@@ -255,8 +272,10 @@ def roofline_probe(unit_fn, passes=3):
         "frac_of_fp32_mfma_peak": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
         "kernel": ("GEMM family (gemm_kernel: sfx_linear / sfx_subm_conv / training data-gradient GEMMs, fp32 "
                    "operands as power-of-two-scaled fp16x2 terms, 3 x v_mfma_f32_32x32x16_f16 per block, fp32 "
-                   "accumulation; wgrad_kernel; mlp_kernel, the fused LN2 + fc1 + GELU + fc2 Block tail; and "
-                   "cpe_residual_ln4_kernel<.., true>, the SubM conv's per-row sum of its stored pair products), "
+                   "accumulation; wgrad_kernel; mlp_kernel, the fused LN2 + fc1 + GELU + fc2 Block tail; "
+                   "subm_cpe_ln_kernel, the SubM conv with its pair products summed on chip + the CPE LayerNorm "
+                   "tail (C <= 128); heads_kernel, the six output MLPs; and cpe_residual_ln4_kernel<.., true>, the "
+                   "C >= 256 SubM conv's per-row sum of its stored pair products), "
                    "every launch of one unit of work incl. operand-maxima passes"),
         "timing": "HIP events around each launch on its stream, in the real launch sequence; median of "
                   f"{passes} passes",

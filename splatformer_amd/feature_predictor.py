@@ -155,13 +155,34 @@ class FeaturePredictor(nn.Module):
             c, f, g, mapper = downsample_for_backbone(method, self.additional_info, means, feat, grid)
             y = self.backbone({"coord": c, "grid_coord": g, "offset": [c.shape[0]], "feat": f}, perms=perms).feat
             h0[:, :cb] = mapper(y)
+        n_tanh = self.ch["means"] if self.output_features[0] == "means" else 0
+        if ops.heads_fused_ok(len(self.output_features), self.nlayer, self.width, self.head_in,
+                              sum(self.ch[f] for f in self.output_features)):
+            st, pr, ocols, out_dim = self._fused_heads()
+            # all six heads + tanh + residual in one launch (csrc/heads.hip): no [N, 768] hidden in HBM
+            return ops.heads(h0, self.head_in, cb, out_dim, n_tanh, ocols, st, pr)
         w1, b1, mids, wl, bl, out_dim = self._packed_heads()
         x = h0[:, :w1.shape[1]]  # [y | feat | 0-pad]
         h = ops.linear(x, w1, b1, act=ops.ACT_RELU)
         for wm, bm in mids:
             h = ops.grouped_linear(h, wm, bm, len(self.output_features), act=ops.ACT_RELU)
-        n_tanh = self.ch["means"] if self.output_features[0] == "means" else 0
         return ops.linear(h, wl, bl, act=ops.ACT_TANH, act_ncols=n_tanh, residual=feat)
+
+    def _fused_heads(self):
+        """(slab stream, parameter table, output columns, out_dim) of the fused heads kernel, rebuilt with the
+        packed heads (when a head parameter changes)."""
+        packed = self._packed_heads()
+        cache = self.__dict__.get("_fused_heads_cache")
+        if cache is None or cache[0] is not packed:
+            w1, b1, mids, wl, bl, out_dim = packed
+            ocols = [0]
+            for f in self.output_features:
+                ocols.append(ocols[-1] + self.ch[f])
+            with torch.no_grad():
+                st, pr, keep = ops.heads_pack(w1, b1, mids, wl, bl, len(self.output_features), self.head_in, ocols)
+            cache = (packed, st, pr, ocols, out_dim, keep)
+            self.__dict__["_fused_heads_cache"] = cache
+        return cache[1], cache[2], cache[3], cache[4]
 
     def unpack(self, packed: Tensor) -> Dict[str, Tensor]:
         out = OrderedDict()

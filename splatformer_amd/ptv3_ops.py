@@ -50,6 +50,10 @@ _lib.register("sfx_subm_cpe_ln", [I, I, P, P, P, P, P, P, P, P, P, P, F, P, P, P
 _lib.register("sfx_gs_pack", [I, P, L, P, L, P, L, P, L, P, L, P, L, I, F, P, L, P, P, P])
 _lib.register("sfx_offsets_to_batch", [I, I, P, P, P])
 _lib.register("sfx_point_embed", [I, I, I, P, L, P, P, P, P, P, L, P])
+_lib.register("sfx_heads_stream_floats", [I, I], Z)
+_lib.register("sfx_heads_params_floats", [I], Z)
+_lib.register("sfx_heads_pack", [I, I, I, P, I, P, P, P, P, P, P, P, P, P])
+_lib.register("sfx_heads", [I, I, I, I, P, L, I, I, P, P, P, P, P])
 _lib.register("sfx_gemm_force_config", [I, I])
 _lib.register("sfx_mlp_stream_floats", [I], Z)
 _lib.register("sfx_mlp_params_floats", [I], Z)
@@ -220,6 +224,46 @@ def point_embed(x: Tensor, weight: Tensor, bias: Optional[Tensor], scale: Option
     call("sfx_point_embed", M, K, N, px, ldx, ptr(weight.detach().contiguous()), ptr(bias), ptr(scale), ptr(shift),
          ptr(out), N, stream())
     return out
+
+
+# FeaturePredictor heads in one launch (csrc/heads.hip); SFX_HEADS_FUSED=0: the four GEMM launches
+HEADS_FUSED = os.environ.get("SFX_HEADS_FUSED", "1") != "0"
+
+
+def heads_fused_ok(ng: int, nlayer: int, width: int, kin: int, out_dim: int) -> bool:
+    return HEADS_FUSED and nlayer == 4 and width == 128 and 1 <= ng <= 6 and kin <= 160 and out_dim <= 64
+
+
+def heads_pack(w1: Tensor, b1: Tensor, mids, wl: Tensor, bl: Tensor, ng: int, kin: int, ocols: List[int]):
+    """Packed head weights (FeaturePredictor._packed_heads layout) -> (fp16x2 slab stream, parameter table) of
+    sfx_heads: w1 [ng*128, >=kin], mids = [(wm [ng,128,128], bm [ng,128])] x 2, wl [out_dim, ng*128] block
+    diagonal, bl [out_dim]."""
+    dev = w1.device
+    out_dim = wl.shape[0]
+    wm = torch.stack([m[0] for m in mids], 0).contiguous()
+    bm = torch.stack([m[1] for m in mids], 0).contiguous()
+    w4 = torch.empty(out_dim, 128, device=dev, dtype=torch.float32)
+    for g in range(ng):
+        w4[ocols[g]:ocols[g + 1]] = wl[ocols[g]:ocols[g + 1], g * 128:(g + 1) * 128]
+    st = torch.empty(int(_lib.fn("sfx_heads_stream_floats")(ng, kin)), device=dev, dtype=torch.float32)
+    pr = torch.empty(int(_lib.fn("sfx_heads_params_floats")(out_dim)), device=dev, dtype=torch.float32)
+    ws = torch.empty(3 * ng * 128, device=dev, dtype=torch.int32)
+    w1c = w1.contiguous()
+    call("sfx_heads_pack", ng, kin, out_dim, ptr(w1c), w1c.shape[1], ptr(b1.contiguous()), ptr(wm), ptr(bm), ptr(w4),
+         ptr(bl.contiguous()), ptr(st), ptr(pr), ptr(ws), stream())
+    return st, pr, (w1c, wm, bm, w4)
+
+
+def heads(x: Tensor, kin: int, res_off: int, out_dim: int, n_tanh: int, ocols: List[int], st: Tensor,
+          pr: Tensor) -> Tensor:
+    """y [N, out_dim] = heads(x[:, :kin]) + x[:, res_off:res_off+out_dim] (tanh on the first n_tanh columns)."""
+    M = x.shape[0]
+    px, ldx = _rows(x)
+    y = torch.empty(M, out_dim, device=x.device, dtype=torch.float32)
+    oc = (ctypes.c_int * len(ocols))(*ocols)
+    call("sfx_heads", M, len(ocols) - 1, kin, out_dim, px, ldx, res_off, n_tanh, oc, ptr(st), ptr(pr), ptr(y),
+         stream())
+    return y
 
 
 def grouped_linear(x: Tensor, weight: Tensor, bias: Tensor, groups: int, *, act: int = ACT_NONE,

@@ -206,6 +206,50 @@ def test_point_embed(device, K, N):
     assert rel_l2(y.cpu().double(), ref) < 1e-6
 
 
+@pytest.mark.parametrize("sh", [1, 0, 3])
+def test_fused_heads(device, sh):
+    """sfx_heads (the six output MLPs + tanh + residual in one launch, csrc/heads.hip) vs the fp64 oracle heads
+    (feature_predictor.py:201-235 restated in ptv3_ref.heads_forward) and vs the unfused GEMM chain: the refined
+    residual within rel L2 2e-6; SH0 (5 heads, Cin 14), SH1 (Cin 23) and SH3 (Cin 59: input K padded to 160,
+    a 45-wide output head); rows of very different magnitude; a row count not a multiple of 256."""
+    from splatformer_amd.feature_predictor import FeaturePredictor
+    torch.manual_seed(sh)
+    fp = FeaturePredictor(sh_degree=sh, zeroinit=False)
+    sd = {k: v.detach().double() for k, v in fp.state_dict().items()}
+    fp = fp.to(device)
+    cb, cin = 96, fp.gs_features_dim
+    n = 5001
+    g = torch.Generator().manual_seed(sh + 10)
+    h0 = torch.zeros(n, (cb + cin + 3) // 4 * 4)
+    h0[:, :cb + cin] = torch.randn(n, cb + cin, generator=g) * torch.exp2(torch.randint(-6, 7, (n, 1), generator=g).float())
+    st, pr, ocols, out_dim = fp._fused_heads()
+    n_tanh = 3
+    y = ops.heads(h0.to(device), fp.head_in, cb, out_dim, n_tanh, ocols, st, pr).cpu()
+    feat = h0[:, cb:cb + cin].double()
+    in_gs, c = {}, 0
+    for f in fp.output_features:
+        w = fp.ch[f]
+        in_gs[f] = feat[:, c:c + w].reshape(n, -1, 3) if f == "features_rest" else feat[:, c:c + w]
+        c += w
+    ref = ptv3_ref.heads_forward(sd, h0[:, :cb].double(), feat, in_gs, sh_degree=sh)
+    rp = torch.cat([ref[f].reshape(n, -1) for f in fp.output_features], 1)
+    err = rel_l2(y.double() - feat, rp - feat)
+    assert err < 2e-6, err
+    prev = ops.HEADS_FUSED
+    ops.HEADS_FUSED = False
+    try:
+        w1, b1, mids, wl, bl, _ = fp._packed_heads()
+        x = h0.to(device)[:, :w1.shape[1]]
+        hh = ops.linear(x.contiguous(), w1, b1, act=ops.ACT_RELU)
+        for wm, bm in mids:
+            hh = ops.grouped_linear(hh, wm, bm, len(fp.output_features), act=ops.ACT_RELU)
+        yu = ops.linear(hh, wl, bl, act=ops.ACT_TANH, act_ncols=n_tanh,
+                        residual=h0.to(device)[:, cb:cb + cin].contiguous()).cpu()
+    finally:
+        ops.HEADS_FUSED = prev
+    assert rel_l2(y.double() - feat, yu.double() - feat) < 4e-6
+
+
 def test_subm_neighbors_duplicates_lowest_index(device):
     grid = torch.tensor([[5, 5, 5], [5, 5, 5], [6, 5, 5], [5, 5, 5], [0, 0, 0]], dtype=torch.int32)
     nbr = ops.subm_neighbors(grid.to(device), None, with_pairs=False).cpu()
