@@ -158,8 +158,8 @@ def test_subm_cpe_ln_fused(device, C, n, unique, sep):
     pair-GEMM path; duplicate voxels, a row count not a multiple of the 128-row block, a separate conv input (the
     first decoder Block's stale skip feature), a single point; rows of very different magnitude (per-row fp16x2
     scales); two runs bitwise equal."""
-    s = make_scene(n, 1, seed=n + C, unique_voxels=unique)
-    grid = torch.floor(s["means"] * 256).int()
+    s = make_scene(max(n, 64), 1, seed=n + C, unique_voxels=unique)
+    grid = torch.floor(s["means"][:n] * 256).int()
     n = grid.shape[0]
     nbr_ref = ptv3_ref.subm_neighbors(grid, torch.zeros(n, dtype=torch.int64))
     smap = ops.subm_neighbors(grid.to(device), None, with_pairs=False)
