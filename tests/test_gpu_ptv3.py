@@ -196,7 +196,7 @@ def test_point_embed(device, K, N):
     head buffer holds them) vs torch fp64: rel L2 <= 1e-6."""
     g = torch.Generator().manual_seed(K)
     n = 4099
-    buf = torch.randn(n, 120, generator=g)
+    buf = torch.randn(n, 160, generator=g)
     x = buf[:, 96:96 + K]
     w, b = torch.randn(N, K, generator=g) * 0.3, torch.randn(N, generator=g)
     sc, sh = torch.rand(N, generator=g) + 0.5, torch.randn(N, generator=g)
