@@ -252,7 +252,7 @@ def test_fused_heads(device, sh):
 
 def test_subm_neighbors_duplicates_lowest_index(device):
     grid = torch.tensor([[5, 5, 5], [5, 5, 5], [6, 5, 5], [5, 5, 5], [0, 0, 0]], dtype=torch.int32)
-    nbr = ops.subm_neighbors(grid.to(device), None, with_pairs=False).cpu()
+    nbr = ops.subm_neighbors(grid.to(device), None, with_pairs=False).nbr.cpu()
     ref = ptv3_ref.subm_neighbors(grid, torch.zeros(5, dtype=torch.int64))
     assert torch.equal(nbr.long(), ref)
     assert nbr[3, 13] == 0 and nbr[0, 22] == 2  # centre -> lowest duplicate; +x neighbour
