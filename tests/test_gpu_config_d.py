@@ -175,6 +175,7 @@ def _oracle_accum(caps, dtype):
     """sum_i grad(micro-step i's 2-scene batch loss) / world, with the running statistics after the 4 steps."""
     sd0 = _model().state_dict()
     names = [k for k, _ in _model().named_parameters() if "attn.qkv" in k]
+    batches = [_batch(i) for i in range(ACCUM)]  # (fp32 scenes: make_scene follows the default dtype)
     prev = torch.get_default_dtype()
     torch.set_default_dtype(dtype)
     try:
@@ -183,7 +184,7 @@ def _oracle_accum(caps, dtype):
             sd[k].requires_grad_()
         for i in range(ACCUM):
             assert caps[0]["perms"][i] == caps[1]["perms"][i] == PERMS[i]
-            gs, counts = _batch(i)
+            gs, counts = batches[i]
             masks = _cat_masks([c["masks"][i] for c in caps])
             relu = {f: [torch.cat([torch.from_numpy(c["relu"][i][f][li]) for c in caps])
                         for li in range(len(caps[0]["relu"][i][f]))] for f in caps[0]["relu"][i]}
