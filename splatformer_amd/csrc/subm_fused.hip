@@ -29,14 +29,17 @@ constexpr int CHK = 16;  // compacted rows per chunk (the 16-row block of one 16
 
 template <int C>
 struct Cfg {
+  static constexpr int NW = C <= 128 ? 4 : 8;     // waves per workgroup
+  static constexpr int NTH = 64 * NW;
   static constexpr int NCB = C / 16;              // 16-column blocks
   static constexpr int NS = C / 32;               // 32-deep k-steps
-  static constexpr int CBW = (NCB + 3) / 4;       // column blocks per wave (at most)
-  static constexpr int SLOTS = C <= 64 ? 16 : 32; // float4 slots per gathered row (power of two >= C / 4)
+  static constexpr int CBW = (NCB + NW - 1) / NW; // column blocks per wave (at most)
+  static constexpr int SLOTS = C <= 64 ? 16 : (C <= 128 ? 32 : 64);  // float4 slots per gathered row (pow2 >= C/4)
   static constexpr int ACC_LD = C + 4;            // floats per LDS sum row
   static constexpr int A_LD = 2 * C + 16;         // bytes per A-image row (one term)
+  static constexpr int NBUF = C <= 128 ? 2 : 1;   // chunk images (C = 256: the 133 KB of row sums leave room for one)
   // LayerNorm epilogue: G lanes per row, NV float4 per lane
-  static constexpr int G = C == 96 ? 8 : C / 4;
+  static constexpr int G = C == 96 ? 8 : (C <= 128 ? C / 4 : 64);
   static constexpr int NV = C / (4 * G);
 };
 
@@ -85,15 +88,15 @@ __device__ __forceinline__ float f16x2_scale(float m) {
 }
 
 template <int C>
-__global__ void __launch_bounds__(256, 2)
+__global__ void __launch_bounds__(Cfg<C>::NTH, 2)
 subm_cpe_ln_kernel(int n, const float* __restrict__ xc, const float* __restrict__ xres, const int* __restrict__ nbr,
                    const uint4* __restrict__ wpk, const float* __restrict__ winv, const float* __restrict__ bias,
                    const float* __restrict__ g_cpe, const float* __restrict__ b_cpe, const float* __restrict__ g1,
                    const float* __restrict__ b1, float eps, float* __restrict__ xout, float* __restrict__ hout) {
   using Q = Cfg<C>;
   __shared__ __attribute__((aligned(16))) float acc[SR * Q::ACC_LD];
-  __shared__ __attribute__((aligned(16))) unsigned char aimg[2][2][CHK * Q::A_LD];  // [buffer][term][row]
-  __shared__ float ainv[2][CHK];      // 1 / (row scale) of a chunk's rows (0: padding row)
+  __shared__ __attribute__((aligned(16))) unsigned char aimg[Q::NBUF][2][CHK * Q::A_LD];  // [buffer][term][row]
+  __shared__ float ainv[Q::NBUF][CHK];  // 1 / (row scale) of a chunk's rows (0: padding row)
   __shared__ int lsrc[SR];            // this offset's compacted source rows
   __shared__ unsigned char lrow[SR];  // ... and the block rows they feed
   __shared__ int wcnt[2][2];          // [offset parity][wave] (a slow wave may still read the last offset's)
@@ -102,7 +105,7 @@ subm_cpe_ln_kernel(int n, const float* __restrict__ xc, const float* __restrict_
   const int r0 = blockIdx.x * SR;
   const unsigned long long lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
 
-  for (int e = tid; e < SR * (C / 4); e += 256) {
+  for (int e = tid; e < SR * (C / 4); e += Q::NTH) {
     const int r = e / (C / 4), c4 = e - r * (C / 4);
     *reinterpret_cast<float4*>(&acc[r * Q::ACC_LD + 4 * c4]) = *reinterpret_cast<const float4*>(bias + 4 * c4);
   }
@@ -130,7 +133,7 @@ subm_cpe_ln_kernel(int n, const float* __restrict__ xc, const float* __restrict_
     if (cnt == 0) continue;  // (uniform)
 #pragma unroll
     for (int i = 0; i < Q::CBW; ++i) {
-      const int cb = wid + 4 * i;
+      const int cb = wid + Q::NW * i;
       if (cb < Q::NCB) {
 #pragma unroll
         for (int s = 0; s < Q::NS; ++s)
@@ -145,7 +148,7 @@ subm_cpe_ln_kernel(int n, const float* __restrict__ xc, const float* __restrict_
     for (int ch = 0; ch < nch; ++ch) {
       // gather + split this chunk's rows into aimg[buf]: 16 rows x SLOTS float4 slots, one row per SLOTS lanes
 #pragma unroll
-      for (int e = tid; e < CHK * Q::SLOTS; e += 256) {
+      for (int e = tid; e < CHK * Q::SLOTS; e += Q::NTH) {
         const int row = e / Q::SLOTS, slot = e - row * Q::SLOTS;
         const int p = ch * CHK + row;
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -163,34 +166,46 @@ subm_cpe_ln_kernel(int n, const float* __restrict__ xc, const float* __restrict_
         if (slot == 0) ainv[buf][row] = p < cnt ? 1.f / sc : 0.f;
       }
       __syncthreads();
+      f16x8 af[Q::NS][2];  // this chunk's A fragments (rows lane & 15, k = 32 s + 8 (lane >> 4) ..)
+#pragma unroll
+      for (int s = 0; s < Q::NS; ++s) {
+        const int off = (lane & 15) * Q::A_LD + (32 * s + 8 * (lane >> 4)) * 2;
+        af[s][0] = *reinterpret_cast<const f16x8*>(&aimg[buf][0][off]);
+        af[s][1] = *reinterpret_cast<const f16x8*>(&aimg[buf][1][off]);
+      }
+      float rinv[4];
+      int rrow[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = 4 * (lane >> 4) + q;
+        const int p = ch * CHK + row;
+        rinv[q] = ainv[buf][row];
+        rrow[q] = p < cnt ? (int)lrow[p] : -1;
+      }
+      if constexpr (Q::NBUF == 1) __syncthreads();  // the one chunk image is free for the next gather
 #pragma unroll
       for (int i = 0; i < Q::CBW; ++i) {
-        const int cb = wid + 4 * i;
+        const int cb = wid + Q::NW * i;
         if (cb < Q::NCB) {
           f32x4 d = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
           for (int s = 0; s < Q::NS; ++s) {
-            const int off = (lane & 15) * Q::A_LD + (32 * s + 8 * (lane >> 4)) * 2;
-            const f16x8 ah = *reinterpret_cast<const f16x8*>(&aimg[buf][0][off]);
-            const f16x8 al = *reinterpret_cast<const f16x8*>(&aimg[buf][1][off]);
-            d = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, wf[i][s][0], d, 0, 0, 0);
-            d = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, wf[i][s][1], d, 0, 0, 0);
-            d = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, wf[i][s][0], d, 0, 0, 0);
+            d = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[s][1], wf[i][s][0], d, 0, 0, 0);
+            d = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[s][0], wf[i][s][1], d, 0, 0, 0);
+            d = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[s][0], wf[i][s][0], d, 0, 0, 0);
           }
           const int o = 16 * cb + (lane & 15);
           const float wi = winv[o];
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            const int row = 4 * (lane >> 4) + q;
-            const int p = ch * CHK + row;
-            if (p < cnt) {
-              float* a = &acc[(int)lrow[p] * Q::ACC_LD + o];
-              *a += d[q] * ainv[buf][row] * wi;
+            if (rrow[q] >= 0) {
+              float* a = &acc[rrow[q] * Q::ACC_LD + o];
+              *a += d[q] * rinv[q] * wi;
             }
           }
         }
       }
-      buf ^= 1;
+      buf = (buf + 1) % Q::NBUF;
     }
   }
   __syncthreads();
@@ -199,7 +214,7 @@ subm_cpe_ln_kernel(int n, const float* __restrict__ xc, const float* __restrict_
   constexpr int G = Q::G, NV = Q::NV;
   const int sub = tid % G;
 #pragma unroll 1
-  for (int rb = 0; rb < SR; rb += 256 / G) {
+  for (int rb = 0; rb < SR; rb += Q::NTH / G) {
     const int row = rb + tid / G;
     const int gi = r0 + row;
     const bool ok = gi < n;
@@ -272,7 +287,7 @@ extern "C" {
 
 // bytes of the packed fp16x2 conv weight of sfx_subm_cpe_ln (0: C not served)
 size_t sfx_subm_cpe_pack_bytes(int C) {
-  if (C != 64 && C != 96 && C != 128) return 0;
+  if (C != 64 && C != 96 && C != 128 && C != 256) return 0;
   return (size_t)27 * C * C * 4;
 }
 
@@ -280,7 +295,7 @@ size_t sfx_subm_cpe_pack_bytes(int C) {
 // Linear folded in) -> packed fragments (sfx_subm_cpe_pack_bytes(C)) + inverse column scales winv[C]
 // (ws: C floats of scratch)
 int sfx_subm_cpe_pack(int C, const float* w, void* wpk, float* winv, float* ws, void* stream) {
-  SFX_REQUIRE(sfx_subm_cpe_pack_bytes(C) > 0, "sfx_subm_cpe_pack: C must be 64, 96 or 128");
+  SFX_REQUIRE(sfx_subm_cpe_pack_bytes(C) > 0, "sfx_subm_cpe_pack: C must be 64, 96, 128 or 256");
   SFX_REQUIRE(w && wpk && winv && ws, "sfx_subm_cpe_pack: null buffer");
   hipStream_t st = sfx::as_stream(stream);
   subm_cpe_wscale_kernel<<<C, 64, 0, st>>>(C, w, winv, ws);
@@ -293,7 +308,7 @@ int sfx_subm_cpe_pack(int C, const float* w, void* wpk, float* winv, float* ws, 
 int sfx_subm_cpe_ln(int n, int C, const float* xc, const float* xres, const int* nbr, const void* wpk,
                     const float* winv, const float* bias, const float* gamma_cpe, const float* beta_cpe,
                     const float* gamma1, const float* beta1, float eps, float* x_out, float* h_out, void* stream) {
-  SFX_REQUIRE(n >= 0 && sfx_subm_cpe_pack_bytes(C) > 0, "sfx_subm_cpe_ln: C must be 64, 96 or 128");
+  SFX_REQUIRE(n >= 0 && sfx_subm_cpe_pack_bytes(C) > 0, "sfx_subm_cpe_ln: C must be 64, 96, 128 or 256");
   if (n == 0) return SFX_OK;
   SFX_REQUIRE(xc && xres && nbr && wpk && winv && bias && gamma_cpe && beta_cpe && gamma1 && beta1 && x_out && h_out,
               "sfx_subm_cpe_ln: null buffer");
@@ -303,15 +318,14 @@ int sfx_subm_cpe_ln(int n, int C, const float* xc, const float* xres, const int*
   hipStream_t st = sfx::as_stream(stream);
   const unsigned grid = sfx::ceil_div(n, SR);
   const uint4* wp = reinterpret_cast<const uint4*>(wpk);
-  if (C == 64)
-    subm_cpe_ln_kernel<64><<<grid, 256, 0, st>>>(n, xc, xres, nbr, wp, winv, bias, gamma_cpe, beta_cpe, gamma1, beta1,
-                                                 eps, x_out, h_out);
-  else if (C == 96)
-    subm_cpe_ln_kernel<96><<<grid, 256, 0, st>>>(n, xc, xres, nbr, wp, winv, bias, gamma_cpe, beta_cpe, gamma1, beta1,
-                                                 eps, x_out, h_out);
-  else
-    subm_cpe_ln_kernel<128><<<grid, 256, 0, st>>>(n, xc, xres, nbr, wp, winv, bias, gamma_cpe, beta_cpe, gamma1, beta1,
-                                                  eps, x_out, h_out);
+#define SFX_SUBM_LN(CC)                                                                                         \
+  subm_cpe_ln_kernel<CC><<<grid, Cfg<CC>::NTH, 0, st>>>(n, xc, xres, nbr, wp, winv, bias, gamma_cpe, beta_cpe, gamma1, \
+                                                         beta1, eps, x_out, h_out)
+  if (C == 64) SFX_SUBM_LN(64);
+  else if (C == 96) SFX_SUBM_LN(96);
+  else if (C == 128) SFX_SUBM_LN(128);
+  else SFX_SUBM_LN(256);
+#undef SFX_SUBM_LN
   return sfx::check_launch("sfx_subm_cpe_ln");
 }
 
