@@ -31,12 +31,15 @@ FAMILIES = [  # (family, kernel-name regex) -- first match wins
     ("gemm", r"^gemm_kernel|^wgrad_kernel"),
     ("mlp (fused Block MLP)", r"^mlp_kernel"),
     ("subm pair-sum LayerNorm", r"^cpe_residual_ln4_kernel<\d+, \d+, true>"),
+    ("fused subm conv + CPE LN", r"^subm_cpe_ln_kernel"),
+    ("fused output heads", r"^heads_kernel"),
+    ("point embedding", r"^point_embed"),
     ("attention", r"^window_attn"),
     ("rasterizer", r"^rasterize_fwd"),
     ("render prep/project + records", r"^render_prep_project|^pack_raster_records|^isect_emit|^tile_bins"),
-    ("radix sort + scans", r"^radix_|^scan_tiles|^scan_single|^add_tile_offsets"),
+    ("radix sort + scans", r"^radix_|^scan_"),
     ("serialization", r"^serialize_"),
-    ("subm maps", r"^subm_"),
+    ("subm maps", r"^subm_(?!cpe)"),
     ("pooling", r"^pool_|^segment_"),
     ("layernorm", r"^layernorm|^cpe_residual_ln"),
     ("copies/fills", r"^__amd_rocclr"),
