@@ -443,6 +443,45 @@ int sfx_mlp_pack(int C, const float* w1, const float* b1, const float* w2, const
 int sfx_block_mlp(int M, int C, const float* x, long long ldx, const float* stream, const float* params, float eps,
                   float* y, long long ldy, void* stream_);
 
+/* (ABI v11) Block.cpe + shortcut + norm1 in one launch (reference calflops.py:45-53: x1 = x + LN_cpe(Linear(
+ * SubMConv3d(x))), h = norm1(x1); Pointcept Block.cpe = spconv SubMConv3d k=3 -> Linear -> LayerNorm), the
+ * SubM pair products summed on chip (no per-pair partial rows, no atomics; rows' sums formed in ascending offset
+ * order: bitwise reproducible).  C in {64, 96, 128, 256}; rows contiguous [n][C], 16-byte aligned.
+ * sfx_subm_cpe_pack (once per weight version): w = the CPE conv with the Linear folded in, W' [C][27 C]
+ *   (row o, column k C + i: spconv [Cout, 3, 3, 3, Cin]) -> wpk (sfx_subm_cpe_pack_bytes(C) bytes of fp16x2
+ *   fragments) + winv [C] (inverse column scales); ws: C floats.
+ * sfx_subm_cpe_ln: xc = the conv input, xres = the shortcut (they differ for the first Block after an
+ *   unpooling: Pointcept's stale sparse_conv_feat), nbr [n][27] (sfx_subm_neighbors), bias = the folded b'. */
+size_t sfx_subm_cpe_pack_bytes(int C);
+int sfx_subm_cpe_pack(int C, const float* w, void* wpk, float* winv, float* ws, void* stream);
+int sfx_subm_cpe_ln(int n, int C, const float* xc, const float* xres, const int* nbr, const void* wpk,
+                    const float* winv, const float* bias, const float* gamma_cpe, const float* beta_cpe,
+                    const float* gamma1, const float* beta1, float eps, float* x_out, float* h_out, void* stream);
+
+/* (ABI v11) PTv3 embedding (reference pointtransformer_v3.py:273-278: Linear(Cin, C) -> BatchNorm1d eval ->
+ * GELU) on the VALU for Cin <= 64, C in {32, 64}: y[i] = GELU((x[i] W^T + b) * scale + shift); x rows strided
+ * (ldx), y [n][ldy] 16-byte aligned; b / scale / shift may be NULL. */
+int sfx_point_embed(int n, int K, int N, const float* x, long long ldx, const float* w, const float* b,
+                    const float* scale, const float* shift, float* y, long long ldy, void* stream);
+
+/* (ABI v11) FeaturePredictor output heads in one launch (reference models/feature_predictor.py:74-94, :201-235):
+ * per head g (ng <= 6): Linear(kin, 128) -> ReLU -> Linear(128, 128) -> ReLU -> Linear(128, 128) -> ReLU ->
+ * Linear(128, c_g); tanh on the first n_tanh output columns; + the residual record x[:, res_off:res_off+out_dim].
+ * Hidden activations stay in registers (fp16x2 MFMA, fp32 accumulation; the last layer in fp32 on the VALU).
+ * sfx_heads_pack (once per weight version): w1 [ng*128][ld1] (the six first layers concatenated, kin columns
+ *   used), b1 [ng*128], wm [2][ng][128][128], bm [2][ng][128], w4 [out_dim][128] (each output row over its own
+ *   head's units), b4 [out_dim] -> stream (sfx_heads_stream_floats) + params (sfx_heads_params_floats);
+ *   ws: 3 ng 128 ints.
+ * sfx_heads: x [M][ldx] (kin <= 160, 16-byte aligned rows), ocols[ng + 1] = head output column starts,
+ *   y [M][out_dim] (out_dim <= 64). */
+size_t sfx_heads_stream_floats(int ng, int kin);
+size_t sfx_heads_params_floats(int out_dim);
+int sfx_heads_pack(int ng, int kin, int out_dim, const float* w1, int ld1, const float* b1, const float* wm,
+                   const float* bm, const float* w4, const float* b4, float* stream, float* params, int* ws,
+                   void* stream_);
+int sfx_heads(int M, int ng, int kin, int out_dim, const float* x, long long ldx, int res_off, int n_tanh,
+              const int* ocols, const float* stream, const float* params, float* y, void* stream_);
+
 #ifdef __cplusplus
 }
 #endif
