@@ -19,7 +19,8 @@ Checked:
 * the optimiser step: HIP's clip + Adam == torch.nn.utils.clip_grad_norm_ + torch.optim.Adam applied to the same
   averaged bucket (rel <= 1e-6); against Adam on the fp64 oracle's gradient every updated weight agrees to
   1e-2 lr except where the fp64 gradient itself is within 1e-3 of its rms of zero (a first Adam step is
-  lr * sign(g): an element whose gradient is rounding noise may take either sign);
+  lr * sign(g): an element whose gradient is rounding noise may take either sign), and such disagreements are
+  at most 2x (+100) as many as the fp32 oracle's own;
 * the next micro-step's train forward on the updated weights vs the oracle's on its own updated weights:
   refined residual rel L2 <= 1e-5.
 """
@@ -239,9 +240,10 @@ def _adam_update(w0, g, steps=1):
     return torch.cat([p.detach().reshape(-1) for p in ps])
 
 
-def test_config_d_optimizer_step(ranks, oracle64):
+def test_config_d_optimizer_step(ranks, oracle32, oracle64):
     from test_gpu_ptv3 import rel_l2
     _, names, g64 = oracle64
+    g32 = oracle32[2]
     sd0 = _model().state_dict()
     w0 = [sd0[k] for k in names]
     hip_w = torch.cat([torch.from_numpy(ranks[0]["qkv"][k]).double().reshape(-1) for k in names])
@@ -256,14 +258,15 @@ def test_config_d_optimizer_step(ranks, oracle64):
     w0f = torch.cat([w.double().reshape(-1) for w in w0])
     du_hip, du_64 = hip_w - w0f, ref64 - w0f
     bad = (du_hip - du_64).abs() > 1e-2 * 3e-5
+    bad32 = ((_adam_update(w0, g32) - w0f) - du_64).abs() > 1e-2 * 3e-5  # the fp32 oracle's own disagreements
     rms = float(g64.pow(2).mean().sqrt())
     noisy = g64.abs() <= 1e-3 * rms
     print(f"\n[config D] Adam on own bucket rel {e_own:.2e}; vs fp64-oracle Adam: {int(bad.sum())} of {bad.numel()} "
-          f"updates differ, all at |g| <= 1e-3 rms: {bool((~noisy[bad]).sum() == 0)}; weights rel "
-          f"{rel_l2(hip_w, ref64):.2e}")
+          f"updates differ (fp32 oracle: {int(bad32.sum())}), all at |g| <= 1e-3 rms: "
+          f"{bool((~noisy[bad]).sum() == 0)}; weights rel {rel_l2(hip_w, ref64):.2e}")
     assert e_own <= 1e-6
     assert int((bad & ~noisy).sum()) == 0
-    assert int(bad.sum()) <= 1e-4 * bad.numel()
+    assert int(bad.sum()) <= 2 * int(bad32.sum()) + 100
 
 
 def test_config_d_next_forward(ranks, oracle32):
