@@ -47,8 +47,8 @@ int sfx_scan_i64(long long n, const int64_t* in, int64_t* out, int inclusive, vo
  * Replaces torch.sort(isect_ids) in gsplat bin_and_sort_gaussians
  * (utils/gs_utils.py:96) and torch.argsort(code) / torch.sort(cluster) in
  * Pointcept serialization/pooling (models/pointtransformer_v3.py:380, :290).
- * (ABI v11) one-sweep passes: a reset of the workspace's look-back area, one
- * histogram launch for all digit passes, then one launch per 8-bit pass. */
+ * (ABI v11) per 8-bit pass: tile histograms, one single-pass look-back scan
+ * (its area reset once per sort), stable scatter. */
 size_t sfx_sort_workspace_bytes(long long n);
 int sfx_sort_pairs_u64(long long n, const uint64_t* keys_in, const int32_t* vals_in, uint64_t* keys_out,
                        int32_t* vals_out, int begin_bit, int end_bit, void* ws, size_t ws_bytes, void* stream);
@@ -446,7 +446,7 @@ int sfx_block_mlp(int M, int C, const float* x, long long ldx, const float* stre
 /* (ABI v11) Block.cpe + shortcut + norm1 in one launch (reference calflops.py:45-53: x1 = x + LN_cpe(Linear(
  * SubMConv3d(x))), h = norm1(x1); Pointcept Block.cpe = spconv SubMConv3d k=3 -> Linear -> LayerNorm), the
  * SubM pair products summed on chip (no per-pair partial rows, no atomics; rows' sums formed in ascending offset
- * order: bitwise reproducible).  C in {64, 96, 128, 256}; rows contiguous [n][C], 16-byte aligned.
+ * order: bitwise reproducible).  C in {64, 96, 128}; rows contiguous [n][C], 16-byte aligned.
  * sfx_subm_cpe_pack (once per weight version): w = the CPE conv with the Linear folded in, W' [C][27 C]
  *   (row o, column k C + i: spconv [Cout, 3, 3, 3, Cin]) -> wpk (sfx_subm_cpe_pack_bytes(C) bytes of fp16x2
  *   fragments) + winv [C] (inverse column scales); ws: C floats.

@@ -20,6 +20,10 @@ namespace sfx {
 
 void set_error(const char* fmt, ...);
 void clear_error();
+// single-pass int32 scan (common.hip) on a caller-managed look-back area (see there)
+long long lookback_scan_words(long long n);
+void lookback_scan_i32(long long n, const int32_t* in, int32_t* out, int inclusive, unsigned* ticket,
+                       unsigned long long* flags, unsigned tag, int32_t* total, hipStream_t st);
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 

@@ -138,7 +138,8 @@ constexpr size_t LB_HEADER = 256;  // ticket counter, then the tile words
 
 __global__ void __launch_bounds__(SCAN_THREADS)
 scan_lookback_i32(const int32_t* __restrict__ in, int32_t* __restrict__ out, long long n, int inclusive, int tiles,
-                  unsigned* __restrict__ ticket, unsigned long long* __restrict__ flags, int32_t* __restrict__ total) {
+                  unsigned* __restrict__ ticket, unsigned long long* __restrict__ flags, int32_t* __restrict__ total,
+                  unsigned tag) {
   __shared__ int32_t smem[SCAN_THREADS / 64];
   __shared__ int s_tile, s_prefix;
   if (threadIdx.x == 0) s_tile = (int)atomicAdd(ticket, 1u);
@@ -161,11 +162,11 @@ scan_lookback_i32(const int32_t* __restrict__ in, int32_t* __restrict__ out, lon
   if (threadIdx.x < 64) {  // wave 0: publish the aggregate, look back, publish the inclusive prefix
     int32_t prefix = 0;
     if (tile == 0) {
-      if (threadIdx.x == 0) sfx::lb_store(flags, sfx::lb_word(1u, sfx::kLbPrefix, agg));
+      if (threadIdx.x == 0) sfx::lb_store(flags, sfx::lb_word(tag, sfx::kLbPrefix, agg));
     } else {
-      if (threadIdx.x == 0) sfx::lb_store(flags + tile, sfx::lb_word(1u, sfx::kLbAgg, agg));
-      prefix = sfx::lb_lookback_wave(flags, tile, 1u);
-      if (threadIdx.x == 0) sfx::lb_store(flags + tile, sfx::lb_word(1u, sfx::kLbPrefix, prefix + agg));
+      if (threadIdx.x == 0) sfx::lb_store(flags + tile, sfx::lb_word(tag, sfx::kLbAgg, agg));
+      prefix = sfx::lb_lookback_wave(flags, tile, tag);
+      if (threadIdx.x == 0) sfx::lb_store(flags + tile, sfx::lb_word(tag, sfx::kLbPrefix, prefix + agg));
     }
     if (threadIdx.x == 0) {
       s_prefix = prefix;
@@ -199,11 +200,24 @@ int scan_lookback_impl(long long n, const int32_t* in, int32_t* out, int inclusi
   scan_lookback_i32<<<(unsigned)tiles, SCAN_THREADS, 0, st>>>(in, out, n, inclusive, (int)tiles,
                                                               reinterpret_cast<unsigned*>(p),
                                                               reinterpret_cast<unsigned long long*>(p + LB_HEADER),
-                                                              total);
+                                                              total, 1u);
   return sfx::check_launch("scan");
 }
 
 }  // namespace
+
+namespace sfx {
+// The look-back scan on a caller-reset area shared by several scans of one stream: `ticket` zero before the
+// first use, `flags` (lookback_scan_words(n) words) zero or holding only smaller tags; `tag` distinct per call.
+long long lookback_scan_words(long long n) { return (n + LB_TILE - 1) / LB_TILE; }
+void lookback_scan_i32(long long n, const int32_t* in, int32_t* out, int inclusive, unsigned* ticket,
+                       unsigned long long* flags, unsigned tag, int32_t* total, hipStream_t st) {
+  if (n == 0) return;
+  const long long tiles = lookback_scan_words(n);
+  scan_lookback_i32<<<(unsigned)tiles, SCAN_THREADS, 0, st>>>(in, out, n, inclusive, (int)tiles, ticket, flags, total,
+                                                              tag);
+}
+}  // namespace sfx
 
 extern "C" {
 

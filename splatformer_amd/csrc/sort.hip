@@ -9,15 +9,12 @@
 // Stability matters: equal keys keep input order, which is what the CUDA
 // radix sorts the reference relies on produce.
 //
-// One sweep per 8-bit digit (Adinets & Merrill's onesweep, re-derived for wave64): a single histogram launch
-// reads the keys once and counts every pass's digits (global [pass][256] counts); then each pass is ONE launch:
-// a 2048-key tile takes a ticket, ranks its keys per wave (8 ballots per digit match, per-wave prefix in LDS),
-// publishes its per-digit counts, gets every digit's exclusive prefix over the preceding tiles by decoupled
-// look-back (one thread per digit, sfx::lb_lookback_thread), publishes its inclusive prefixes and scatters.
-// The workspace's look-back words are tagged with the pass, so one memset per sort resets all of them.
+// Per pass: histogram per tile -> exclusive scan over [digit][tile] (one single-pass look-back launch, its
+// area reset once per sort and tagged per pass) -> stable rank+scatter.  Ranking is wave-local with 8 ballots
+// per digit match (wave64 __ballot masks), then a per-wave prefix in LDS.  (A one-sweep form -- per-digit
+// look-back inside the scatter, no per-tile histograms -- measured slower here: with every tile resident at once
+// the per-digit chains are long; 47.6 vs ~37 us per pass on config B's intersection sort.)
 #include "common.h"
-
-#include <algorithm>
 
 
 namespace {
@@ -28,59 +25,31 @@ constexpr int RS_ITEMS = 8;
 constexpr int RS_TILE = RS_THREADS * RS_ITEMS;
 constexpr int RS_BINS = 256;
 
-constexpr int RS_MAX_PASSES = 8;
-// workspace: [tickets[8] u32 | pad] [hist[8][256] i32] [flags[tiles][256] u64]
-constexpr size_t RS_HDR = 64;
-constexpr size_t RS_HIST = RS_MAX_PASSES * RS_BINS * sizeof(int);
-
-// every pass's digit histogram in one read of the keys (per-workgroup LDS counts, then one atomic per bin)
 __global__ void __launch_bounds__(RS_THREADS)
-radix_hist_all(const uint64_t* __restrict__ keys, long long n, int begin_bit, int passes, int* __restrict__ hist) {
-  __shared__ int h[RS_MAX_PASSES][RS_BINS];
-  for (int k = threadIdx.x; k < RS_MAX_PASSES * RS_BINS; k += RS_THREADS) (&h[0][0])[k] = 0;
+radix_hist(const uint64_t* __restrict__ keys, long long n, int shift, int num_tiles, int* __restrict__ hist) {
+  __shared__ int h[RS_BINS];
+  h[threadIdx.x] = 0;
   __syncthreads();
-  const long long stride = (long long)gridDim.x * RS_THREADS;
-  for (long long i = (long long)blockIdx.x * RS_THREADS + threadIdx.x; i < n; i += stride) {
-    const uint64_t k = keys[i] >> begin_bit;
-    for (int p = 0; p < passes; ++p) atomicAdd(&h[p][(int)((k >> (8 * p)) & 0xff)], 1);
+  const long long base = (long long)blockIdx.x * RS_TILE;
+#pragma unroll
+  for (int r = 0; r < RS_ITEMS; ++r) {
+    const long long i = base + (long long)r * RS_THREADS + threadIdx.x;
+    if (i < n) atomicAdd(&h[(int)((keys[i] >> shift) & 0xff)], 1);
   }
   __syncthreads();
-  for (int k = threadIdx.x; k < passes * RS_BINS; k += RS_THREADS) {
-    const int c = (&h[0][0])[k];
-    if (c) atomicAdd(hist + k, c);
-  }
+  hist[(long long)threadIdx.x * num_tiles + blockIdx.x] = h[threadIdx.x];
 }
 
 __global__ void __launch_bounds__(RS_THREADS)
-radix_onesweep(const uint64_t* __restrict__ keys_in, const int32_t* __restrict__ vals_in, long long n, int shift,
-               int pass, unsigned* __restrict__ tickets, const int* __restrict__ hist,
-               unsigned long long* __restrict__ flags, uint64_t* __restrict__ keys_out, int32_t* __restrict__ vals_out) {
+radix_scatter(const uint64_t* __restrict__ keys_in, const int32_t* __restrict__ vals_in, long long n, int shift,
+              int num_tiles, const int* __restrict__ offs, uint64_t* __restrict__ keys_out,
+              int32_t* __restrict__ vals_out) {
   __shared__ int cnt[RS_WAVES][RS_BINS];
-  __shared__ int base[RS_BINS];
-  __shared__ int wsum[RS_WAVES];
-  __shared__ int s_tile;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  if (threadIdx.x == 0) s_tile = (int)atomicAdd(tickets + pass, 1u);
   for (int k = threadIdx.x; k < RS_WAVES * RS_BINS; k += RS_THREADS) (&cnt[0][0])[k] = 0;
-  {
-    // global exclusive digit offsets of this pass (the histogram launch finished before this one)
-    const int c = hist[pass * RS_BINS + threadIdx.x];
-    int x = c;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int y = __shfl_up(x, o, 64);
-      if (lane >= o) x += y;
-    }
-    if (lane == 63) wsum[wid] = x;
-    __syncthreads();
-    int off = 0;
-    for (int w = 0; w < wid; ++w) off += wsum[w];
-    base[threadIdx.x] = off + x - c;
-  }
   __syncthreads();
-  const int tile = s_tile;
 
-  const long long wbase = (long long)tile * RS_TILE + (long long)wid * 64 * RS_ITEMS;
+  const long long wbase = (long long)blockIdx.x * RS_TILE + (long long)wid * 64 * RS_ITEMS;
   const unsigned long long lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   uint64_t k_reg[RS_ITEMS];
   int32_t v_reg[RS_ITEMS];
@@ -106,22 +75,9 @@ radix_onesweep(const uint64_t* __restrict__ keys_in, const int32_t* __restrict__
   }
   __syncthreads();
   {
-    // digit d: this tile's count -> publish, look back, publish the inclusive prefix; then per-wave offsets
+    // per-digit exclusive prefix across the waves + global tile offset
     const int d = threadIdx.x;
-    int agg = 0;
-#pragma unroll
-    for (int w = 0; w < RS_WAVES; ++w) agg += cnt[w][d];
-    const unsigned tag = (unsigned)pass + 1u;
-    unsigned long long* my = flags + (long long)tile * RS_BINS + d;
-    int excl = 0;
-    if (tile == 0) {
-      sfx::lb_store(my, sfx::lb_word(tag, sfx::kLbPrefix, agg));
-    } else {
-      sfx::lb_store(my, sfx::lb_word(tag, sfx::kLbAgg, agg));
-      excl = sfx::lb_lookback_thread(flags + d, RS_BINS, tile, tag);
-      sfx::lb_store(my, sfx::lb_word(tag, sfx::kLbPrefix, excl + agg));
-    }
-    int run = base[d] + excl;
+    int run = offs[(long long)d * num_tiles + blockIdx.x];
 #pragma unroll
     for (int w = 0; w < RS_WAVES; ++w) {
       const int c = cnt[w][d];
@@ -159,8 +115,9 @@ extern "C" {
 
 size_t sfx_sort_workspace_bytes(long long n) {
   const long long tiles = (n + RS_TILE - 1) / RS_TILE;
-  return align256(sizeof(uint64_t) * (size_t)n) + align256(sizeof(int32_t) * (size_t)n) + RS_HDR + RS_HIST +
-         sizeof(unsigned long long) * (size_t)(tiles > 0 ? tiles : 1) * RS_BINS;
+  const long long hist = (tiles > 0 ? tiles : 1) * RS_BINS;
+  return align256(sizeof(uint64_t) * (size_t)n) + align256(sizeof(int32_t) * (size_t)n) +
+         align256(sizeof(int32_t) * (size_t)hist) + 256 + sizeof(unsigned long long) * (size_t)sfx::lookback_scan_words(hist);
 }
 
 // Sort `n` pairs by bits [begin_bit, end_bit) of the key (stable).  vals_in may
@@ -179,21 +136,23 @@ int sfx_sort_pairs_u64(long long n, const uint64_t* keys_in, const int32_t* vals
     iota_copy<<<sfx::ceil_div(n, 256), 256, 0, st>>>(keys_in, vals_in, n, keys_out, vals_out);
     return sfx::check_launch("sfx_sort_pairs_u64");
   }
-  SFX_REQUIRE(passes <= RS_MAX_PASSES, "sfx_sort_pairs_u64: too many digit passes");
   char* p = reinterpret_cast<char*>(ws);
   uint64_t* k_alt = reinterpret_cast<uint64_t*>(p);
   p += align256(sizeof(uint64_t) * (size_t)n);
   int32_t* v_alt = reinterpret_cast<int32_t*>(p);
   p += align256(sizeof(int32_t) * (size_t)n);
   const int tiles = (int)((n + RS_TILE - 1) / RS_TILE);
+  const long long hist_n = (long long)tiles * RS_BINS;
+  int* hist = reinterpret_cast<int*>(p);
+  p += align256(sizeof(int32_t) * (size_t)hist_n);
+  // look-back area of the per-pass scans: 8 tickets + words tagged with the pass; reset once here
   unsigned* tickets = reinterpret_cast<unsigned*>(p);
-  int* hist = reinterpret_cast<int*>(p + RS_HDR);
-  unsigned long long* flags = reinterpret_cast<unsigned long long*>(p + RS_HDR + RS_HIST);
-  // one reset per sort: tickets, histograms and the look-back words (tagged per pass)
-  if (hipMemsetAsync(p, 0, RS_HDR + RS_HIST + sizeof(unsigned long long) * (size_t)tiles * RS_BINS, st) != hipSuccess)
+  unsigned long long* flags = reinterpret_cast<unsigned long long*>(p + 256);
+  SFX_REQUIRE(passes <= 64, "sfx_sort_pairs_u64: too many passes");
+  if (hipMemsetAsync(p, 0, 256 + sizeof(unsigned long long) * (size_t)sfx::lookback_scan_words(hist_n), st) !=
+      hipSuccess)
     return sfx::check_launch("sfx_sort_pairs_u64 (workspace reset)");
-  const int hist_blocks = (int)std::min<long long>(tiles, 1024);
-  radix_hist_all<<<hist_blocks, RS_THREADS, 0, st>>>(keys_in, n, begin_bit, passes, hist);
+
   const uint64_t* ksrc = keys_in;
   const int32_t* vsrc = vals_in;
   for (int pass = 0; pass < passes; ++pass) {
@@ -201,7 +160,9 @@ int sfx_sort_pairs_u64(long long n, const uint64_t* keys_in, const int32_t* vals
     const bool to_out = ((passes - 1 - pass) % 2) == 0;
     uint64_t* kdst = to_out ? keys_out : k_alt;
     int32_t* vdst = to_out ? vals_out : v_alt;
-    radix_onesweep<<<tiles, RS_THREADS, 0, st>>>(ksrc, vsrc, n, shift, pass, tickets, hist, flags, kdst, vdst);
+    radix_hist<<<tiles, RS_THREADS, 0, st>>>(ksrc, n, shift, tiles, hist);
+    sfx::lookback_scan_i32(hist_n, hist, hist, 0, tickets + pass, flags, (unsigned)pass + 1u, nullptr, st);
+    radix_scatter<<<tiles, RS_THREADS, 0, st>>>(ksrc, vsrc, n, shift, tiles, hist, kdst, vdst);
     ksrc = kdst;
     vsrc = vdst;
   }

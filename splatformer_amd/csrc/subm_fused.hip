@@ -35,9 +35,8 @@ struct Cfg {
   static constexpr int NS = C / 32;               // 32-deep k-steps
   static constexpr int CBW = (NCB + NW - 1) / NW; // column blocks per wave (at most)
   static constexpr int SLOTS = C <= 64 ? 16 : (C <= 128 ? 32 : 64);  // float4 slots per gathered row (pow2 >= C/4)
-  static constexpr int ACC_LD = C + 4;            // floats per LDS sum row
+  static constexpr int ACC_LD = C == 96 ? C : C + 4;  // floats per LDS sum row (C = 96: unpadded, 2 workgroups/CU)
   static constexpr int A_LD = 2 * C + 16;         // bytes per A-image row (one term)
-  static constexpr int NBUF = C <= 128 ? 2 : 1;   // chunk images (C = 256: the 133 KB of row sums leave room for one)
   // LayerNorm epilogue: G lanes per row, NV float4 per lane
   static constexpr int G = C == 96 ? 8 : (C <= 128 ? C / 4 : 64);
   static constexpr int NV = C / (4 * G);
@@ -94,12 +93,16 @@ subm_cpe_ln_kernel(int n, const float* __restrict__ xc, const float* __restrict_
                    const float* __restrict__ g_cpe, const float* __restrict__ b_cpe, const float* __restrict__ g1,
                    const float* __restrict__ b1, float eps, float* __restrict__ xout, float* __restrict__ hout) {
   using Q = Cfg<C>;
+  constexpr int NG = CHK * Q::SLOTS / Q::NTH;  // gathered float4 slots per thread per chunk
+  constexpr bool WDB = C <= 128;               // W'_k fragments double-buffered in registers (next offset prefetched)
   __shared__ __attribute__((aligned(16))) float acc[SR * Q::ACC_LD];
-  __shared__ __attribute__((aligned(16))) unsigned char aimg[Q::NBUF][2][CHK * Q::A_LD];  // [buffer][term][row]
-  __shared__ float ainv[Q::NBUF][CHK];  // 1 / (row scale) of a chunk's rows (0: padding row)
-  __shared__ int lsrc[SR];            // this offset's compacted source rows
-  __shared__ unsigned char lrow[SR];  // ... and the block rows they feed
-  __shared__ int wcnt[2][2];          // [offset parity][wave] (a slow wave may still read the last offset's)
+  __shared__ __attribute__((aligned(16))) unsigned char aimg[2][2][CHK * Q::A_LD];  // [buffer][term][row]
+  __shared__ float ainv[2][CHK];          // 1 / (row scale) of a chunk's rows (0: padding row)
+  __shared__ int lsrc[27][SR];            // per offset: compacted source rows
+  __shared__ unsigned char lrow[27][SR];  // ... and the block rows they feed
+  __shared__ int wcnt[27][2];
+  __shared__ unsigned char item_k[27 * (SR / CHK)], item_c[27 * (SR / CHK)];  // flat chunk list
+  __shared__ int s_nitems;
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int r0 = blockIdx.x * SR;
@@ -109,28 +112,45 @@ subm_cpe_ln_kernel(int n, const float* __restrict__ xc, const float* __restrict_
     const int r = e / (C / 4), c4 = e - r * (C / 4);
     *reinterpret_cast<float4*>(&acc[r * Q::ACC_LD + 4 * c4]) = *reinterpret_cast<const float4*>(bias + 4 * c4);
   }
+  // compaction of all 27 offsets: block rows with a neighbour at offset k, ascending (waves 0 and 1, a row each)
+  int src[27], pos[27];
+  if (tid < SR) {
+    const int gi = r0 + tid;
+#pragma unroll
+    for (int k = 0; k < 27; ++k) {
+      src[k] = gi < n ? nbr[27ll * gi + k] : -1;
+      const unsigned long long m = __ballot(src[k] >= 0);
+      pos[k] = __popcll(m & lt_mask);
+      if (lane == 0) wcnt[k][wid] = __popcll(m);
+    }
+  }
+  __syncthreads();
+  if (tid < SR) {
+#pragma unroll
+    for (int k = 0; k < 27; ++k)
+      if (src[k] >= 0) {
+        const int p = pos[k] + (wid == 1 ? wcnt[k][0] : 0);
+        lsrc[k][p] = src[k];
+        lrow[k][p] = (unsigned char)tid;
+      }
+  }
+  if (tid == 0) {
+    int ni = 0;
+    for (int k = 0; k < 27; ++k) {
+      const int nch = (wcnt[k][0] + wcnt[k][1] + CHK - 1) / CHK;
+      for (int c = 0; c < nch; ++c, ++ni) {
+        item_k[ni] = (unsigned char)k;
+        item_c[ni] = (unsigned char)c;
+      }
+    }
+    s_nitems = ni;
+  }
+  __syncthreads();
+  const int nitems = s_nitems;
 
-  f16x8 wf[Q::CBW][Q::NS][2];  // this wave's W'_k fragments: [column block][k-step][term]
-  int buf = 0;
-#pragma unroll 1
-  for (int k = 0; k < 27; ++k) {
-    // compaction: block rows with a neighbour at offset k, ascending (waves 0 and 1, one thread per row)
-    int src = -1, pos = 0;
-    if (tid < SR) {
-      const int gi = r0 + tid;
-      src = gi < n ? nbr[27ll * gi + k] : -1;
-      const unsigned long long m = __ballot(src >= 0);
-      pos = __popcll(m & lt_mask);
-      if (lane == 0) wcnt[k & 1][wid] = __popcll(m);
-    }
-    __syncthreads();  // (also: every wave is done with the previous offset's lists and chunk images)
-    const int cnt = wcnt[k & 1][0] + wcnt[k & 1][1];
-    if (tid < SR && src >= 0) {
-      const int p = pos + (wid == 1 ? wcnt[k & 1][0] : 0);
-      lsrc[p] = src;
-      lrow[p] = (unsigned char)tid;
-    }
-    if (cnt == 0) continue;  // (uniform)
+  // this wave's W'_k fragments [column block][k-step][term]; wn: the next offset's (prefetched, WDB)
+  f16x8 wf[Q::CBW][Q::NS][2], wn[WDB ? Q::CBW : 1][Q::NS][2];
+  auto load_w = [&](int k, f16x8 (&w)[Q::CBW][Q::NS][2]) {
 #pragma unroll
     for (int i = 0; i < Q::CBW; ++i) {
       const int cb = wid + Q::NW * i;
@@ -139,76 +159,127 @@ subm_cpe_ln_kernel(int n, const float* __restrict__ xc, const float* __restrict_
         for (int s = 0; s < Q::NS; ++s)
 #pragma unroll
           for (int t = 0; t < 2; ++t)
-            wf[i][s][t] = __builtin_bit_cast(f16x8, wpk[((((long long)k * Q::NCB + cb) * Q::NS + s) * 2 + t) * 64 + lane]);
+            w[i][s][t] = __builtin_bit_cast(f16x8, wpk[((((long long)k * Q::NCB + cb) * Q::NS + s) * 2 + t) * 64 + lane]);
       }
     }
-    __syncthreads();  // lists visible
-    const int nch = (cnt + CHK - 1) / CHK;
-#pragma unroll 1
-    for (int ch = 0; ch < nch; ++ch) {
-      // gather + split this chunk's rows into aimg[buf]: 16 rows x SLOTS float4 slots, one row per SLOTS lanes
+  };
+  // next offset with chunks after item index c (27: none)
+  auto next_k = [&](int c) {
+    const int k = item_k[c];
+    for (int j = c + 1; j < nitems; ++j)
+      if (item_k[j] != k) return (int)item_k[j];
+    return 27;
+  };
+  // chunk gather: this thread's NG float4 slots of item c's 16 rows
+  auto gather = [&](int c, float4 (&v)[NG]) {
+    const int k = item_k[c], cnt = wcnt[k][0] + wcnt[k][1];
 #pragma unroll
-      for (int e = tid; e < CHK * Q::SLOTS; e += Q::NTH) {
-        const int row = e / Q::SLOTS, slot = e - row * Q::SLOTS;
-        const int p = ch * CHK + row;
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (p < cnt && slot < C / 4) v = *reinterpret_cast<const float4*>(xc + (long long)lsrc[p] * C + 4 * slot);
-        float m = fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w)));
-#pragma unroll
-        for (int o = Q::SLOTS / 2; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
-        const float sc = f16x2_scale(m);
-        if (slot < C / 4) {
-          uint2 t[2];
-          sfx::split2h(v, sc, t);
-          *reinterpret_cast<uint2*>(&aimg[buf][0][row * Q::A_LD + 8 * slot]) = t[0];
-          *reinterpret_cast<uint2*>(&aimg[buf][1][row * Q::A_LD + 8 * slot]) = t[1];
-        }
-        if (slot == 0) ainv[buf][row] = p < cnt ? 1.f / sc : 0.f;
-      }
-      __syncthreads();
-      f16x8 af[Q::NS][2];  // this chunk's A fragments (rows lane & 15, k = 32 s + 8 (lane >> 4) ..)
-#pragma unroll
-      for (int s = 0; s < Q::NS; ++s) {
-        const int off = (lane & 15) * Q::A_LD + (32 * s + 8 * (lane >> 4)) * 2;
-        af[s][0] = *reinterpret_cast<const f16x8*>(&aimg[buf][0][off]);
-        af[s][1] = *reinterpret_cast<const f16x8*>(&aimg[buf][1][off]);
-      }
-      float rinv[4];
-      int rrow[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int row = 4 * (lane >> 4) + q;
-        const int p = ch * CHK + row;
-        rinv[q] = ainv[buf][row];
-        rrow[q] = p < cnt ? (int)lrow[p] : -1;
-      }
-      if constexpr (Q::NBUF == 1) __syncthreads();  // the one chunk image is free for the next gather
-#pragma unroll
-      for (int i = 0; i < Q::CBW; ++i) {
-        const int cb = wid + Q::NW * i;
-        if (cb < Q::NCB) {
-          f32x4 d = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-          for (int s = 0; s < Q::NS; ++s) {
-            d = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[s][1], wf[i][s][0], d, 0, 0, 0);
-            d = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[s][0], wf[i][s][1], d, 0, 0, 0);
-            d = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[s][0], wf[i][s][0], d, 0, 0, 0);
-          }
-          const int o = 16 * cb + (lane & 15);
-          const float wi = winv[o];
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            if (rrow[q] >= 0) {
-              float* a = &acc[rrow[q] * Q::ACC_LD + o];
-              *a += d[q] * rinv[q] * wi;
-            }
-          }
-        }
-      }
-      buf = (buf + 1) % Q::NBUF;
+    for (int g = 0; g < NG; ++g) {
+      const int e = tid + Q::NTH * g;
+      const int row = e / Q::SLOTS, slot = e - row * Q::SLOTS;
+      const int p = item_c[c] * CHK + row;
+      v[g] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (p < cnt && slot < C / 4) v[g] = *reinterpret_cast<const float4*>(xc + (long long)lsrc[k][p] * C + 4 * slot);
     }
+  };
+  // split the gathered rows into chunk image b (per-row power-of-two scale)
+  auto stage = [&](int c, int b, const float4 (&v)[NG]) {
+    const int k = item_k[c], cnt = wcnt[k][0] + wcnt[k][1];
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      const int e = tid + Q::NTH * g;
+      const int row = e / Q::SLOTS, slot = e - row * Q::SLOTS;
+      const int p = item_c[c] * CHK + row;
+      float m = fmaxf(fmaxf(fabsf(v[g].x), fabsf(v[g].y)), fmaxf(fabsf(v[g].z), fabsf(v[g].w)));
+#pragma unroll
+      for (int o = Q::SLOTS / 2; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+      const float sc = f16x2_scale(m);
+      if (slot < C / 4) {
+        uint2 t[2];
+        sfx::split2h(v[g], sc, t);
+        *reinterpret_cast<uint2*>(&aimg[b][0][row * Q::A_LD + 8 * slot]) = t[0];
+        *reinterpret_cast<uint2*>(&aimg[b][1][row * Q::A_LD + 8 * slot]) = t[1];
+      }
+      if (slot == 0) ainv[b][row] = p < cnt ? 1.f / sc : 0.f;
+    }
+  };
+
+  if (nitems > 0) {
+    float4 v[NG];
+    load_w(item_k[0], wf);
+    gather(0, v);
+    if constexpr (WDB) {
+      const int k1 = next_k(0);
+      if (k1 < 27) load_w(k1, wn);
+    }
+    stage(0, 0, v);
   }
   __syncthreads();
+#pragma unroll 1
+  for (int c = 0; c < nitems; ++c) {
+    const int b = c & 1;
+    const int k = item_k[c], cnt = wcnt[k][0] + wcnt[k][1];
+    float4 v[NG];
+    if (c + 1 < nitems) gather(c + 1, v);  // next chunk's rows: in flight during this chunk's MFMAs
+    f16x8 af[Q::NS][2];  // this chunk's A fragments (rows lane & 15, k = 32 s + 8 (lane >> 4) ..)
+#pragma unroll
+    for (int s = 0; s < Q::NS; ++s) {
+      const int off = (lane & 15) * Q::A_LD + (32 * s + 8 * (lane >> 4)) * 2;
+      af[s][0] = *reinterpret_cast<const f16x8*>(&aimg[b][0][off]);
+      af[s][1] = *reinterpret_cast<const f16x8*>(&aimg[b][1][off]);
+    }
+    float rinv[4];
+    int rrow[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int row = 4 * (lane >> 4) + q;
+      const int p = item_c[c] * CHK + row;
+      rinv[q] = ainv[b][row];
+      rrow[q] = p < cnt ? (int)lrow[k][p] : -1;
+    }
+#pragma unroll
+    for (int i = 0; i < Q::CBW; ++i) {
+      const int cb = wid + Q::NW * i;
+      if (cb < Q::NCB) {
+        f32x4 d = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < Q::NS; ++s) {
+          d = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[s][1], wf[i][s][0], d, 0, 0, 0);
+          d = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[s][0], wf[i][s][1], d, 0, 0, 0);
+          d = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[s][0], wf[i][s][0], d, 0, 0, 0);
+        }
+        const int o = 16 * cb + (lane & 15);
+        const float wi = winv[o];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          if (rrow[q] >= 0) {
+            float* a = &acc[rrow[q] * Q::ACC_LD + o];
+            *a += d[q] * rinv[q] * wi;
+          }
+        }
+      }
+    }
+    if (c + 1 < nitems) {
+      stage(c + 1, b ^ 1, v);
+      const int kn = item_k[c + 1];
+      if (kn != k) {  // the next chunk starts a new offset
+        if constexpr (WDB) {
+#pragma unroll
+          for (int i = 0; i < Q::CBW; ++i)
+#pragma unroll
+            for (int s = 0; s < Q::NS; ++s) {
+              wf[i][s][0] = wn[i][s][0];
+              wf[i][s][1] = wn[i][s][1];
+            }
+          const int k2 = next_k(c + 1);
+          if (k2 < 27) load_w(k2, wn);
+        } else {
+          load_w(kn, wf);
+        }
+      }
+    }
+    __syncthreads();
+  }
 
   // epilogue: LN_cpe -> + shortcut -> LN1, G lanes per row
   constexpr int G = Q::G, NV = Q::NV;
@@ -287,7 +358,7 @@ extern "C" {
 
 // bytes of the packed fp16x2 conv weight of sfx_subm_cpe_ln (0: C not served)
 size_t sfx_subm_cpe_pack_bytes(int C) {
-  if (C != 64 && C != 96 && C != 128 && C != 256) return 0;
+  if (C != 64 && C != 96 && C != 128) return 0;
   return (size_t)27 * C * C * 4;
 }
 
@@ -295,7 +366,7 @@ size_t sfx_subm_cpe_pack_bytes(int C) {
 // Linear folded in) -> packed fragments (sfx_subm_cpe_pack_bytes(C)) + inverse column scales winv[C]
 // (ws: C floats of scratch)
 int sfx_subm_cpe_pack(int C, const float* w, void* wpk, float* winv, float* ws, void* stream) {
-  SFX_REQUIRE(sfx_subm_cpe_pack_bytes(C) > 0, "sfx_subm_cpe_pack: C must be 64, 96, 128 or 256");
+  SFX_REQUIRE(sfx_subm_cpe_pack_bytes(C) > 0, "sfx_subm_cpe_pack: C must be 64, 96 or 128");
   SFX_REQUIRE(w && wpk && winv && ws, "sfx_subm_cpe_pack: null buffer");
   hipStream_t st = sfx::as_stream(stream);
   subm_cpe_wscale_kernel<<<C, 64, 0, st>>>(C, w, winv, ws);
@@ -308,7 +379,7 @@ int sfx_subm_cpe_pack(int C, const float* w, void* wpk, float* winv, float* ws, 
 int sfx_subm_cpe_ln(int n, int C, const float* xc, const float* xres, const int* nbr, const void* wpk,
                     const float* winv, const float* bias, const float* gamma_cpe, const float* beta_cpe,
                     const float* gamma1, const float* beta1, float eps, float* x_out, float* h_out, void* stream) {
-  SFX_REQUIRE(n >= 0 && sfx_subm_cpe_pack_bytes(C) > 0, "sfx_subm_cpe_ln: C must be 64, 96, 128 or 256");
+  SFX_REQUIRE(n >= 0 && sfx_subm_cpe_pack_bytes(C) > 0, "sfx_subm_cpe_ln: C must be 64, 96 or 128");
   if (n == 0) return SFX_OK;
   SFX_REQUIRE(xc && xres && nbr && wpk && winv && bias && gamma_cpe && beta_cpe && gamma1 && beta1 && x_out && h_out,
               "sfx_subm_cpe_ln: null buffer");
@@ -323,8 +394,7 @@ int sfx_subm_cpe_ln(int n, int C, const float* xc, const float* xres, const int*
                                                          beta1, eps, x_out, h_out)
   if (C == 64) SFX_SUBM_LN(64);
   else if (C == 96) SFX_SUBM_LN(96);
-  else if (C == 128) SFX_SUBM_LN(128);
-  else SFX_SUBM_LN(256);
+  else SFX_SUBM_LN(128);
 #undef SFX_SUBM_LN
   return sfx::check_launch("sfx_subm_cpe_ln");
 }

@@ -150,7 +150,7 @@ def test_subm_conv_partials_atomic_free(device):
         assert torch.equal(xo, xo2) and torch.equal(h, h2)
 
 
-@pytest.mark.parametrize("C", [64, 96, 128, 256])
+@pytest.mark.parametrize("C", [64, 96, 128])
 @pytest.mark.parametrize("n,unique,sep", [(6000, True, False), (4133, False, True), (1, True, False)])
 def test_subm_cpe_ln_fused(device, C, n, unique, sep):
     """sfx_subm_cpe_ln (conv + LN_cpe + shortcut + norm1 in one launch, pair products summed on chip) against the
