@@ -709,6 +709,261 @@ window_attn_split_kernel(const float* __restrict__ qkv, const int* __restrict__ 
 }
 
 
+// window_attn_split_kernel<D, true> as a software pipeline over consecutive (window, head) items (window-major:
+// all heads of a window back to back): a workgroup owns `ipw` consecutive items and, while it computes item i from
+// LDS buffer i & 1, has item i + 1's row indices and q / k / v slices in flight into registers, split into the
+// other buffer after item i's MFMAs -- the row gathers (the old kernel's whole latency: one item per workgroup,
+// gather -> barrier -> compute -> store) overlap the compute.  Same arithmetic, same term order: outputs are bit
+// for bit those of window_attn_split_kernel (test_window_attention_seq_bitwise).
+template <int D>
+__global__ void __launch_bounds__(256, 2)
+window_attn_seq_kernel(const float* __restrict__ qkv, const int* __restrict__ order, const int* __restrict__ win,
+                       int Kwin, int C, float scale, float* __restrict__ out,
+                       const unsigned long long* __restrict__ qkv_amax, unsigned qkv_tag, int items, int ipw) {
+  typedef _Float16 bf16x8 __attribute__((ext_vector_type(8)));
+  constexpr int NT = 2;
+  constexpr int KD = D == 16 ? 16 : 32;
+  constexpr int NKS = KD / 16;
+  constexpr int QROW = KD == 16 ? 48 : 64;
+  constexpr int VST = 136;
+  constexpr int QK_BYTES = NT * KMAX * QROW;
+  constexpr int V_BYTES = NT * D * VST * 2;
+  constexpr int BUF = QK_BYTES + V_BYTES;
+  constexpr int CH = D / 4;
+  constexpr int NK = (KMAX * CH + 255) / 256;         // K float4 per thread
+  constexpr int NV = ((KMAX / 2) * CH + 255) / 256;   // V key pairs per thread
+  float sq = 1.f, iq = 1.f;
+  {
+    const float m = sfx::read_amax(qkv_amax, qkv_tag);
+    int e = 0;
+    if (m > 0.f && m <= 3.4028235e38f) {
+      (void)frexpf(m, &e);
+      e = 15 - e;
+      e = e > 126 ? 126 : (e < -126 ? -126 : e);
+    }
+    sq = ldexpf(1.f, e);
+    iq = ldexpf(1.f, -e);
+  }
+  __shared__ __attribute__((aligned(16))) char lds[2 * BUF];
+  auto qk_off = [](int r, int c) -> int {
+    return KD == 16 ? r * 48 + c * 16 : r * 64 + (((c ^ (r >> 2)) & 3) << 4);
+  };
+  const int heads = C / D;
+  const int nb = (int)gridDim.x;
+  const int L = (int)(blockIdx.x % 8) * (nb / 8) + (int)(blockIdx.x / 8);
+  const int i0 = L * ipw, i1 = min(items, i0 + ipw);
+  if (i0 >= i1) return;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, h = lane >> 5, l32 = lane & 31;
+  const long long ld = 3ll * C;
+  if (D < KD)  // K columns D..KD-1 of both buffers: zero once
+    for (int rr = tid; rr < 2 * NT * KMAX; rr += 256) {
+      const int b = rr / (NT * KMAX), r2 = rr - b * NT * KMAX;
+      *reinterpret_cast<uint4*>(lds + b * BUF + qk_off(r2, D / 8)) = make_uint4(0, 0, 0, 0);
+    }
+
+  // ---- one item's gathered slices (registers) ----
+  float4 kv[NK], vv0[NV], vv1[NV], qv[NKS][2];
+  int qrow = -1;  // this lane's query point (output row) of the staged item
+  auto fetch = [&](int it) {
+    const int w = it / heads, head = it - w * heads;
+    const int key_start = win[2 * w];
+#pragma unroll
+    for (int j = 0; j < NK; ++j) {
+      const int e = tid + 256 * j;
+      const int row = e / CH, ch = e - row * CH;
+      kv[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (row < Kwin && e < KMAX * CH) {
+        const int src = order[key_start + row];
+        kv[j] = *reinterpret_cast<const float4*>(qkv + (long long)src * ld + C + head * D + 4 * ch);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const int e = tid + 256 * j;
+      const int kp = e / CH, ch = e - kp * CH;
+      vv0[j] = vv1[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (e < (KMAX / 2) * CH) {
+        const int r0 = 2 * kp;
+        if (r0 < Kwin)
+          vv0[j] = *reinterpret_cast<const float4*>(qkv + (long long)order[key_start + r0] * ld + 2 * C + head * D + 4 * ch);
+        if (r0 + 1 < Kwin)
+          vv1[j] = *reinterpret_cast<const float4*>(qkv + (long long)order[key_start + r0 + 1] * ld + 2 * C + head * D +
+                                                    4 * ch);
+      }
+    }
+    const int qi = 32 * wid + l32;
+    qrow = qi < Kwin ? order[key_start + qi] : -1;
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      const int d0 = 16 * ks + 8 * h;
+      qv[ks][0] = qv[ks][1] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (qrow >= 0 && d0 < D) {
+        const float* qp = qkv + (long long)qrow * ld + head * D + d0;
+        qv[ks][0] = *reinterpret_cast<const float4*>(qp);
+        if (d0 + 4 < D) qv[ks][1] = *reinterpret_cast<const float4*>(qp + 4);
+      }
+    }
+  };
+  // ---- split into LDS buffer b (K, V^T) and the q fragments ----
+  bf16x8 qf[NKS][NT];
+  int qrow_s = -1;
+  auto stage = [&](int b) {
+    char* Ks = lds + b * BUF;
+    unsigned short* Vt = reinterpret_cast<unsigned short*>(lds + b * BUF + QK_BYTES);
+#pragma unroll
+    for (int j = 0; j < NK; ++j) {
+      const int e = tid + 256 * j;
+      if (e < KMAX * CH) {
+        const int row = e / CH, ch = e - row * CH;
+        uint2 t[NT];
+        sfx::split2h(kv[j], sq, t);
+        const int o = qk_off(row, ch >> 1) + ((ch & 1) << 3);
+#pragma unroll
+        for (int q = 0; q < NT; ++q) *reinterpret_cast<uint2*>(Ks + q * KMAX * QROW + o) = t[q];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const int e = tid + 256 * j;
+      if (e < (KMAX / 2) * CH) {
+        const int kp = e / CH, ch = e - kp * CH;
+        const int row = 2 * kp;
+        uint2 t0[NT], t1[NT];
+        sfx::split2h(vv0[j], sq, t0);
+        sfx::split2h(vv1[j], sq, t1);
+        const int kk = row & 15;
+        const int pos = (row & ~15) + 8 * ((kk >> 2) & 1) + (((kk >> 3) << 2) | (kk & 3));
+#pragma unroll
+        for (int q = 0; q < NT; ++q) {
+          unsigned* vt = reinterpret_cast<unsigned*>(Vt + (q * D + 4 * ch) * VST + pos);
+          vt[0] = (t0[q].x & 0xffffu) | (t1[q].x << 16);
+          vt[VST / 2] = (t0[q].x >> 16) | (t1[q].x & 0xffff0000u);
+          vt[VST] = (t0[q].y & 0xffffu) | (t1[q].y << 16);
+          vt[3 * VST / 2] = (t0[q].y >> 16) | (t1[q].y & 0xffff0000u);
+        }
+      }
+    }
+    const float qs = scale * 1.4426950408889634f;
+    typedef unsigned uintx4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      float4 a = qv[ks][0], bb = qv[ks][1];
+      a.x *= qs; a.y *= qs; a.z *= qs; a.w *= qs;
+      bb.x *= qs; bb.y *= qs; bb.z *= qs; bb.w *= qs;
+      uint2 ta[NT], tb[NT];
+      sfx::split2h(a, sq, ta);
+      sfx::split2h(bb, sq, tb);
+#pragma unroll
+      for (int q = 0; q < NT; ++q) qf[ks][q] = __builtin_bit_cast(bf16x8, (uintx4){ta[q].x, ta[q].y, tb[q].x, tb[q].y});
+    }
+    qrow_s = qrow;
+  };
+
+  fetch(i0);
+  stage(0);
+  __syncthreads();
+  constexpr int QA[3] = {1, 0, 0}, QB[3] = {0, 1, 0};
+  auto mfma = [](const bf16x8& a, const bf16x8& b, floatx16 c) -> floatx16 {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+  };
+#pragma unroll 1
+  for (int it = i0; it < i1; ++it) {
+    const int b = (it - i0) & 1;
+    const int w = it / heads, head = it - w * heads;
+    const int key_start = win[2 * w], query_start = win[2 * w + 1];
+    if (it + 1 < i1) fetch(it + 1);  // next item's slices in flight during this item's compute
+    const char* Ks = lds + b * BUF;
+    const unsigned short* Vt = reinterpret_cast<const unsigned short*>(lds + b * BUF + QK_BYTES);
+    floatx16 sacc[4];
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sacc[kb][r] = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) {
+        bf16x8 kf[NT];
+#pragma unroll
+        for (int q = 0; q < NT; ++q)
+          kf[q] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(
+                                                 Ks + q * KMAX * QROW + qk_off(kb * 32 + l32, 2 * ks + h)));
+#pragma unroll
+        for (int j = 0; j < 3; ++j) sacc[kb] = mfma(kf[QA[j]], qf[ks][QB[j]], sacc[kb]);
+      }
+    }
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sacc[kb][r] = sacc[kb][r] * iq * iq;
+    if (Kwin < KMAX) {
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          if (key >= Kwin) sacc[kb][r] = -INFINITY;
+        }
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sacc[kb][r]);
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    float sum = 0.f;
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float e = __builtin_amdgcn_exp2f(sacc[kb][r] - mx);
+        sacc[kb][r] = e;
+        sum += e;
+      }
+    sum += __shfl_xor(sum, 32, 64);
+    const float rinv = 1.f / sum;
+    floatx16 o;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[r] = 0.f;
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        uint2 a[NT], bb[NT];
+        sfx::split2h(make_float4(sacc[kb][8 * st + 0], sacc[kb][8 * st + 1], sacc[kb][8 * st + 2], sacc[kb][8 * st + 3]),
+                     16384.f, a);
+        sfx::split2h(make_float4(sacc[kb][8 * st + 4], sacc[kb][8 * st + 5], sacc[kb][8 * st + 6], sacc[kb][8 * st + 7]),
+                     16384.f, bb);
+        bf16x8 pf[NT], vf[NT];
+#pragma unroll
+        for (int q = 0; q < NT; ++q) {
+          pf[q] = __builtin_bit_cast(bf16x8, make_uint4(a[q].x, a[q].y, bb[q].x, bb[q].y));
+          uint4 v4 = make_uint4(0, 0, 0, 0);
+          if (l32 < D) v4 = *reinterpret_cast<const uint4*>(Vt + (q * D + l32) * VST + (2 * kb + st) * 16 + 8 * h);
+          vf[q] = __builtin_bit_cast(bf16x8, v4);
+        }
+#pragma unroll
+        for (int j = 0; j < 3; ++j) o = mfma(vf[QA[j]], pf[QB[j]], o);
+      }
+    const float oscale = rinv * iq * (1.f / 16384.f);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[r] *= oscale;
+    const int qi = 32 * wid + l32;
+    const int qpos = key_start + qi;
+    if (qi < Kwin && qpos >= query_start) {
+      float* dst = out + (long long)qrow_s * C + head * D;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int dd = 8 * g + 4 * h;
+        if (dd + 3 < D) *reinterpret_cast<float4*>(dst + dd) = make_float4(o[4 * g + 0], o[4 * g + 1], o[4 * g + 2], o[4 * g + 3]);
+      }
+    }
+    if (it + 1 < i1) stage(b ^ 1);
+    __syncthreads();
+  }
+}
+
+
 // Flash mode on split MFMA terms (default for sfx_window_attention_varlen): window_attn_split_kernel's
 // dataflow (per-lane query fragments, K / V^T term images, S^T = K Q^T and O^T = V^T P^T on fp16x2 or bf16x3
 // terms) with the window's keys streamed in 128-key blocks and an online softmax: the running maximum
@@ -1193,6 +1448,12 @@ window_attn_bwd_kernel(const float* __restrict__ qkv, const int* __restrict__ or
   }
 }
 
+// SFX_ATTN_SEQ=0: one (window, head) item per workgroup (window_attn_split_kernel) instead of the pipeline
+bool attn_seq() {
+  const char* e = getenv("SFX_ATTN_SEQ");  // (read per call: tests switch it)
+  return !(e && e[0] == '0');
+}
+
 }  // namespace
 
 extern "C" {
@@ -1224,6 +1485,17 @@ int sfx_window_attention(int num_windows, int window, int heads, int head_dim, i
       window_attn_kernel<24><<<grid, 256, 0, st>>>(qkv, order, win, window, channels, scale, out);
     else
       window_attn_kernel<32><<<grid, 256, 0, st>>>(qkv, order, win, window, channels, scale, out);
+  } else if (qkv_amax && attn_seq()) {  // fp16x2 terms, pipelined over (window, head) items
+    const int items = num_windows * heads;
+    const int ipw = (items + 511) / 512;  // at most 512 workgroups: one round at 2 per CU
+    const long long nwg = ((long long)(items + ipw - 1) / ipw + 7) / 8 * 8;
+#define SFX_ATTN_SEQ(DD)                                                                                     \
+  window_attn_seq_kernel<DD><<<dim3((unsigned)nwg), 256, 0, st>>>(qkv, order, win, window, channels, scale, out, \
+                                                                   qkv_amax, qkv_tag, items, ipw)
+    if (head_dim == 16) SFX_ATTN_SEQ(16);
+    else if (head_dim == 24) SFX_ATTN_SEQ(24);
+    else SFX_ATTN_SEQ(32);
+#undef SFX_ATTN_SEQ
   } else if (qkv_amax) {  // fp16x2 terms (the caller bounds |qkv|)
 #define SFX_ATTN(DD, F)                                                                                  \
   window_attn_split_kernel<DD, F><<<dim3((unsigned)nblk), 256, 0, st>>>(qkv, order, win, window, channels, scale, \

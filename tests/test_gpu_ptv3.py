@@ -376,6 +376,28 @@ def test_window_attention_vs_reference_padding(device, n, heads, C, terms):
     assert rel_l2(out.cpu(), ref) < 2e-6
 
 
+@pytest.mark.parametrize("n,heads,C", [(100_000, 2, 64), (90_434, 4, 96), (37_759, 16, 256), (14_764, 32, 512),
+                                       (3000, 4, 96), (77, 2, 64)])
+def test_window_attention_seq_bitwise(device, n, heads, C, monkeypatch):
+    """The pipelined attention (window_attn_seq_kernel: consecutive (window, head) items per workgroup, the next
+    item's gathers in flight during the current one's MFMAs) equals the one-item-per-workgroup kernel bit for bit
+    (same arithmetic, same term order) at the config-B stage shapes, a ragged last window and K = n < 128."""
+    g = torch.Generator().manual_seed(n + heads)
+    qkv = (torch.randn(n, 3 * C, generator=g) * 0.3).to(device)
+    order = torch.randperm(n, generator=g).int().to(device)
+    K = min(n, 128)
+    tab = ops.window_table([n], K)
+    win = torch.tensor(tab, dtype=torch.int32).to(device)
+    slot = ops.new_amax(qkv.device)
+    from splatformer_amd._lib import call, ptr, stream
+    call("sfx_amax_f32", n, 3 * C, ptr(qkv), 3 * C, slot[0], slot[1], stream())
+    monkeypatch.setenv("SFX_ATTN_SEQ", "1")
+    a = ops.window_attention(qkv, order, win, len(tab), K, heads, C, qkv_amax=slot)
+    monkeypatch.setenv("SFX_ATTN_SEQ", "0")
+    b = ops.window_attention(qkv, order, win, len(tab), K, heads, C, qkv_amax=slot)
+    assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("terms", ["bf16x3", "fp16x2"])
 @pytest.mark.parametrize("K", [1024, 256])
 @pytest.mark.parametrize("heads,C", [(2, 32), (4, 96), (8, 256)])
