@@ -124,16 +124,22 @@ __device__ __forceinline__ float wave_max(float v) {
 }
 // Sum over the 64 lanes, result uniform (every lane): DPP butterflies inside each 16-lane row
 // (quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror, row_mirror) + the four row sums read back as scalars.
-// No LDS traffic, unlike __shfl_xor (ds_bpermute).
+// No LDS traffic, unlike __shfl_xor (ds_bpermute).  bound_ctrl set (every lane of these patterns reads a
+// valid lane, so it changes nothing) lets the compiler fold the move into v_add_f32_dpp.
 __device__ __forceinline__ float dpp_add(float v, int ctrl_sel) {
   int t;
   switch (ctrl_sel) {
-    case 0: t = __builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false); break;   // quad [1,0,3,2]
-    case 1: t = __builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, false); break;   // quad [2,3,0,1]
-    case 2: t = __builtin_amdgcn_mov_dpp(__float_as_int(v), 0x141, 0xF, 0xF, false); break;  // row_half_mirror
-    default: t = __builtin_amdgcn_mov_dpp(__float_as_int(v), 0x140, 0xF, 0xF, false); break; // row_mirror
+    case 0: t = __builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, true); break;   // quad [1,0,3,2]
+    case 1: t = __builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, true); break;   // quad [2,3,0,1]
+    case 2: t = __builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xF, 0xF, true); break;  // row_half_mirror
+    default: t = __builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x140, 0xF, 0xF, true); break; // row_mirror
   }
   return v + __int_as_float(t);
+}
+// v of the lane the DPP control selects (quad_perm / row_ror / mirror patterns: every lane reads a valid lane)
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, true));
 }
 __device__ __forceinline__ float wave_sum_dpp(float v) {
   v = dpp_add(v, 0);

@@ -1275,7 +1275,7 @@ rasterize_bwd_quad_kernel(int tiles_x, int tiles_y, int img_h, int img_w, const 
   const int wave_bin_final = sfx::wave_max_i(inside ? bin_final : -1);
   const unsigned long long lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   constexpr int RING = 8;
-  __shared__ float ring[4][RING][11][4];
+  __shared__ float ring[4][RING][12][4];
   __shared__ int ring_g[4][RING];
   int nring = 0;  // records parked in this wave's ring (wave-uniform)
   auto flush_ring = [&]() {
@@ -1381,20 +1381,33 @@ rasterize_bwd_quad_kernel(int tiles_x, int tiles_y, int img_h, int img_w, const 
         g_ay = fabsf(g_xy1);
         g_o = vis * v_alpha;
       }
-      // row sums (4 DPP butterflies per value) parked in this wave's LDS ring; the 4 row partials of 8 records
-      // are added and sent with one atomic per (record, value) by the wave's lanes in parallel (flush below)
-      float vals[11] = {g_rgb0, g_rgb1, g_rgb2, g_c0, g_c1, g_c2, g_xy0, g_xy1, g_o, g_ax, g_ay};
-      const int nvals = v_xy_abs ? 11 : 9;
+      // row sums of the 12 slots by a transposing butterfly: lane bit 0 then bit 1 split the slots between the
+      // two partners (each keeps half, adds the other's copy of it: 12 -> 6 -> 3 slots per lane), then two
+      // rotations sum the row's 4 quads -- 6 + 3 + 6 DPP moves instead of 4 per slot.  Lane (l & 3) of each row
+      // then holds slots 6 (l & 1) + 3 ((l >> 1) & 1) + {0, 1, 2}, parked in this wave's LDS ring; the 4 row
+      // partials of 8 records are added and sent with one atomic per (record, value) by the wave's lanes in
+      // parallel (flush below)
+      const float vals[12] = {g_rgb0, g_rgb1, g_rgb2, g_c0, g_c1, g_c2, g_xy0, g_xy1, g_o, g_ax, g_ay, 0.f};
+      const bool hi0 = lane & 1, hi1 = lane & 2;
+      float h6[6], h3[3];
 #pragma unroll
-      for (int c = 0; c < 11; ++c) {
-        if (c < nvals) {
-          float x = vals[c];
-          x = sfx::dpp_add(x, 0);
-          x = sfx::dpp_add(x, 1);
-          x = sfx::dpp_add(x, 2);
-          x = sfx::dpp_add(x, 3);
-          if ((lane & 15) == 0) ring[w][nring][c][lane >> 4] = x;
-        }
+      for (int i = 0; i < 6; ++i) {
+        const float keep = hi0 ? vals[i + 6] : vals[i], send = hi0 ? vals[i] : vals[i + 6];
+        h6[i] = keep + sfx::dpp_mov<0xB1>(send);  // quad [1,0,3,2]
+      }
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        const float keep = hi1 ? h6[i + 3] : h6[i], send = hi1 ? h6[i] : h6[i + 3];
+        h3[i] = keep + sfx::dpp_mov<0x4E>(send);  // quad [2,3,0,1]
+      }
+#pragma unroll
+      for (int i = 0; i < 3; ++i) h3[i] += sfx::dpp_mov<0x124>(h3[i]);  // row_ror:4
+#pragma unroll
+      for (int i = 0; i < 3; ++i) h3[i] += sfx::dpp_mov<0x128>(h3[i]);  // row_ror:8
+      if ((lane & 15) < 4) {
+        const int base = 6 * (lane & 1) + 3 * ((lane >> 1) & 1);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) ring[w][nring][base + i][lane >> 4] = h3[i];
       }
       if (lane == 0) ring_g[w][nring] = id_batch[t];
       if (++nring == RING) flush_ring();

@@ -4,7 +4,7 @@ cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 O=gpurun_out
 T=${1:-r04a}
 SEL=${2:-"tests/test_gpu_ptv3.py tests/test_gpu_render.py"}
-K=${3:-"fused or sort or scan or embed or seq"}
+K=${3:-"fused or sort or scan or embed or seq or cull or backward"}
 mkdir -p $O
 step() { echo "== $(date +%T) $*"; }
 step tests
@@ -18,4 +18,6 @@ SFX_ATTN_SEQ=0 timeout -k 10 400 python -u bench.py --steps 20 --no-cpu-baseline
 python -c "import json; d=json.load(open('$O/${T}_bench_attn0.json')); print('attn-seq off', d['value'], d['ms_per_step'])"
 step profB
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/${T}_pb -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --profile-only > $O/${T}_pb.log 2>&1 || { tail -20 $O/${T}_pb.log; exit 1; }
+step profC
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/${T}_pc -o run --output-format csv -- python3 bench.py --config C --steps 3 --warmup 1 --profile-only > $O/${T}_pc.log 2>&1 || { tail -20 $O/${T}_pc.log; exit 1; }
 step done
