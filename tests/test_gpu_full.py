@@ -121,6 +121,37 @@ def check_cull_view(w: Workload, v: int, m):
         assert torch.equal(M["final_Ts"][v].cpu(), F["final_Ts"][v].cpu()), f"view {v}: culling changed final T"
 
 
+def check_cull_view_vs_full(w: Workload, v: int):
+    """check_cull_view against the HIP full-list render of the same view instead of the oracle's list (the full
+    list equals the oracle's key for key on the views check_render_view covers); vectorised, for the views whose
+    oracle render is too slow at config E's size.  The culled list is a subsequence of the full list, its tile
+    counts are <= gsplat's, and images / alphas / final T are bit-identical."""
+    M, F = w.meta, w.meta_full
+    n = w.out["means"].shape[0]
+    assert M["culled"] and not F["culled"]
+    exp_t = F["num_tiles_hit"][v].cpu()
+    assert torch.equal(M["num_tiles_hit"][v].cpu(), exp_t), f"view {v}: gsplat tile counts differ"
+    got_t = M["num_tiles_kept"][v].cpu()
+    assert bool((got_t <= exp_t).all()), f"view {v}: culled tile count above gsplat's"
+    assert (M["per_view"][v] > 0) == (int(exp_t.sum()) > 0)
+    if int(got_t.sum()) > 0:
+        keys, gids, _ = _view_list(M, v, n)
+        ek, eg, _ = _view_list(F, v, n)
+        assert keys.numel() == int(got_t.sum()) and ek.numel() == int(exp_t.sum())
+        comp_f = (ek >> 32) * n + eg.long()
+        comp_c = (keys >> 32) * n + gids.long()
+        sf, order = torch.sort(comp_f)
+        idx = torch.searchsorted(sf, comp_c).clamp_max(sf.numel() - 1)
+        assert torch.equal(sf[idx], comp_c), f"view {v}: culled pair missing from the full list"
+        p = order[idx]
+        assert bool((p[1:] > p[:-1]).all()), f"view {v}: culled list is not a subsequence of the full list"
+        assert torch.equal(keys, ek[p]), f"view {v}: culled keys differ"
+    assert torch.equal(w.rgbs[v].cpu(), w.rgbs_full[v].cpu()), f"view {v}: culling changed the image"
+    assert torch.equal(w.alphas[v].cpu(), w.alphas_full[v].cpu()), f"view {v}: culling changed alpha"
+    if "final_Ts" in M:
+        assert torch.equal(M["final_Ts"][v].cpu(), F["final_Ts"][v].cpu()), f"view {v}: culling changed final T"
+
+
 def check_render_view(w: Workload, v: int):
     """HIP eval render vs the oracle render of the same (HIP-refined) Gaussians, view v: the full (unculled)
     list key for key, and the culled default path through check_cull_view."""
@@ -228,3 +259,9 @@ def test_config_e_refine(we):
 @pytest.mark.parametrize("v", [0, 5])
 def test_config_e_render_exact(we, v):
     check_render_view(we, v)
+
+
+def test_config_e_cull_all_views(we):
+    """Culled vs full list on all 9 config-E views (views 0 and 5 also against the oracle above)."""
+    for v in range(9):
+        check_cull_view_vs_full(we, v)
