@@ -1448,10 +1448,13 @@ window_attn_bwd_kernel(const float* __restrict__ qkv, const int* __restrict__ or
   }
 }
 
-// SFX_ATTN_SEQ=0: one (window, head) item per workgroup (window_attn_split_kernel) instead of the pipeline
-bool attn_seq() {
+// SFX_ATTN_SEQ=0: one (window, head) item per workgroup (window_attn_split_kernel) instead of the pipeline;
+// SFX_ATTN_SEQ=<n> (n > 1): the pipeline on at most n workgroups (default 512)
+int attn_seq() {
   const char* e = getenv("SFX_ATTN_SEQ");  // (read per call: tests switch it)
-  return !(e && e[0] == '0');
+  if (!e || !e[0]) return 512;
+  const int v = atoi(e);
+  return v == 0 ? 0 : v > 1 ? v : 512;
 }
 
 }  // namespace
@@ -1485,9 +1488,9 @@ int sfx_window_attention(int num_windows, int window, int heads, int head_dim, i
       window_attn_kernel<24><<<grid, 256, 0, st>>>(qkv, order, win, window, channels, scale, out);
     else
       window_attn_kernel<32><<<grid, 256, 0, st>>>(qkv, order, win, window, channels, scale, out);
-  } else if (qkv_amax && attn_seq()) {  // fp16x2 terms, pipelined over (window, head) items
+  } else if (const int seq_wgs = qkv_amax ? attn_seq() : 0) {  // fp16x2 terms, pipelined over (window, head) items
     const int items = num_windows * heads;
-    const int ipw = (items + 511) / 512;  // at most 512 workgroups: one round at 2 per CU
+    const int ipw = (items + seq_wgs - 1) / seq_wgs;  // at most seq_wgs workgroups (512: one round at 2 per CU)
     const long long nwg = ((long long)(items + ipw - 1) / ipw + 7) / 8 * 8;
 #define SFX_ATTN_SEQ(DD)                                                                                     \
   window_attn_seq_kernel<DD><<<dim3((unsigned)nwg), 256, 0, st>>>(qkv, order, win, window, channels, scale, out, \
