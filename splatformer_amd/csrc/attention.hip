@@ -1448,11 +1448,12 @@ window_attn_bwd_kernel(const float* __restrict__ qkv, const int* __restrict__ or
   }
 }
 
-// SFX_ATTN_SEQ=0: one (window, head) item per workgroup (window_attn_split_kernel) instead of the pipeline;
-// SFX_ATTN_SEQ=<n> (n > 1): the pipeline on at most n workgroups (default 512)
+// SFX_ATTN_SEQ=1: the pipelined kernel (window_attn_seq_kernel) on at most 512 workgroups, SFX_ATTN_SEQ=<n>
+// (n > 1) on at most n; default and 0: one (window, head) item per workgroup (window_attn_split_kernel), which
+// measured faster (config B 568 vs 553 renders/s at 768 / 1024 workgroups, profiles/r04_ab_bench.txt)
 int attn_seq() {
   const char* e = getenv("SFX_ATTN_SEQ");  // (read per call: tests switch it)
-  if (!e || !e[0]) return 512;
+  if (!e || !e[0]) return 0;
   const int v = atoi(e);
   return v == 0 ? 0 : v > 1 ? v : 512;
 }

@@ -676,8 +676,9 @@ def subm_partials_ok(x: Tensor, smap: "SubmMap", cout: int) -> bool:
 
 
 # Block.cpe + shortcut + norm1 of the eval forward in one launch with the pair products summed on chip
-# (csrc/subm_fused.hip) for these channel counts; SFX_SUBM_FUSED=0 restores the pair GEMM + pair-sum LayerNorm
-SUBM_FUSED = os.environ.get("SFX_SUBM_FUSED", "1") != "0"
+# (csrc/subm_fused.hip) for these channel counts -- opt-in (SFX_SUBM_FUSED=1): measured slower than the pair GEMM +
+# pair-sum LayerNorm it replaces (config B 513 vs 568 renders/s, profiles/r04_ab_bench.txt)
+SUBM_FUSED = os.environ.get("SFX_SUBM_FUSED", "0") == "1"
 SUBM_FUSED_KERNELS = (64, 96, 128)  # the channel counts sfx_subm_cpe_ln has kernels for
 SUBM_FUSED_CHANNELS = tuple(int(c) for c in os.environ.get("SFX_SUBM_FUSED_CHANNELS", "64,96,128").split(",")
                             if c and int(c) in SUBM_FUSED_KERNELS)
