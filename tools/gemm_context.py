@@ -5,8 +5,9 @@ the config-B refine) timed where the refine issues them and replayed alone on th
                                                                GRBM counters, then TCC hit/miss)
   summarize:  python tools/gemm_context.py summarize <outdir>
 
-The program: 2 warm-up refines; marker; 2 refines (the in-refine launches are recorded: the linears whose shape
-is one of SHAPES); marker; each recorded launch replayed REPS times back to back on its own inputs; marker.
+The program: 2 warm-up refines; 2 refines in which every linear whose shape is one of SHAPES is bracketed by two
+marker kernels (its in-refine launch); then per shape the first recorded call replayed REPS times back to back on
+its own inputs, bracketed by two markers.  labels.json (written by the program) names the brackets in order.
 Per shape and context: median kernel duration (trace pass), effective clock = GRBM_GUI_ACTIVE / 8 XCDs /
 duration (MI355X_MICROARCH.md, DVFS give-back), matrix-pipe busy = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x
 GRBM_GUI_ACTIVE / 8), wait share = SQ_WAIT_ANY / SQ_WAVE_CYCLES, L2 hit rate = TCC_HIT / (TCC_HIT + TCC_MISS).
@@ -31,6 +32,7 @@ PASSES = {
 
 
 def program():
+    import json
     import torch
     from splatformer_amd import _lib
     from splatformer_amd import ptv3_ops as ops
@@ -43,40 +45,48 @@ def program():
     for _ in range(2):
         model.refine_packed(scene)
     torch.cuda.synchronize()
-    rec = []
+    rec, labels = [], []
     orig = ops.linear
+    mark = lambda: _lib.call("sfx_profile_marker", 0, _lib.stream())
 
     def linear(x, weight, bias=None, **kw):
-        out = orig(x, weight, bias, **kw)
         M = x.shape[0] if kw.get("rows") is None else kw["rows"]
         key = (M, weight.shape[0], weight.shape[1])
-        if key in SHAPES and kw.get("gather_idx") is None and len(rec) < 64:
+        if key not in SHAPES or kw.get("gather_idx") is not None:
+            return orig(x, weight, bias, **kw)
+        mark()  # each recorded launch bracketed by two markers
+        out = orig(x, weight, bias, **kw)
+        mark()
+        labels.append(("refine", SHAPES[key]))
+        if len(rec) < 64:
             rec.append((SHAPES[key], x, weight, bias, dict(kw)))
         return out
 
-    mark = lambda i: _lib.call("sfx_profile_marker", i, _lib.stream())
-    mark(0)
     ops.linear = linear
     for _ in range(2):
         model.refine_packed(scene)
     ops.linear = orig
-    mark(1)
     seen = set()
     for name, x, w, b, kw in rec:
         if name in seen:
             continue
         seen.add(name)
         kw = {k: v for k, v in kw.items() if k not in ("out", "y_amax")}
+        mark()
         for _ in range(REPS):
             orig(x, w, b, **kw)
-    mark(2)
+        mark()
+        labels.append(("isolated", name))
     torch.cuda.synchronize()
-    print("recorded", sorted(seen), flush=True)
+    with open(os.environ["GEMM_CTX_LABELS"], "w") as f:
+        json.dump(labels, f)
+    print("recorded", sorted(seen), len(labels), flush=True)
 
 
 def run(outdir):
     os.makedirs(outdir, exist_ok=True)
     for tag, opts in PASSES.items():
+        os.environ["GEMM_CTX_LABELS"] = os.path.join(outdir, "labels.json")
         cmd = ["timeout", "-s", "KILL", "240", "rocprofv3", *opts, "-d", os.path.join(outdir, tag), "-o", "run",
                "--output-format", "csv", "--", sys.executable, os.path.abspath(__file__), "program"]
         print("==", tag, flush=True)
@@ -86,55 +96,54 @@ def run(outdir):
             sys.exit(r.returncode)
 
 
-def _segments(rows):
-    """rows sorted by dispatch id: (id, kernel, grid, payload) -> (in-refine rows, isolated rows) by markers."""
-    marks = [d for d, k, _, _ in rows if "profile_marker_kernel" in k]
-    if len(marks) < 3:
-        raise SystemExit(f"expected 3 markers, found {len(marks)}")
-    inref = [r for r in rows if marks[0] < r[0] < marks[1] and "gemm_kernel" in r[1]]
-    iso = [r for r in rows if marks[1] < r[0] < marks[2] and "gemm_kernel" in r[1]]
-    return inref, iso
-
-
 def summarize(outdir):
+    import json
+    labels = json.load(open(os.path.join(outdir, "labels.json")))
+
+    def launches(tag):
+        """label index -> dispatch ids of the GEMM launches between its two markers (dispatch order)."""
+        f = glob.glob(os.path.join(outdir, tag, "**", "*kernel_trace.csv" if tag == "trace" else "*counter_collection.csv"),
+                      recursive=True)[0]
+        seen, rows = set(), []
+        for r in csv.DictReader(open(f)):
+            d = int(r["Dispatch_Id"])
+            if d not in seen:
+                seen.add(d)
+                rows.append((d, r["Kernel_Name"]))
+        rows.sort()
+        marks = [i for i, (d, k) in enumerate(rows) if "profile_marker_kernel" in k]
+        assert len(marks) == 2 * len(labels), (tag, len(marks), len(labels))
+        return [[rows[j][0] for j in range(marks[2 * i] + 1, marks[2 * i + 1]) if "gemm_kernel" in rows[j][1]]
+                for i in range(len(labels))]
+
     tr = glob.glob(os.path.join(outdir, "trace", "**", "*kernel_trace.csv"), recursive=True)[0]
-    dur = {}
-    rows = []
-    for r in csv.DictReader(open(tr)):
-        d = int(r["Dispatch_Id"])
-        dur[d] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3  # us
-        rows.append((d, r["Kernel_Name"], r.get("Grid_Size", ""), None))
-    rows.sort()
-    inref, iso = _segments(rows)
-    # isolated launches: REPS per recorded shape in recording order; match the in-refine launches by grid size
-    grids_iso = defaultdict(list)
-    for d, k, g, _ in iso:
-        grids_iso[g].append(d)
-    cnt = {}
+    dur = {int(r["Dispatch_Id"]): (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+           for r in csv.DictReader(open(tr))}
+    cnt, ids = {}, {"trace": launches("trace")}
     for tag in ("sq", "tcc"):
         f = glob.glob(os.path.join(outdir, tag, "**", "*counter_collection.csv"), recursive=True)[0]
         c = defaultdict(dict)
         for r in csv.DictReader(open(f)):
             c[int(r["Dispatch_Id"])][r["Counter_Name"]] = float(r["Counter_Value"])
         cnt[tag] = c
-    print(f"{'grid':>10s} {'ctx':>8s} {'n':>3s} {'us':>8s} {'GHz':>6s} {'MFMA%':>6s} {'wait%':>6s} {'L2hit%':>7s}")
-    for g, ids_iso in sorted(grids_iso.items()):
-        ids_in = [d for d, k, gg, _ in inref if gg == g]
-        for ctx, ids in (("refine", ids_in), ("isolated", ids_iso)):
-            if not ids:
+        ids[tag] = launches(tag)
+    print(f"{'shape':>6s} {'ctx':>8s} {'n':>3s} {'us':>8s} {'GHz':>6s} {'MFMA%':>6s} {'wait%':>6s} {'L2hit%':>7s}")
+    for name in ("qkv", "fc1", "fc2"):
+        for ctx in ("refine", "isolated"):
+            sel = [i for i, (c, nm) in enumerate(labels) if c == ctx and nm == name]
+            if not sel:
                 continue
-            us = statistics.median(dur[d] for d in ids)
-            ga = statistics.median(cnt["sq"][d].get("GRBM_GUI_ACTIVE", 0) for d in ids if d in cnt["sq"])
-            busy = statistics.median(cnt["sq"][d].get("SQ_VALU_MFMA_BUSY_CYCLES", 0) for d in ids if d in cnt["sq"])
-            wa = statistics.median(cnt["sq"][d].get("SQ_WAIT_ANY", 0) for d in ids if d in cnt["sq"])
-            wc = statistics.median(cnt["sq"][d].get("SQ_WAVE_CYCLES", 1) for d in ids if d in cnt["sq"])
-            hit = statistics.median(cnt["tcc"][d].get("TCC_HIT_sum", 0) for d in ids if d in cnt["tcc"])
-            miss = statistics.median(cnt["tcc"][d].get("TCC_MISS_sum", 0) for d in ids if d in cnt["tcc"])
+            us = statistics.median(dur[d] for i in sel for d in ids["trace"][i])
+            med = lambda tag, k, dflt=0.0: statistics.median(cnt[tag][d].get(k, dflt) for i in sel for d in ids[tag][i])
+            ga, busy = med("sq", "GRBM_GUI_ACTIVE"), med("sq", "SQ_VALU_MFMA_BUSY_CYCLES")
+            wa, wc = med("sq", "SQ_WAIT_ANY"), med("sq", "SQ_WAVE_CYCLES", 1.0)
+            hit, miss = med("tcc", "TCC_HIT_sum"), med("tcc", "TCC_MISS_sum")
+            n = sum(len(ids["trace"][i]) for i in sel)
             # the pmc passes serialise dispatches: their GRBM cycles over the trace pass's duration give the clock
             # the kernel ran at only approximately (profiled passes clock 2-5 % lower, DVFS give-back item 2)
             ghz = ga / 8 / (us * 1e3) if us > 0 else 0.0
             mfma = busy / (1024 * ga / 8) if ga > 0 else 0.0
-            print(f"{g:>10s} {ctx:>8s} {len(ids):3d} {us:8.1f} {ghz:6.2f} {100 * mfma:6.1f} {100 * wa / wc:6.1f} "
+            print(f"{name:>6s} {ctx:>8s} {n:3d} {us:8.1f} {ghz:6.2f} {100 * mfma:6.1f} {100 * wa / wc:6.1f} "
                   f"{100 * hit / max(1.0, hit + miss):7.1f}")
 
 
