@@ -33,9 +33,10 @@ const char* sfx_last_error(void);
 /* int32/int64 scan (inclusive != 0 -> inclusive).  `total` (optional, device)
  * receives the grand total.  Replaces torch.cumsum(num_tiles_hit, dtype=int32)
  * inside gsplat rasterize_gaussians (called at utils/gs_utils.py:96).
- * (ABI v11) int32: one single-pass launch with decoupled look-back after a
- * reset of `ws` (scratch, no initialisation needed; not shared by concurrent
- * calls); in place (in == out) allowed. */
+ * (ABI v11) int32: one single-pass launch with decoupled look-back on a
+ * library-owned ticket + tile-word area per (device, stream), epoch-tagged so
+ * it needs no reset between scans (`ws` is still size-checked, unused);
+ * in place (in == out) allowed. */
 size_t sfx_scan_workspace_bytes(long long n);
 int sfx_scan_i32(long long n, const int32_t* in, int32_t* out, int inclusive, void* ws, size_t ws_bytes,
                  int32_t* total, void* stream);
@@ -48,7 +49,7 @@ int sfx_scan_i64(long long n, const int64_t* in, int64_t* out, int inclusive, vo
  * (utils/gs_utils.py:96) and torch.argsort(code) / torch.sort(cluster) in
  * Pointcept serialization/pooling (models/pointtransformer_v3.py:380, :290).
  * (ABI v11) per 8-bit pass: tile histograms, one single-pass look-back scan
- * (its area reset once per sort), stable scatter. */
+ * (on the stream's library-owned area, as sfx_scan_i32), stable scatter. */
 size_t sfx_sort_workspace_bytes(long long n);
 int sfx_sort_pairs_u64(long long n, const uint64_t* keys_in, const int32_t* vals_in, uint64_t* keys_out,
                        int32_t* vals_out, int begin_bit, int end_bit, void* ws, size_t ws_bytes, void* stream);

@@ -20,7 +20,9 @@ namespace sfx {
 
 void set_error(const char* fmt, ...);
 void clear_error();
-// single-pass int32 scan (common.hip) on a caller-managed look-back area (see there)
+// single-pass int32 scan (common.hip) on a look-back area (see there); lookback_state: the library-owned area of
+// a (device, stream) with room for `words` tile words, plus a fresh tag for one scan on it
+int lookback_state(hipStream_t st, long long words, unsigned** ticket, unsigned long long** flags, unsigned* tag);
 long long lookback_scan_words(long long n);
 void lookback_scan_i32(long long n, const int32_t* in, int32_t* out, int inclusive, unsigned* ticket,
                        unsigned long long* flags, unsigned tag, int32_t* total, hipStream_t st);

@@ -1,4 +1,8 @@
 // Error plumbing + generic device primitives (scan) shared by every stage.
+#include <map>
+#include <mutex>
+#include <utility>
+
 #include "common.h"
 
 #include <cstring>
@@ -129,9 +133,11 @@ int scan_impl(long long n, const T* in, T* out, int inclusive, void* ws, size_t 
 }
 
 // ---- int32: single pass with decoupled look-back --------------------------------------------------------------
-// One launch after a memset of the (tile-word) workspace: each 2048-element tile takes a ticket, scans itself,
-// publishes its aggregate, gets its exclusive prefix from its predecessors' words (sfx::lb_lookback_wave), publishes
-// its inclusive prefix and writes.  The last tile writes the grand total.
+// One launch: each 2048-element tile takes a ticket, scans itself, publishes its aggregate, gets its exclusive prefix
+// from its predecessors' words (sfx::lb_lookback_wave), publishes its inclusive prefix and writes.  The last tile
+// writes the grand total.  The ticket and tile words live in a library-owned area per (device, stream)
+// (sfx::lookback_state): the last ticket's holder puts the counter back to 0 and every call tags its words with a
+// new epoch, so stale words of earlier scans never match -- no memset per scan.
 constexpr int LB_ITEMS = 8;
 constexpr int LB_TILE = SCAN_THREADS * LB_ITEMS;
 constexpr size_t LB_HEADER = 256;  // ticket counter, then the tile words
@@ -142,7 +148,11 @@ scan_lookback_i32(const int32_t* __restrict__ in, int32_t* __restrict__ out, lon
                   unsigned tag) {
   __shared__ int32_t smem[SCAN_THREADS / 64];
   __shared__ int s_tile, s_prefix;
-  if (threadIdx.x == 0) s_tile = (int)atomicAdd(ticket, 1u);
+  if (threadIdx.x == 0) {
+    const int t = (int)atomicAdd(ticket, 1u);
+    s_tile = t;
+    if (t == tiles - 1) atomicExch(ticket, 0u);  // every ticket handed out: ready for the stream's next scan
+  }
   __syncthreads();
   const int tile = s_tile;
   const long long base = (long long)tile * LB_TILE + (long long)threadIdx.x * LB_ITEMS;
@@ -195,20 +205,65 @@ int scan_lookback_impl(long long n, const int32_t* in, int32_t* out, int inclusi
     sfx::set_error("scan: workspace too small or misaligned (%zu < %zu)", ws_bytes, need);
     return SFX_ERR_WORKSPACE;
   }
-  char* p = reinterpret_cast<char*>(ws);
-  if (hipMemsetAsync(p, 0, need, st) != hipSuccess) return sfx::check_launch("scan (workspace reset)");
-  scan_lookback_i32<<<(unsigned)tiles, SCAN_THREADS, 0, st>>>(in, out, n, inclusive, (int)tiles,
-                                                              reinterpret_cast<unsigned*>(p),
-                                                              reinterpret_cast<unsigned long long*>(p + LB_HEADER),
-                                                              total, 1u);
+  unsigned* ticket;
+  unsigned long long* flags;
+  unsigned tag;
+  const int rc = sfx::lookback_state(st, tiles, &ticket, &flags, &tag);
+  if (rc != SFX_OK) return rc;
+  scan_lookback_i32<<<(unsigned)tiles, SCAN_THREADS, 0, st>>>(in, out, n, inclusive, (int)tiles, ticket, flags,
+                                                              total, tag);
   return sfx::check_launch("scan");
 }
 
 }  // namespace
 
 namespace sfx {
-// The look-back scan on a caller-reset area shared by several scans of one stream: `ticket` zero before the
-// first use, `flags` (lookback_scan_words(n) words) zero or holding only smaller tags; `tag` distinct per call.
+namespace {
+struct LbState {
+  unsigned* ticket = nullptr;
+  unsigned long long* flags = nullptr;
+  long long words = 0;
+  unsigned epoch = 0;
+};
+std::mutex g_lb_mu;
+std::map<std::pair<int, hipStream_t>, LbState> g_lb;
+constexpr unsigned kLbEpochMax = (1u << 30) - 1;  // lb_tag is 30 bits
+}  // namespace
+
+int lookback_state(hipStream_t st, long long words, unsigned** ticket, unsigned long long** flags, unsigned* tag) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return check_launch("look-back state (device)");
+  std::lock_guard<std::mutex> lock(g_lb_mu);
+  LbState& s = g_lb[{dev, st}];
+  if (s.words < words) {  // first use of this stream, or a larger scan: (re)allocate, zeroed in stream order
+    const long long w = words > (1ll << 16) ? words : (1ll << 16);
+    if (s.ticket) {  // an earlier scan of this stream may still be running on the old area
+      if (hipStreamSynchronize(st) != hipSuccess || hipFree(s.ticket) != hipSuccess)
+        return check_launch("look-back state (release)");
+      s = LbState();
+    }
+    void* p = nullptr;
+    const size_t bytes = 256 + sizeof(unsigned long long) * (size_t)w;
+    if (hipMalloc(&p, bytes) != hipSuccess) return check_launch("look-back state (allocate)");
+    if (hipMemsetAsync(p, 0, bytes, st) != hipSuccess) return check_launch("look-back state (reset)");
+    s.ticket = static_cast<unsigned*>(p);
+    s.flags = reinterpret_cast<unsigned long long*>(static_cast<char*>(p) + 256);
+    s.words = w;
+    s.epoch = 0;
+  }
+  if (s.epoch == kLbEpochMax) {  // tags about to wrap: clear the words once
+    if (hipMemsetAsync(s.flags, 0, sizeof(unsigned long long) * (size_t)s.words, st) != hipSuccess)
+      return check_launch("look-back state (epoch wrap)");
+    s.epoch = 0;
+  }
+  *tag = ++s.epoch;
+  *ticket = s.ticket;
+  *flags = s.flags;
+  return SFX_OK;
+}
+
+// The look-back scan on a given area: `ticket` zero (the kernel puts it back to zero), `flags`
+// (lookback_scan_words(n) words) holding no word with this call's `tag` (sfx::lookback_state hands out both).
 long long lookback_scan_words(long long n) { return (n + LB_TILE - 1) / LB_TILE; }
 void lookback_scan_i32(long long n, const int32_t* in, int32_t* out, int inclusive, unsigned* ticket,
                        unsigned long long* flags, unsigned tag, int32_t* total, hipStream_t st) {

@@ -145,13 +145,7 @@ int sfx_sort_pairs_u64(long long n, const uint64_t* keys_in, const int32_t* vals
   const long long hist_n = (long long)tiles * RS_BINS;
   int* hist = reinterpret_cast<int*>(p);
   p += align256(sizeof(int32_t) * (size_t)hist_n);
-  // look-back area of the per-pass scans: 8 tickets + words tagged with the pass; reset once here
-  unsigned* tickets = reinterpret_cast<unsigned*>(p);
-  unsigned long long* flags = reinterpret_cast<unsigned long long*>(p + 256);
-  SFX_REQUIRE(passes <= 64, "sfx_sort_pairs_u64: too many passes");
-  if (hipMemsetAsync(p, 0, 256 + sizeof(unsigned long long) * (size_t)sfx::lookback_scan_words(hist_n), st) !=
-      hipSuccess)
-    return sfx::check_launch("sfx_sort_pairs_u64 (workspace reset)");
+  // the per-pass digit-count scans run on the stream's library-owned look-back area (no reset per sort)
 
   const uint64_t* ksrc = keys_in;
   const int32_t* vsrc = vals_in;
@@ -161,7 +155,12 @@ int sfx_sort_pairs_u64(long long n, const uint64_t* keys_in, const int32_t* vals
     uint64_t* kdst = to_out ? keys_out : k_alt;
     int32_t* vdst = to_out ? vals_out : v_alt;
     radix_hist<<<tiles, RS_THREADS, 0, st>>>(ksrc, n, shift, tiles, hist);
-    sfx::lookback_scan_i32(hist_n, hist, hist, 0, tickets + pass, flags, (unsigned)pass + 1u, nullptr, st);
+    unsigned* ticket;
+    unsigned long long* flags;
+    unsigned tag;
+    const int rc = sfx::lookback_state(st, sfx::lookback_scan_words(hist_n), &ticket, &flags, &tag);
+    if (rc != SFX_OK) return rc;
+    sfx::lookback_scan_i32(hist_n, hist, hist, 0, ticket, flags, tag, nullptr, st);
     radix_scatter<<<tiles, RS_THREADS, 0, st>>>(ksrc, vsrc, n, shift, tiles, hist, kdst, vdst);
     ksrc = kdst;
     vsrc = vdst;

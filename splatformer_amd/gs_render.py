@@ -185,7 +185,7 @@ def _render_fused_views(gs, c2ws, cameras, meta=None):
             kept = torch.empty(V * n, device=dev, dtype=torch.int32)
             call("sfx_isect_count_cull_views", V * n, n, ptr(xys), ptr(conics), ptr(opac), ptr(radii), tiles_x,
                  tiles_y, bw, H, W, ptr(kept), stream())
-        tot_dev = torch.zeros(1, device=dev, dtype=torch.int32)
+        tot_dev = torch.empty(1, device=dev, dtype=torch.int32)
         ws = _lib.workspace(_lib.fn("sfx_scan_workspace_bytes")(V * n), dev)
         call("sfx_scan_i32", V * n, ptr(kept), ptr(cum), 1, ptr(ws), ws.numel(), ptr(tot_dev), stream())
         ends_rd = _lib.HostRead(cum.view(V, n)[:, -1])

@@ -138,7 +138,7 @@ def compute_cumulative_intersects(num_tiles_hit: Tensor) -> Tuple[int, Tensor]:
     dev = num_tiles_hit.device
     nth = num_tiles_hit.to(torch.int32).contiguous()
     cum = torch.empty(n, device=dev, dtype=torch.int32)
-    total = torch.zeros(1, device=dev, dtype=torch.int32)
+    total = torch.empty(1, device=dev, dtype=torch.int32)
     ws = _lib.workspace(_lib.fn("sfx_scan_workspace_bytes")(n), dev)
     call("sfx_scan_i32", n, ptr(nth), ptr(cum), 1, ptr(ws), ws.numel(), ptr(total), stream())
     return int(total.item()), cum
@@ -245,7 +245,7 @@ def _culled_counts(n, num_tiles_hit, xys, radii, conics, opacity, H, W, tiles_x,
     call("sfx_isect_count_cull_views", n, n, ptr(xys), ptr(conics), ptr(opacity), ptr(radii), tiles_x, tiles_y, 16, H,
          W, ptr(kept), stream())
     cum = torch.empty(n, device=dev, dtype=torch.int32)
-    flags = torch.zeros(2, device=dev, dtype=torch.int32)  # [gsplat non-empty, culled total]
+    flags = torch.empty(2, device=dev, dtype=torch.int32)  # [gsplat non-empty, culled total]
     ws = _lib.workspace(_lib.fn("sfx_scan_workspace_bytes")(n), dev)
     call("sfx_scan_i32", n, ptr(kept), ptr(cum), 1, ptr(ws), ws.numel(), ptr(flags[1:]), stream())
     flags[0] = (num_tiles_hit.max() > 0).to(torch.int32)

@@ -475,7 +475,7 @@ def scan_i32(x: Tensor, inclusive: bool = True, total: Optional[Tensor] = None) 
     n = x.shape[0]
     out = torch.empty_like(x)
     if total is None:
-        total = torch.zeros(1, device=x.device, dtype=torch.int32)
+        total = torch.empty(1, device=x.device, dtype=torch.int32)
     ws = _lib.workspace(_lib.fn("sfx_scan_workspace_bytes")(n), x.device)
     call("sfx_scan_i32", n, ptr(x), ptr(out), 1 if inclusive else 0, ptr(ws), ws.numel(), ptr(total), stream())
     return out, total

@@ -93,7 +93,7 @@ def test_scan_and_sort_exact(device):
 
 
 def test_lookback_scan_and_onesweep_sort_cases(device):
-    """The single-pass scan and one-sweep sort (decoupled look-back, ABI v11) on the cases their hand-off has to
+    """The single-pass scan and the radix sort's per-pass scans (decoupled look-back, ABI v11) on the cases their hand-off has to
     survive: thousands of tiles (long look-back chains, tiles finishing out of order), one workspace reused by
     back-to-back calls of different sizes without a host sync, exclusive and in-place scans, a bit range that
     does not start at 0, 64-bit keys using all passes, and negative values."""
@@ -119,6 +119,18 @@ def test_lookback_scan_and_onesweep_sort_cases(device):
     _lib.call("sfx_scan_i32", x.numel(), xd.data_ptr(), xd.data_ptr(), 1, ws.data_ptr(), ws.numel(), None,
               _lib.stream())  # in place
     assert torch.equal(xd.cpu(), torch.cumsum(x, 0, dtype=torch.int32))
+    # more tiles than the stream's look-back area holds (65536 words): the area is reallocated, then a small scan
+    # and a sort on the new one; totals written without a zeroed `total`
+    for n in (2048 * 65536 + 3, 5000):
+        x = torch.randint(0, 2, (n,), generator=g, dtype=torch.int32)
+        xd = x.to(device)
+        out = torch.empty_like(xd)
+        tot = torch.full((1,), -7, device=device, dtype=torch.int32)
+        wsn = _lib.workspace(_lib.fn("sfx_scan_workspace_bytes")(n), device)
+        _lib.call("sfx_scan_i32", n, xd.data_ptr(), out.data_ptr(), 1, wsn.data_ptr(), wsn.numel(), tot.data_ptr(),
+                  _lib.stream())
+        assert torch.equal(out.cpu(), torch.cumsum(x, 0, dtype=torch.int32)) and int(tot) == int(x.sum()), n
+        del xd, out
     for n, lo, hi in [(5_000_000, 0, 47), (300_000, 5, 61), (70_000, 0, 64)]:
         keys = torch.randint(-(1 << 62), 1 << 62, (n,), generator=g, dtype=torch.int64)
         keys[::3] = keys[1]
