@@ -102,7 +102,32 @@ __device__ __forceinline__ int row_exp(float m) {
   return e > 126 ? 126 : (e < -126 ? -126 : e);
 }
 
-__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+// erf GELU (torch approximate='none') with a branch-free erf: the two argument ranges of the device library's
+// erff (|x| < 1: odd polynomial; |x| >= 1: 1 - exp(-(|x| + |x| P(|x|))), same coefficients) are both evaluated
+// and selected, so the compiler can interleave the epilogue with the MFMA stream (the library form branches per
+// lane and splits the loop into ~30 basic blocks); exp by v_exp_f32 (__expf: its error, a few ulp of
+// exp(-p) <= e^-1, moves erf by < 1e-7 of its value -- the fp32 GEMMs' own rounding level), ~30 % fewer VALU
+// than expf's range reduction (the fused MLP's GELU is its VALU bottleneck, profiles/r04_mlp_gelu_variants.txt).
+__device__ __forceinline__ float erf_nb(float x) {
+  const float ax = fabsf(x);
+  const float t = ax * ax;
+  float p1 = __builtin_fmaf(t, -0x1.268bc2p-11f, 0x1.420828p-8f);
+  p1 = __builtin_fmaf(t, p1, -0x1.b5937p-6f);
+  p1 = __builtin_fmaf(t, p1, 0x1.ce077cp-4f);
+  p1 = __builtin_fmaf(t, p1, -0x1.81266p-2f);
+  p1 = __builtin_fmaf(t, p1, 0x1.06eba0p-3f);
+  const float r1 = __builtin_fmaf(ax, p1, ax);
+  float p2 = __builtin_fmaf(ax, 0x1.1d3156p-16f, -0x1.8d129p-12f);
+  p2 = __builtin_fmaf(ax, p2, 0x1.f9a6d2p-9f);
+  p2 = __builtin_fmaf(ax, p2, -0x1.8c3164p-6f);
+  p2 = __builtin_fmaf(ax, p2, 0x1.b4e9c8p-4f);
+  p2 = __builtin_fmaf(ax, p2, 0x1.4515fap-1f);
+  p2 = __builtin_fmaf(ax, p2, 0x1.078e50p-3f);
+  p2 = __builtin_fmaf(ax, p2, ax);
+  const float r2 = 1.0f - __expf(-p2);
+  return __builtin_copysignf(ax < 1.0f ? r1 : r2, x);
+}
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erf_nb(x * 0.70710678118654752f)); }
 // d/dx of the erf GELU (torch GeluBackward, approximate='none')
 __device__ __forceinline__ float gelu_erf_grad(float x) {
   const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));

@@ -71,31 +71,6 @@ __device__ __forceinline__ int slab_off(int r, int q) {
 // (lgkmcnt(0)), so the slot the phase refills after the barrier is no longer being read (cdna_hip_programming.md
 // §5, "Read a staged buffer one phase AFTER the wait that retires it": a slot restaged one phase after its last
 // read needs that lgkmcnt before the barrier).
-// erf GELU (torch approximate='none') with a branch-free erf: the two argument ranges of the device library's
-// erff (|x| < 1: odd polynomial; |x| >= 1: 1 - exp(-(|x| + |x| P(|x|))), same coefficients) are both evaluated
-// and selected, so the compiler can interleave the epilogue with the MFMA stream (the library form branches per
-// lane and splits the loop into ~30 basic blocks).
-__device__ __forceinline__ float erf_nb(float x) {
-  const float ax = fabsf(x);
-  const float t = ax * ax;
-  float p1 = __builtin_fmaf(t, -0x1.268bc2p-11f, 0x1.420828p-8f);
-  p1 = __builtin_fmaf(t, p1, -0x1.b5937p-6f);
-  p1 = __builtin_fmaf(t, p1, 0x1.ce077cp-4f);
-  p1 = __builtin_fmaf(t, p1, -0x1.81266p-2f);
-  p1 = __builtin_fmaf(t, p1, 0x1.06eba0p-3f);
-  const float r1 = __builtin_fmaf(ax, p1, ax);
-  float p2 = __builtin_fmaf(ax, 0x1.1d3156p-16f, -0x1.8d129p-12f);
-  p2 = __builtin_fmaf(ax, p2, 0x1.f9a6d2p-9f);
-  p2 = __builtin_fmaf(ax, p2, -0x1.8c3164p-6f);
-  p2 = __builtin_fmaf(ax, p2, 0x1.b4e9c8p-4f);
-  p2 = __builtin_fmaf(ax, p2, 0x1.4515fap-1f);
-  p2 = __builtin_fmaf(ax, p2, 0x1.078e50p-3f);
-  p2 = __builtin_fmaf(ax, p2, ax);
-  const float r2 = 1.0f - expf(-p2);
-  return __builtin_copysignf(ax < 1.0f ? r1 : r2, x);
-}
-__device__ __forceinline__ float gelu_nb(float x) { return 0.5f * x * (1.f + erf_nb(x * 0.70710678118654752f)); }
-
 template <int N>
 __device__ __forceinline__ void wait_vm_lgkm() {
   static_assert(N >= 0 && N <= 63, "vmcnt range");
@@ -247,8 +222,8 @@ __global__ void __launch_bounds__(WAVES * 64, (WAVES == 4 && C > 128) ? 1 : 2)
 #pragma unroll
           for (int i2 = 0; i2 < 8; ++i2) {
             const float4 wb = pp[i2];  // (1/s_u, b1_u) of registers 2 i2, 2 i2 + 1
-            g[2 * i2 + 0] = gelu_nb(acc1[cb][2 * i2 + 0] * (sinv * wb.x) + wb.y) * tsc;
-            g[2 * i2 + 1] = gelu_nb(acc1[cb][2 * i2 + 1] * (sinv * wb.z) + wb.w) * tsc;
+            g[2 * i2 + 0] = gelu_erf(acc1[cb][2 * i2 + 0] * (sinv * wb.x) + wb.y) * tsc;
+            g[2 * i2 + 1] = gelu_erf(acc1[cb][2 * i2 + 1] * (sinv * wb.z) + wb.w) * tsc;
           }
 #pragma unroll
           for (int st = 0; st < 2; ++st) {
