@@ -40,6 +40,52 @@ def test_linear_vs_torch(device, M, N, K, act):
     assert rel_l2(y.cpu(), ref) < 2e-6
 
 
+def _slot_value(device, slot):
+    """max over the sub-slots of an amax slot (ops.new_amax ring) carrying its tag."""
+    buf = ops._amax_state[device][0] if device in ops._amax_state else ops._amax_state[torch.device(device)][0]
+    off = (slot[0] - buf.data_ptr()) // 8
+    w = buf[off:off + ops.AMAX_SUB].cpu()
+    vals = [int(v) & 0xFFFFFFFF for v in w.tolist() if (int(v) >> 32) & 0xFFFFFFFF == slot[1]]
+    return max(torch.tensor(vals, dtype=torch.int64).to(torch.int32).view(torch.float32).tolist()) if vals else 0.0
+
+
+@pytest.mark.parametrize("M,N,K", [(4097, 96, 96), (1, 128, 128), (31, 100, 64), (3001, 288, 96), (2500, 384, 128),
+                                   (777, 64, 128)])
+def test_linear_narrow_cases(device, M, N, K):
+    """The W-resident narrow-K path (gemm_narrow.hip, dense K in {64, 96, 128}): bias, GELU on the first columns
+    only, residual (also in place), max |Y| published to a slot, strided input / output, ragged M and N, rows of
+    very different magnitudes -- each row within 2x (+1e-7) of torch's fp32 CPU error against fp64."""
+    g = torch.Generator().manual_seed(M * 7 + N + K)
+    xb = torch.randn(M, K + 8, generator=g)
+    xb[::3] *= 1e4
+    xb[1::7] *= 1e-5
+    x = xb[:, 4:4 + K]
+    w = torch.randn(N, K, generator=g) / K ** 0.5
+    b = torch.randn(N, generator=g)
+    res = torch.randn(M, N, generator=g)
+    ac = N // 2
+    z = x.double() @ w.double().T + b.double()
+    ref = torch.cat([torch.nn.functional.gelu(z[:, :ac]), z[:, ac:]], 1) + res.double()
+    z32 = x @ w.T + b
+    f32 = (torch.cat([torch.nn.functional.gelu(z32[:, :ac]), z32[:, ac:]], 1) + res).double()
+    xd = xb.to(device)[:, 4:4 + K]
+    out = torch.full((M, N + 12), 7.0, device=device)
+    y, slot = ops.linear(xd, w.to(device), b.to(device), act=ops.ACT_GELU, act_ncols=ac, residual=res.to(device),
+                         out=out[:, :N], y_amax=True)
+    yh = y.cpu().double()
+    rn = ref.norm(dim=1).clamp_min(1e-30)
+    e_hip, e_f32 = (yh - ref).norm(dim=1) / rn, (f32 - ref).norm(dim=1) / rn
+    assert bool((e_hip <= 2 * e_f32 + 1e-7).all()), float((e_hip - 2 * e_f32).max())
+    assert bool((out[:, N:] == 7.0).all())
+    amax = _slot_value(device, slot)
+    assert abs(amax - float(yh.abs().max())) <= 1e-6 * float(yh.abs().max())
+    # in-place residual (Y = R): x W^T + b added onto the residual rows
+    r2 = res.to(device).clone()
+    ops.linear(xd, w.to(device), b.to(device), residual=r2, out=r2)
+    ref2 = z + res.double()
+    assert rel_l2(r2.cpu(), ref2) <= 2 * rel_l2((x @ w.T + b + res), ref2) + 1e-7
+
+
 @pytest.mark.parametrize("scale", [1.0, 1e-30, 1e30])
 def test_linear_split_precision_is_fp32(device, scale):
     """The fp16x2 split GEMM (default for K >= 64: a power-of-two scale per operand row -- A' rows chosen online
