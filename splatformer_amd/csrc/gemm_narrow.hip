@@ -61,6 +61,38 @@ __global__ void __launch_bounds__(NRW * 64, 2)
   const int n0 = cblk * NCOL;
   const int ncb = min(4, (N - n0 + 31) / 32);  // 32-column blocks of this workgroup (wave-uniform)
 
+  const __amdgpu_buffer_rsrc_t rA = rsrc_ext(A, (unsigned)M * (unsigned)lda * 4u);
+  const __amdgpu_buffer_rsrc_t rY = rsrc_ext(Y, (unsigned)M * (unsigned)ldy * 4u);
+  const __amdgpu_buffer_rsrc_t rR = rsrc_ext(R ? R : Y, R ? (unsigned)M * (unsigned)ldr * 4u : 0u);
+  const int ntiles = (M + 31) / 32;
+  const int tstride = nrowgrp * NRW;
+  int tile = rgrp * NRW + wid;
+
+  auto load_rows = [&](int t, float4 (&v)[2 * KT]) {
+    const int m = t * 32 + r32;
+    const unsigned base = (t < ntiles && m < M) ? (unsigned)m * (unsigned)lda : 0xffffffffu;
+#pragma unroll
+    for (int s = 0; s < KT; ++s) {
+      const unsigned c = (unsigned)(16 * s + 8 * h);
+      v[2 * s] = bload4(rA, base != 0xffffffffu ? (base + c) * 4u : OOB);
+      v[2 * s + 1] = bload4(rA, base != 0xffffffffu ? (base + c + 4u) * 4u : OOB);
+    }
+  };
+  // the residual rows of tile t for every column block of this workgroup (loaded with the tile's A rows)
+  auto load_res = [&](int t, float4 (&rv)[16]) {
+    const int m = t * 32 + r32;
+    const bool ok = R != nullptr && t < ntiles && m < M;
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int n = n0 + cb * 32 + 8 * g + 4 * h;
+        rv[4 * cb + g] = bload4(rR, (ok && cb < ncb && n < N) ? ((unsigned)m * (unsigned)ldr + (unsigned)n) * 4u : OOB);
+      }
+  };
+  float4 vn[2 * KT];
+  load_rows(tile, vn);  // the first tile's rows fly while W is staged
+
   // ---- stage the W block (pre-split rows n0 .. n0 + 127; rows past N zero) + its column constants ----
   {
     constexpr int GROUPS = NCOL * (K / 4);  // 4-element groups: 16 bytes of the split each (4 h then 4 l)
@@ -80,23 +112,6 @@ __global__ void __launch_bounds__(NRW * 64, 2)
   }
   __syncthreads();
 
-  const __amdgpu_buffer_rsrc_t rA = rsrc_ext(A, (unsigned)M * (unsigned)lda * 4u);
-  const __amdgpu_buffer_rsrc_t rY = rsrc_ext(Y, (unsigned)M * (unsigned)ldy * 4u);
-  const __amdgpu_buffer_rsrc_t rR = rsrc_ext(R ? R : Y, R ? (unsigned)M * (unsigned)ldr * 4u : 0u);
-  const int ntiles = (M + 31) / 32;
-  const int tstride = nrowgrp * NRW;
-  int tile = rgrp * NRW + wid;
-
-  auto load_rows = [&](int t, float4 (&v)[2 * KT]) {
-    const int m = t * 32 + r32;
-    const unsigned base = (t < ntiles && m < M) ? (unsigned)m * (unsigned)lda : 0xffffffffu;
-#pragma unroll
-    for (int s = 0; s < KT; ++s) {
-      const unsigned c = (unsigned)(16 * s + 8 * h);
-      v[2 * s] = bload4(rA, base != 0xffffffffu ? (base + c) * 4u : OOB);
-      v[2 * s + 1] = bload4(rA, base != 0xffffffffu ? (base + c + 4u) * 4u : OOB);
-    }
-  };
   auto mfma3 = [](const f16x8& ah, const f16x8& al, const f16x8& bh, const f16x8& bl, floatx16 c) {
     c = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, c, 0, 0, 0);  // smallest terms first
     c = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, c, 0, 0, 0);
@@ -104,12 +119,12 @@ __global__ void __launch_bounds__(NRW * 64, 2)
   };
 
   float ymax = 0.f;
-  float4 vn[2 * KT];
-  load_rows(tile, vn);
   for (; tile < ntiles; tile += tstride) {
     float4 v[2 * KT];
 #pragma unroll
     for (int i = 0; i < 2 * KT; ++i) v[i] = vn[i];
+    float4 rv[16];
+    load_res(tile, rv);             // this tile's residual, needed only in the epilogues
     load_rows(tile + tstride, vn);  // the next tile's rows in flight during this one's MFMAs
     // row scale: the exact row maximum (this lane's half row + its partner's) in [2^13, 2^14)
     float mx = 0.f;
@@ -134,14 +149,6 @@ __global__ void __launch_bounds__(NRW * 64, 2)
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb) {
       if (cb >= ncb) break;
-      // residual of this lane's row / column block, loaded ahead of the MFMAs
-      float4 rv[4];
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int n = n0 + cb * 32 + 8 * g + 4 * h;
-        rv[g] = R ? bload4(rR, (mok && n < N) ? ((unsigned)m * (unsigned)ldr + (unsigned)n) * 4u : OOB)
-                  : make_float4(0.f, 0.f, 0.f, 0.f);
-      }
       floatx16 acc;
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc[i] = 0.f;
@@ -165,10 +172,10 @@ __global__ void __launch_bounds__(NRW * 64, 2)
           if (act == ACT_GELU && n + q < act_ncols) t = gelu_erf(t);
           y[q] = t;
         }
-        y[0] += rv[g].x;
-        y[1] += rv[g].y;
-        y[2] += rv[g].z;
-        y[3] += rv[g].w;
+        y[0] += rv[4 * cb + g].x;
+        y[1] += rv[4 * cb + g].y;
+        y[2] += rv[4 * cb + g].z;
+        y[3] += rv[4 * cb + g].w;
         const bool ok = mok && n < N;
         if (y_amax && ok)
           ymax = fmaxf(ymax, fmaxf(fmaxf(fabsf(y[0]), fabsf(y[1])), fmaxf(fabsf(y[2]), fabsf(y[3]))));
