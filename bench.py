@@ -55,10 +55,9 @@ F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense fp16 / bf16 MFMA (no
 # fp32-equivalent ceiling is the dense fp16 peak / 3.
 SPLIT_PEAK_TFLOPS = round(F16_MFMA_PEAK_TFLOPS / 3, 1)
 HBM_PEAK_GBS = 8000.0
-# kernel-name prefixes of the dominant family: the GEMMs (incl. the W-resident narrow-K kernel, gemm_narrow.hip),
-# the fused Block MLP, the fused SubM conv + CPE LayerNorm (subm_fused.hip) and the fused output heads (heads.hip)
-GEMM_FAMILY = ("gemm_kernel", "gemm_narrow_kernel", "wgrad_kernel", "mlp_kernel", "subm_cpe_ln_kernel",
-               "heads_kernel")
+# kernel-name prefixes of the dominant family: the GEMMs, the fused Block MLP, the fused SubM conv + CPE
+# LayerNorm (subm_fused.hip) and the fused output heads (heads.hip)
+GEMM_FAMILY = ("gemm_kernel", "wgrad_kernel", "mlp_kernel", "subm_cpe_ln_kernel", "heads_kernel")
 
 
 def in_family(kernel_name: str) -> bool:
@@ -273,8 +272,7 @@ def roofline_probe(unit_fn, passes=3):
         "frac_of_fp32_mfma_peak": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
         "kernel": ("GEMM family (gemm_kernel: sfx_linear / sfx_subm_conv / training data-gradient GEMMs, fp32 "
                    "operands as power-of-two-scaled fp16x2 terms, 3 x v_mfma_f32_32x32x16_f16 per block, fp32 "
-                   "accumulation; gemm_narrow_kernel, the dense K <= 128 linears on LDS-resident weights; "
-                   "wgrad_kernel; mlp_kernel, the fused LN2 + fc1 + GELU + fc2 Block tail; "
+                   "accumulation; wgrad_kernel; mlp_kernel, the fused LN2 + fc1 + GELU + fc2 Block tail; "
                    "subm_cpe_ln_kernel, the SubM conv with its pair products summed on chip + the CPE LayerNorm "
                    "tail (C <= 128); heads_kernel, the six output MLPs; and cpe_residual_ln4_kernel<.., true>, the "
                    "C >= 256 SubM conv's per-row sum of its stored pair products), "
@@ -286,8 +284,7 @@ def roofline_probe(unit_fn, passes=3):
                        "tflops": round(top[3] / (top[0] * 1e-3) / 1e12, 2)},
         "pure_gemm": {"launches": len(pure), "ms_per_unit": round(pms, 3), "gflop_per_unit": round(pfl / 1e9, 1),
                       "achieved": round(pure_tf, 2), "frac": round(pure_tf / SPLIT_PEAK_TFLOPS, 4),
-                      "kernels": "gemm_kernel + gemm_narrow_kernel + wgrad_kernel launches (the rounds 1-2 family "
-                                 "definition; the narrow kernel serves launches gemm_kernel ran before round 4)"},
+                      "kernels": "gemm_kernel + wgrad_kernel launches only (the rounds 1-2 family definition)"},
     }
 
 

@@ -1410,8 +1410,7 @@ int sfx_linear(int M, int N, int K, const float* A, long long lda, const int* ga
     SFX_REQUIRE(groups == 1 || group_stride_W == (long long)N * K, "sfx_linear: w_split needs contiguous groups");
     a.Wsp = w_split; a.ldws = K; a.winv = w_inv; a.gWinv = N;
   }
-  if (!(vec && split_mode(K) == 2 && gemm_narrow(a, groups, vec, sfx::as_stream(stream))))
-    dispatch(a, groups, vec, sfx::as_stream(stream));
+  dispatch(a, groups, vec, sfx::as_stream(stream));
   return sfx::check_launch("sfx_linear");
 }
 

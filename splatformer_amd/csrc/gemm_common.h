@@ -179,7 +179,4 @@ using sfx::split2h;  // fp32 -> two fp16 terms of the scaled value (common.h)
 
 enum Mode { MODE_DENSE = 0, MODE_GATHER1 = 1, MODE_GATHERS = 2, MODE_PAIR = 3 };
 
-// dense K <= 128 linears on the W-resident kernel (gemm_narrow.hip); false: not applicable, nothing launched
-bool gemm_narrow(const GemmArgs& a, int groups, bool vec, hipStream_t st);
-
 }  // namespace sfxg

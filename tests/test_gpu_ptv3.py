@@ -52,9 +52,9 @@ def _slot_value(device, slot):
 @pytest.mark.parametrize("M,N,K", [(4097, 96, 96), (1, 128, 128), (31, 100, 64), (3001, 288, 96), (2500, 384, 128),
                                    (777, 64, 128)])
 def test_linear_narrow_cases(device, M, N, K):
-    """The W-resident narrow-K path (gemm_narrow.hip, dense K in {64, 96, 128}): bias, GELU on the first columns
-    only, residual (also in place), max |Y| published to a slot, strided input / output, ragged M and N, rows of
-    very different magnitudes -- each row within 2x (+1e-7) of torch's fp32 CPU error against fp64."""
+    """The refine's narrow dense linears (K in {64, 96, 128}): bias, GELU on the first columns only, residual
+    (also in place), max |Y| published to a slot, strided input / output, ragged M and N, rows of very different
+    magnitudes -- each row within 2x (+1e-7) of torch's fp32 CPU error against fp64."""
     g = torch.Generator().manual_seed(M * 7 + N + K)
     xb = torch.randn(M, K + 8, generator=g)
     xb[::3] *= 1e4

@@ -28,7 +28,7 @@ PASSES = {
             "GRBM_GUI_ACTIVE"],
 }
 FAMILIES = [  # (family, kernel-name regex) -- first match wins
-    ("gemm", r"^gemm_kernel|^gemm_narrow_kernel|^wgrad_kernel"),
+    ("gemm", r"^gemm_kernel|^wgrad_kernel"),
     ("mlp (fused Block MLP)", r"^mlp_kernel"),
     ("subm pair-sum LayerNorm", r"^cpe_residual_ln4_kernel<\d+, \d+, true>"),
     ("fused subm conv + CPE LN", r"^subm_cpe_ln_kernel"),
