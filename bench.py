@@ -75,8 +75,8 @@ DEPTH1 = dict(enc_depths=(1, 1, 1, 1, 1), dec_depths=(1, 1, 1, 1))
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", choices=sorted(DEFAULTS), default="B")
     ap.add_argument("--n", type=int, default=None)
     ap.add_argument("--res", type=str, default=None, help="W or WxH")
