@@ -102,32 +102,26 @@ __device__ __forceinline__ int row_exp(float m) {
   return e > 126 ? 126 : (e < -126 ? -126 : e);
 }
 
-// erf GELU (torch approximate='none') with a branch-free erf: the two argument ranges of the device library's
-// erff (|x| < 1: odd polynomial; |x| >= 1: 1 - exp(-(|x| + |x| P(|x|))), same coefficients) are both evaluated
-// and selected, so the compiler can interleave the epilogue with the MFMA stream (the library form branches per
-// lane and splits the loop into ~30 basic blocks); exp by v_exp_f32 (__expf: its error, a few ulp of
-// exp(-p) <= e^-1, moves erf by < 1e-7 of its value -- the fp32 GEMMs' own rounding level), ~30 % fewer VALU
-// than expf's range reduction (the fused MLP's GELU is its VALU bottleneck, profiles/r04_mlp_gelu_variants.txt).
-__device__ __forceinline__ float erf_nb(float x) {
-  const float ax = fabsf(x);
-  const float t = ax * ax;
-  float p1 = __builtin_fmaf(t, -0x1.268bc2p-11f, 0x1.420828p-8f);
-  p1 = __builtin_fmaf(t, p1, -0x1.b5937p-6f);
-  p1 = __builtin_fmaf(t, p1, 0x1.ce077cp-4f);
-  p1 = __builtin_fmaf(t, p1, -0x1.81266p-2f);
-  p1 = __builtin_fmaf(t, p1, 0x1.06eba0p-3f);
-  const float r1 = __builtin_fmaf(ax, p1, ax);
-  float p2 = __builtin_fmaf(ax, 0x1.1d3156p-16f, -0x1.8d129p-12f);
-  p2 = __builtin_fmaf(ax, p2, 0x1.f9a6d2p-9f);
-  p2 = __builtin_fmaf(ax, p2, -0x1.8c3164p-6f);
-  p2 = __builtin_fmaf(ax, p2, 0x1.b4e9c8p-4f);
-  p2 = __builtin_fmaf(ax, p2, 0x1.4515fap-1f);
-  p2 = __builtin_fmaf(ax, p2, 0x1.078e50p-3f);
-  p2 = __builtin_fmaf(ax, p2, ax);
-  const float r2 = 1.0f - __expf(-p2);
-  return __builtin_copysignf(ax < 1.0f ? r1 : r2, x);
+// erf GELU (torch approximate='none'), GELU(x) = x Phi(x), with Phi from ONE fitted exponent: the upper normal tail
+// is erfc(t / sqrt 2) = 2^-h(t) with h(t) = t Q(t), Q a degree-7 polynomial (weighted least squares on [0, 5.65]
+// against scipy's erfc in fp64, weights = the tail itself, so the fit is tight where it matters for Phi), t = |x|
+// clamped to 5.65 (Phi(5.65) = 1 - 8e-9 rounds to 1).  Phi = 1 - tail / 2 (x >= 0) or tail / 2: max |Phi - Phi_exact|
+// = 6.2e-8 over [-8, 8] in fp32 evaluation, the rounding level of Phi itself.  Branch-free and 16 VALU (one
+// v_exp_f32) against ~25 for the two-range erf it replaced -- GELU is the fused MLP's VALU bottleneck
+// (profiles/r04_mlp_gelu_variants.txt: the MLP ran 1.3-1.5x faster with GELU removed).
+__device__ __forceinline__ float gelu_erf(float x) {
+  const float t = fminf(fabsf(x), 5.65f);
+  float q = 2.79405867e-06f;
+  q = __builtin_fmaf(q, t, -3.89084234e-05f);
+  q = __builtin_fmaf(q, t, 0.000184072458f);
+  q = __builtin_fmaf(q, t, 0.000141672252f);
+  q = __builtin_fmaf(q, t, -0.00706906663f);
+  q = __builtin_fmaf(q, t, 0.0524996631f);
+  q = __builtin_fmaf(q, t, 0.459207207f);
+  q = __builtin_fmaf(q, t, 1.15110528f);
+  const float half_tail = 0.5f * __builtin_amdgcn_exp2f(-(t * q));
+  return x * (x >= 0.f ? 1.f - half_tail : half_tail);
 }
-__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erf_nb(x * 0.70710678118654752f)); }
 // d/dx of the erf GELU (torch GeluBackward, approximate='none')
 __device__ __forceinline__ float gelu_erf_grad(float x) {
   const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
