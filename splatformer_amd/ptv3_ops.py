@@ -287,10 +287,10 @@ def grouped_linear(x: Tensor, weight: Tensor, bias: Tensor, groups: int, *, act:
 # ---- fused Block MLP tail (csrc/mlp.hip) ---------------------------------------------------------------------
 MLP_FUSED = os.environ.get("SFX_MLP_FUSED", "1") != "0"  # SFX_MLP_FUSED=0: LayerNorm + two GEMM launches
 MLP_CHANNELS = (64, 96, 128, 256)  # what sfx_block_mlp serves
-# where the eval forward uses it: measured faster than LayerNorm + two GEMMs for C <= 128 (1.1-1.5x,
-# profiles/r03_mlp_bench.txt); at C = 256 it is 0.92x, so those Blocks keep the three launches
-# (SFX_MLP_CHANNELS=64,96,128,256 overrides)
-MLP_FUSED_CHANNELS = tuple(int(c) for c in os.environ.get("SFX_MLP_CHANNELS", "64,96,128").split(",") if c)
+# where the eval forward uses it: every channel count it serves -- with the round-4 GELU it is 1.12-1.68x faster
+# than LayerNorm + two GEMMs, C = 256 included (230.9 vs 259.2 us; round 3: 0.92x there, profiles/r03_mlp_bench.txt);
+# SFX_MLP_CHANNELS=64,96,128 restores round 3's choice
+MLP_FUSED_CHANNELS = tuple(int(c) for c in os.environ.get("SFX_MLP_CHANNELS", "64,96,128,256").split(",") if c)
 
 
 def mlp_pack(ln2, fc1, fc2) -> Tuple[Tensor, Tensor]:
