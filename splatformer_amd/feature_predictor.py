@@ -97,7 +97,10 @@ class FeaturePredictor(nn.Module):
 
     # ---- packed head weights (rebuilt only when a parameter changes) --------------
     def _packed_heads(self):
-        params = [p for f in self.output_features for p in self.features_outputhead[f].parameters()]
+        params = self.__dict__.get("_head_params")
+        if params is None:  # (the heads' module structure is fixed; the list is built once)
+            params = [p for f in self.output_features for p in self.features_outputhead[f].parameters()]
+            self.__dict__["_head_params"] = params
         key = tuple((p.data_ptr(), p._version) for p in params)
         if self._pack_cache is not None and self._pack_cache[0] == key:
             return self._pack_cache[1]
@@ -138,6 +141,12 @@ class FeaturePredictor(nn.Module):
         cin = self.gs_features_dim
         cb = self.backbone.output_dim
         ld = (cb + cin + 3) // 4 * 4
+        n_tanh = self.ch["means"] if self.output_features[0] == "means" else 0
+        fused_heads = ops.heads_fused_ok(len(self.output_features), self.nlayer, self.width, self.head_in,
+                                         sum(self.ch[f] for f in self.output_features))
+        # the heads' pack check (a version key over every head parameter) runs here, while the GPU still
+        # renders the previous scene, not between the backbone's last launch and the heads' (a host gap)
+        heads_pack = self._fused_heads() if fused_heads else None
         h0 = torch.zeros(n, ld, device=dev, dtype=torch.float32)
         feat = h0[:, cb:cb + cin]
         grid = torch.empty(n, 3, device=dev, dtype=torch.int32)
@@ -155,10 +164,8 @@ class FeaturePredictor(nn.Module):
             c, f, g, mapper = downsample_for_backbone(method, self.additional_info, means, feat, grid)
             y = self.backbone({"coord": c, "grid_coord": g, "offset": [c.shape[0]], "feat": f}, perms=perms).feat
             h0[:, :cb] = mapper(y)
-        n_tanh = self.ch["means"] if self.output_features[0] == "means" else 0
-        if ops.heads_fused_ok(len(self.output_features), self.nlayer, self.width, self.head_in,
-                              sum(self.ch[f] for f in self.output_features)):
-            st, pr, ocols, out_dim = self._fused_heads()
+        if heads_pack is not None:
+            st, pr, ocols, out_dim = heads_pack
             # all six heads + tanh + residual in one launch (csrc/heads.hip): no [N, 768] hidden in HBM
             return ops.heads(h0, self.head_in, cb, out_dim, n_tanh, ocols, st, pr)
         w1, b1, mids, wl, bl, out_dim = self._packed_heads()
