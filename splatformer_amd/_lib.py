@@ -119,6 +119,10 @@ class HostRead:
             self._v = self._h.tolist()
         return self._v
 
+    def ready(self) -> bool:
+        """Whether get() would return without waiting."""
+        return self._v is not None or self._ev.query()
+
 
 def require_gpu(t: torch.Tensor | None = None) -> None:
     if not torch.cuda.is_available():
@@ -140,7 +144,14 @@ def ptr(t: torch.Tensor | None, dtype: torch.dtype | None = None) -> int | None:
     return t.data_ptr()
 
 
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
 def stream() -> int:
+    """The current HIP stream of the current device (torch's), as a pointer.  Called once per launch: the raw
+    accessor costs ~0.3 us against ~8 us for torch.cuda.current_stream()'s Python wrapper (tools/host_profile.py)."""
+    if _raw_stream is not None and torch.cuda.is_initialized():
+        return _raw_stream(torch._C._cuda_getDevice())
     return torch.cuda.current_stream().cuda_stream
 
 

@@ -435,6 +435,7 @@ class PointTransformerV3(nn.Module):
             depth, cum = depth - pd, cum + pd
             shifts.append(3 * cum)
         counts_rd = ops.pool_counts_begin(point.codes_phys, point.order_phys, shifts) if POOL_COUNTS_UPFRONT else None
+        self.check_deferred(wait=True)  # the previous forward's pooling checks (long complete by now)
         deferred: list = []
         k = 1
         for s in range(self.num_stages):
@@ -458,9 +459,22 @@ class PointTransformerV3(nn.Module):
                     conv_in = point.pop("stale_conv_feat", None)
                     last = di == len(dec_names) - 1 and ci == len(children) - 1
                     point = mod.run(point, conv_in=conv_in, out=out if last else None)
-        for rd, m in deferred:  # (the whole refine is enqueued: this wait starves nothing)
-            ops.check_pool_runs(rd.get(), m)
+        # the pooling run-count checks whose reads have landed run now; the rest at the next forward (or
+        # check_deferred()): waiting here would hold back the launches the caller enqueues after the backbone
+        # (the heads, the render) until the whole backbone has run -- a drained queue at every refine
+        self._deferred = deferred
+        self.check_deferred(wait=False)
         return point
+
+    def check_deferred(self, wait: bool = True) -> None:
+        """Validate the pooled run counts read back asynchronously by forward (pool_geometry_end's `deferred`)."""
+        pending = []
+        for rd, m in self.__dict__.get("_deferred", []):
+            if wait or rd.ready():
+                ops.check_pool_runs(rd.get(), m)
+            else:
+                pending.append((rd, m))
+        self._deferred = pending
 
 
 class PointTransformerV3Model(nn.Module):
