@@ -449,12 +449,20 @@ int sfx_block_mlp(int M, int C, const float* x, long long ldx, const float* stre
               "sfx_block_mlp: operand exceeds the 2 GiB buffer-descriptor range");
   SFX_REQUIRE(x != y, "sfx_block_mlp: in-place output is not supported");
   hipStream_t st = sfx::as_stream(stream_);
+  static int waves = -1;  // SFX_MLP_WAVES=4: 128-point workgroups for C <= 128 (tuning experiment)
+  if (waves < 0) {
+    const char* e = getenv("SFX_MLP_WAVES");
+    waves = (e && *e) ? atoi(e) : 8;
+  }
   switch (C) {
     // (waves, ring phases): 8 waves = 256 points per workgroup, 2 workgroups per CU for C <= 128 (64 KB ring);
     // C = 256 needs 4 waves (its 128 point columns of LN2 fragments + output accumulators fill 512 registers)
-    case 64: return run_impl<64, 8, 4>(M, x, ldx, stream, params, eps, y, ldy, st);
-    case 96: return run_impl<96, 8, 4>(M, x, ldx, stream, params, eps, y, ldy, st);
-    case 128: return run_impl<128, 8, 4>(M, x, ldx, stream, params, eps, y, ldy, st);
+    case 64: return waves == 4 ? run_impl<64, 4, 4>(M, x, ldx, stream, params, eps, y, ldy, st)
+                               : run_impl<64, 8, 4>(M, x, ldx, stream, params, eps, y, ldy, st);
+    case 96: return waves == 4 ? run_impl<96, 4, 4>(M, x, ldx, stream, params, eps, y, ldy, st)
+                               : run_impl<96, 8, 4>(M, x, ldx, stream, params, eps, y, ldy, st);
+    case 128: return waves == 4 ? run_impl<128, 4, 4>(M, x, ldx, stream, params, eps, y, ldy, st)
+                                : run_impl<128, 8, 4>(M, x, ldx, stream, params, eps, y, ldy, st);
     default: return run_impl<256, 4, 8>(M, x, ldx, stream, params, eps, y, ldy, st);
   }
 }
