@@ -16,14 +16,14 @@
 //     at most, so no chunk overflows fp16 and no running rescale is needed);
 //   * W1 rows / W2 rows: their own maxima in [2^14, 2^15) (pre-split once per weight version, sfx_mlp_pack).
 //
-// Work decomposition: one workgroup = 64 points, 4 waves as 2 (point halves pm) x 2 (unit halves cn).  The hidden
-// layer is processed in chunks of 64 units.  Computed transposed (points on the lanes): per chunk, wave (pm, cn)
-// forms hid^T[32 units (cn), 32 points (pm)] = W1_chunk(cn) . LN2(X2)^T (A = W1 rows from LDS, B = the LN2 image
-// in LDS), applies bias + GELU + split in registers, and feeds the accumulator registers straight back as the
-// B operand of fc2 (a 32x32 accumulator's registers 8s..8s+7 are the k-step s fragment of A.X, the k order
-// permuted: cdna_hip_programming.md §3) -- the hidden never touches LDS either.  fc2^T: acc2^T[C channels,
-// 32 points] += W2[:, the wave's 32 units] . hid^T; the two unit halves' partial sums of a point half are added
-// once per tile through LDS.
+// Work decomposition (mlp_kernel below): one workgroup = WAVES x 32 points, wave w owns 32 points and computes
+// every hidden unit and every output channel for them.  The hidden layer is processed in chunks of 64 units.
+// Computed transposed (points on the lanes): per chunk, the wave forms hid^T[2 x 32 units, 32 points] =
+// W1_chunk . LN2(X2)^T (A = W1 rows from the LDS ring, B = the wave's LN2 fragments held in registers), applies
+// bias + GELU + split in registers, and feeds the accumulator registers straight back as the B operand of fc2 (a
+// 32x32 accumulator's registers 8s..8s+7 are the k-step s fragment of A.X, the k order permuted:
+// cdna_hip_programming.md §3) -- the hidden never touches LDS either.  fc2^T: acc2^T[C channels, 32 points] +=
+// W2[:, the chunk's 64 units] . hid^T, kept in registers for the whole tile.
 //
 // Weights stream through an LDS ring by LDS-DMA (global_load_lds_dwordx4): sfx_mlp_pack lays W1 / W2 out as
 // 8 KB slabs in exactly the swizzled order the fragments are read in (so a slab is a plain contiguous copy) and in
