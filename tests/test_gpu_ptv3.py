@@ -86,6 +86,22 @@ def test_linear_narrow_cases(device, M, N, K):
     assert rel_l2(r2.cpu(), ref2) <= 2 * rel_l2((x @ w.T + b + res), ref2) + 1e-7
 
 
+def test_gelu_fitted_tail_accuracy(device):
+    """The GEMM epilogue's GELU (gemm_common.h gelu_erf: Phi from one fitted tail exponent, shared by the fused
+    MLP) against fp64 erf-GELU over [-12, 12] and at 0 / +-tiny: |dGELU| <= 2e-7 max(1, |x|) -- the fit's 6e-8 on Phi
+    plus the fp16x2 identity product's 2^-22."""
+    x = torch.linspace(-12.0, 12.0, 4096 * 64, dtype=torch.float64)
+    x[:8] = torch.tensor([0.0, 1e-30, -1e-30, 1e-8, -1e-8, 5.65, -5.65, 0.5])
+    x32 = x.float().reshape(4096, 64)
+    eye = torch.eye(64)
+    y = ops.linear(x32.to(device), eye.to(device), None, act=ops.ACT_GELU).cpu().double().flatten()
+    xd = x32.double().flatten()
+    ref = 0.5 * xd * (1.0 + torch.erf(xd / 2 ** 0.5))
+    err = (y - ref).abs() / xd.abs().clamp_min(1.0)
+    assert float(err.max()) <= 2e-7, (float(err.max()), float(xd[int(err.argmax())]))
+    assert float(y[0]) == 0.0 and torch.isfinite(y).all()
+
+
 @pytest.mark.parametrize("scale", [1.0, 1e-30, 1e30])
 def test_linear_split_precision_is_fp32(device, scale):
     """The fp16x2 split GEMM (default for K >= 64: a power-of-two scale per operand row -- A' rows chosen online
