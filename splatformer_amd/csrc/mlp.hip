@@ -82,11 +82,17 @@ __device__ __forceinline__ void wait_vm_lgkm() {
 // lives in its registers as the fc1 B fragments (lane (r, h) holds point r's channels 16 t + 8 h .. + 7 for every
 // k-step t -- half a row per lane, LayerNorm statistics completed with the partner lane r + 32), and the weights
 // are read from the LDS ring by all WAVES waves (WAVES-fold reuse per DMA'd byte).
-template <int C, int WAVES, int RING>
+// HS (hidden split): a PAIR of waves owns 32 points, wave cn = wid & 1 taking the 32-unit half cn of every 64-unit
+// hidden chunk (half the fc1 / GELU / fc2 work and LDS reads per wave); the two partial fc2 sums meet once through
+// LDS at the end (cn 0 + cn 1, a fixed order).  Twice the waves per point: at C = 256 (37759 points, one 512-register
+// wave per SIMD) 1180 whole-tile waves over 1024 SIMDs take two full rounds, 2360 half-work waves take three half
+// rounds.
+template <int C, int WAVES, int RING, bool HS = false>
 __global__ void __launch_bounds__(WAVES * 64, (WAVES == 4 && C > 128) ? 1 : 2)
     mlp_kernel(int M, const float* __restrict__ X, long long ldx, const float* __restrict__ stream,
                const float* __restrict__ par, float eps, float* __restrict__ Y, long long ldy, int rot) {
   using G = MlpGeom<C>;
+  constexpr int PTS = HS ? WAVES * 16 : WAVES * 32;  // points per workgroup
   constexpr int NB = G::NB, NP = G::NP, PPC = G::PPC, NT = C / 16;  // NT: fc1 k-steps
   constexpr int NTH = WAVES * 64;
   constexpr int PIECES = 16 / WAVES;  // 1 KB LDS-DMA pieces per wave per phase
@@ -98,7 +104,9 @@ __global__ void __launch_bounds__(WAVES * 64, (WAVES == 4 && C > 128) ? 1 : 2)
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int h = lane >> 5, r32 = lane & 31;
-  const int prow = (int)blockIdx.x * (WAVES * 32) + wid * 32 + r32;  // this lane's point
+  const int cn = HS ? (wid & 1) : 0;        // HS: this wave's hidden half
+  const int pg = HS ? (wid >> 1) : wid;      // this wave's 32-point group
+  const int prow = (int)blockIdx.x * PTS + pg * 32 + r32;  // this lane's point
   const bool pok = prow < M;
 
   // ---- weight stream: logical phase q -> ring slot q % RING; rot: each workgroup starts at its own hidden
@@ -200,7 +208,8 @@ __global__ void __launch_bounds__(WAVES * 64, (WAVES == 4 && C > 128) ? 1 : 2)
     for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
-        const char* half = base + cb * 4096;
+        if (HS && cb != 0) break;              // HS: the own half only, in slot 0
+        const char* half = base + (HS ? cn : cb) * 4096;
         const int o = slab_off(r32, 16 * t + 8 * h);
         fa[cb][t][0] = *reinterpret_cast<const f16x8*>(half + o);
         fa[cb][t][1] = *reinterpret_cast<const f16x8*>(half + 2048 + o);
@@ -208,16 +217,18 @@ __global__ void __launch_bounds__(WAVES * 64, (WAVES == 4 && C > 128) ? 1 : 2)
   };
   // one slab: sl < NB -> fc1 slab sl (input channels 32 sl .. +32, both 32-unit blocks), else fc2 slab sl - NB
   auto slab = [&](const f16x8 (&fa)[2][2][2], int sl, int j) {
+    constexpr int NCB = HS ? 1 : 2;  // unit blocks of a chunk this wave computes
     if (sl < NB) {
 #pragma unroll
-      for (int cb = 0; cb < 2; ++cb)
+      for (int cb = 0; cb < NCB; ++cb)
 #pragma unroll
         for (int t = 0; t < 2; ++t)
           acc1[cb] = mfma3(fa[cb][t][0], fa[cb][t][1], hb[2 * sl + t][0], hb[2 * sl + t][1], acc1[cb]);
       if (sl == NB - 1) {  // hidden chunk complete: bias, GELU, split -> fc2 B fragments (registers)
 #pragma unroll
-        for (int cb = 0; cb < 2; ++cb) {
-          const float4* pp = reinterpret_cast<const float4*>(s_par + 2 * C + 2 * fc1_par_index(j, cb, h, 0));
+        for (int cb = 0; cb < NCB; ++cb) {
+          const float4* pp =
+              reinterpret_cast<const float4*>(s_par + 2 * C + 2 * fc1_par_index(j, HS ? cn : cb, h, 0));
           float g[16];
 #pragma unroll
           for (int i2 = 0; i2 < 8; ++i2) {
@@ -243,7 +254,7 @@ __global__ void __launch_bounds__(WAVES * 64, (WAVES == 4 && C > 128) ? 1 : 2)
     } else {
       const int b = sl - NB;
 #pragma unroll
-      for (int cb = 0; cb < 2; ++cb)
+      for (int cb = 0; cb < NCB; ++cb)
 #pragma unroll
         for (int st = 0; st < 2; ++st)
           acc2[b] = mfma3(fa[cb][st][0], fa[cb][st][1], hf[cb][st][0], hf[cb][st][1], acc2[b]);
@@ -254,7 +265,7 @@ __global__ void __launch_bounds__(WAVES * 64, (WAVES == 4 && C > 128) ? 1 : 2)
   for (int jl = 0; jl < G::NCH; ++jl) {
     const int j = jl + j0 - (jl + j0 >= G::NCH ? G::NCH : 0);  // the hidden chunk of this logical chunk
 #pragma unroll
-    for (int cb = 0; cb < 2; ++cb)
+    for (int cb = 0; cb < (HS ? 1 : 2); ++cb)
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc1[cb][i] = 0.f;
 #pragma unroll
@@ -273,6 +284,32 @@ __global__ void __launch_bounds__(WAVES * 64, (WAVES == 4 && C > 128) ? 1 : 2)
     }
   }
 
+  if constexpr (HS) {  // the cn = 1 wave's partial fc2 sums -> LDS (the drained ring) -> added by its cn = 0 partner
+    static_assert((WAVES / 2) * 64 * NB * 16 * 4 <= RING * PHASE_BYTES, "HS exchange fits the ring");
+    __builtin_amdgcn_s_barrier();  // every wave's last ring reads are done (the tail waited for every DMA)
+    asm volatile("" ::: "memory");
+    float4* xch = reinterpret_cast<float4*>(lds) + (size_t)pg * 64 * NB * 4;
+    if (cn == 1) {
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          xch[(b * 4 + q) * 64 + lane] = make_float4(acc2[b][4 * q], acc2[b][4 * q + 1], acc2[b][4 * q + 2],
+                                                     acc2[b][4 * q + 3]);
+    }
+    __syncthreads();
+    if (cn == 1) return;
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 o = xch[(b * 4 + q) * 64 + lane];
+        acc2[b][4 * q] += o.x;
+        acc2[b][4 * q + 1] += o.y;
+        acc2[b][4 * q + 2] += o.z;
+        acc2[b][4 * q + 3] += o.w;
+      }
+  }
   // ---- epilogue: Y = X2 + acc2 / (t s_c) + b2, 16-byte stores of 4 consecutive channels ----
   const __amdgpu_buffer_rsrc_t rY = rsrc_ext(Y, (unsigned)M * (unsigned)ldy * 4u);
   const unsigned yr = (unsigned)prow * (unsigned)ldy;
@@ -401,7 +438,7 @@ int pack_impl(const float* w1, const float* b1, const float* w2, const float* b2
   return sfx::check_launch("sfx_mlp_pack");
 }
 
-template <int C, int WAVES, int RING>
+template <int C, int WAVES, int RING, bool HS = false>
 int run_impl(int M, const float* x, long long ldx, const float* stream, const float* par, float eps, float* y,
              long long ldy, hipStream_t st) {
   static int rot = -1;
@@ -409,8 +446,8 @@ int run_impl(int M, const float* x, long long ldx, const float* stream, const fl
     const char* e = getenv("SFX_MLP_ROT");
     rot = (e && *e) ? (atoi(e) != 0) : 1;
   }
-  mlp_kernel<C, WAVES, RING><<<sfx::ceil_div(M, WAVES * 32), WAVES * 64, 0, st>>>(M, x, ldx, stream, par, eps, y, ldy,
-                                                                                 rot);
+  mlp_kernel<C, WAVES, RING, HS><<<sfx::ceil_div(M, HS ? WAVES * 16 : WAVES * 32), WAVES * 64, 0, st>>>(
+      M, x, ldx, stream, par, eps, y, ldy, rot);
   return sfx::check_launch("sfx_block_mlp");
 }
 
@@ -449,10 +486,12 @@ int sfx_block_mlp(int M, int C, const float* x, long long ldx, const float* stre
               "sfx_block_mlp: operand exceeds the 2 GiB buffer-descriptor range");
   SFX_REQUIRE(x != y, "sfx_block_mlp: in-place output is not supported");
   hipStream_t st = sfx::as_stream(stream_);
-  static int waves = -1;  // SFX_MLP_WAVES=4: 128-point workgroups for C <= 128 (tuning experiment)
+  static int waves = -1, hs = -1;  // SFX_MLP_WAVES=4: 128-point workgroups for C <= 128 (tuning experiment)
   if (waves < 0) {
     const char* e = getenv("SFX_MLP_WAVES");
     waves = (e && *e) ? atoi(e) : 8;
+    const char* f = getenv("SFX_MLP_HS");  // hidden split at C = 256 (1, default) or whole tiles per wave (0)
+    hs = (f && *f) ? (atoi(f) != 0) : 1;
   }
   switch (C) {
     // (waves, ring phases): 8 waves = 256 points per workgroup, 2 workgroups per CU for C <= 128 (64 KB ring);
@@ -463,7 +502,8 @@ int sfx_block_mlp(int M, int C, const float* x, long long ldx, const float* stre
                                : run_impl<96, 8, 4>(M, x, ldx, stream, params, eps, y, ldy, st);
     case 128: return waves == 4 ? run_impl<128, 4, 4>(M, x, ldx, stream, params, eps, y, ldy, st)
                                 : run_impl<128, 8, 4>(M, x, ldx, stream, params, eps, y, ldy, st);
-    default: return run_impl<256, 4, 8>(M, x, ldx, stream, params, eps, y, ldy, st);
+    default: return hs ? run_impl<256, 4, 8, true>(M, x, ldx, stream, params, eps, y, ldy, st)
+                       : run_impl<256, 4, 8>(M, x, ldx, stream, params, eps, y, ldy, st);
   }
 }
 
