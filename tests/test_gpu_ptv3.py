@@ -88,8 +88,8 @@ def test_linear_narrow_cases(device, M, N, K):
 
 def test_gelu_fitted_tail_accuracy(device):
     """The GEMM epilogue's GELU (gemm_common.h gelu_erf: Phi from one fitted tail exponent, shared by the fused
-    MLP) against fp64 erf-GELU over [-12, 12] and at 0 / +-tiny: |dGELU| <= 2e-7 max(1, |x|) -- the fit's 6e-8 on Phi
-    plus the fp16x2 identity product's 2^-22."""
+    MLP) against fp64 erf-GELU over [-12, 12] and at 0 / +-tiny: |dGELU| <= 4e-7 max(1, |x|) -- the fit's 6e-8 on Phi
+    plus the fp16x2 split of the identity product's input (x = h + l to 2^-22 = 2.4e-7 relative)."""
     x = torch.linspace(-12.0, 12.0, 4096 * 64, dtype=torch.float64)
     x[:8] = torch.tensor([0.0, 1e-30, -1e-30, 1e-8, -1e-8, 5.65, -5.65, 0.5])
     x32 = x.float().reshape(4096, 64)
@@ -98,7 +98,7 @@ def test_gelu_fitted_tail_accuracy(device):
     xd = x32.double().flatten()
     ref = 0.5 * xd * (1.0 + torch.erf(xd / 2 ** 0.5))
     err = (y - ref).abs() / xd.abs().clamp_min(1.0)
-    assert float(err.max()) <= 2e-7, (float(err.max()), float(xd[int(err.argmax())]))
+    assert float(err.max()) <= 4e-7, (float(err.max()), float(xd[int(err.argmax())]))
     assert float(y[0]) == 0.0 and torch.isfinite(y).all()
 
 
