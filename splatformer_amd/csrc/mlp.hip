@@ -486,16 +486,18 @@ int sfx_block_mlp(int M, int C, const float* x, long long ldx, const float* stre
               "sfx_block_mlp: operand exceeds the 2 GiB buffer-descriptor range");
   SFX_REQUIRE(x != y, "sfx_block_mlp: in-place output is not supported");
   hipStream_t st = sfx::as_stream(stream_);
-  static int waves = -1, hs = -1;  // SFX_MLP_WAVES=4: 128-point workgroups for C <= 128 (tuning experiment)
+  // C <= 128: 4-wave (128-point) workgroups, two per CU -- measured 1.0-1.2x faster than one 8-wave workgroup
+  // (profiles/r04_mlp_waves_hs.txt); SFX_MLP_WAVES=8 restores the 256-point workgroups
+  static int waves = -1, hs = -1;
   if (waves < 0) {
     const char* e = getenv("SFX_MLP_WAVES");
-    waves = (e && *e) ? atoi(e) : 8;
+    waves = (e && *e) ? atoi(e) : 4;
     const char* f = getenv("SFX_MLP_HS");  // hidden split at C = 256 (1, default) or whole tiles per wave (0)
     hs = (f && *f) ? (atoi(f) != 0) : 1;
   }
   switch (C) {
-    // (waves, ring phases): 8 waves = 256 points per workgroup, 2 workgroups per CU for C <= 128 (64 KB ring);
-    // C = 256 needs 4 waves (its 128 point columns of LN2 fragments + output accumulators fill 512 registers)
+    // (waves, ring phases): 4 waves = 128 points per workgroup, 2 workgroups per CU for C <= 128 (64 KB ring);
+    // C = 256 runs 4 waves as 2 hidden-split pairs (its LN2 fragments + output accumulators fill 512 registers)
     case 64: return waves == 4 ? run_impl<64, 4, 4>(M, x, ldx, stream, params, eps, y, ldy, st)
                                : run_impl<64, 8, 4>(M, x, ldx, stream, params, eps, y, ldy, st);
     case 96: return waves == 4 ? run_impl<96, 4, 4>(M, x, ldx, stream, params, eps, y, ldy, st)
