@@ -492,8 +492,10 @@ int sfx_block_mlp(int M, int C, const float* x, long long ldx, const float* stre
   if (waves < 0) {
     const char* e = getenv("SFX_MLP_WAVES");
     waves = (e && *e) ? atoi(e) : 4;
-    const char* f = getenv("SFX_MLP_HS");  // hidden split at C = 256 (1, default) or whole tiles per wave (0);
-    hs = (f && *f) ? atoi(f) : 1;          // 2: also at C <= 128 (4-wave workgroups; tuning experiment)
+    // hidden split (profiles/r04_mlp_waves_hs.txt): 1 (default) at C = 128 and 256, where it measured faster
+    // (108.8 -> 100.0 / 239.7 -> 220.6 us); 2 at every C; 0 nowhere (whole 32-point tiles per wave)
+    const char* f = getenv("SFX_MLP_HS");
+    hs = (f && *f) ? atoi(f) : 1;
   }
   switch (C) {
     // (waves, ring phases): 4 waves = 128 points per workgroup, 2 workgroups per CU for C <= 128 (64 KB ring);
@@ -504,7 +506,7 @@ int sfx_block_mlp(int M, int C, const float* x, long long ldx, const float* stre
     case 96: return waves == 4 ? (hs == 2 ? run_impl<96, 4, 4, true>(M, x, ldx, stream, params, eps, y, ldy, st)
                                           : run_impl<96, 4, 4>(M, x, ldx, stream, params, eps, y, ldy, st))
                                : run_impl<96, 8, 4>(M, x, ldx, stream, params, eps, y, ldy, st);
-    case 128: return waves == 4 ? (hs == 2 ? run_impl<128, 4, 4, true>(M, x, ldx, stream, params, eps, y, ldy, st)
+    case 128: return waves == 4 ? (hs >= 1 ? run_impl<128, 4, 4, true>(M, x, ldx, stream, params, eps, y, ldy, st)
                                           : run_impl<128, 4, 4>(M, x, ldx, stream, params, eps, y, ldy, st))
                                 : run_impl<128, 8, 4>(M, x, ldx, stream, params, eps, y, ldy, st);
     default: return hs ? run_impl<256, 4, 8, true>(M, x, ldx, stream, params, eps, y, ldy, st)
