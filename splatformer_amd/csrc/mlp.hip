@@ -487,16 +487,13 @@ int sfx_block_mlp(int M, int C, const float* x, long long ldx, const float* stre
   SFX_REQUIRE(x != y, "sfx_block_mlp: in-place output is not supported");
   hipStream_t st = sfx::as_stream(stream_);
   // C <= 128: 4-wave (128-point) workgroups, two per CU -- measured 1.0-1.2x faster than one 8-wave workgroup
-  // (profiles/r04_mlp_waves_hs.txt); SFX_MLP_WAVES=8 restores the 256-point workgroups
-  static int waves = -1, hs = -1;
-  if (waves < 0) {
-    const char* e = getenv("SFX_MLP_WAVES");
-    waves = (e && *e) ? atoi(e) : 4;
-    // hidden split (profiles/r04_mlp_waves_hs.txt): 1 (default) at C = 128 and 256, where it measured faster
-    // (108.8 -> 100.0 / 239.7 -> 220.6 us); 2 at every C; 0 nowhere (whole 32-point tiles per wave)
-    const char* f = getenv("SFX_MLP_HS");
-    hs = (f && *f) ? atoi(f) : 1;
-  }
+  // (profiles/r04_mlp_waves_hs.txt); SFX_MLP_WAVES=8 restores the 256-point workgroups.  Hidden split (a wave pair
+  // per 32 points): SFX_MLP_HS=1 (default) at C = 128 and 256, where it measured faster (108.8 -> 100.0 /
+  // 239.7 -> 220.6 us); 2 at every C; 0 nowhere.  Both read per call (tests switch them).
+  const char* e = getenv("SFX_MLP_WAVES");
+  const int waves = (e && *e) ? atoi(e) : 4;
+  const char* f = getenv("SFX_MLP_HS");
+  const int hs = (f && *f) ? atoi(f) : 1;
   switch (C) {
     // (waves, ring phases): 4 waves = 128 points per workgroup, 2 workgroups per CU for C <= 128 (64 KB ring);
     // C = 256 runs 4 waves as 2 hidden-split pairs (its LN2 fragments + output accumulators fill 512 registers)

@@ -86,3 +86,26 @@ def test_block_fused_equals_unfused(device):
     m = ops.linear(h, fc1.weight, fc1.bias, act=ops.ACT_GELU)
     y0 = ops.linear(m, fc2.weight, fc2.bias, residual=x)
     assert rel_l2((y - x).cpu(), (y0 - x).cpu()) < 4e-6
+
+
+@pytest.mark.parametrize("C", ops.MLP_CHANNELS)
+@pytest.mark.parametrize("waves,hs", [("4", "0"), ("4", "1"), ("4", "2"), ("8", "0"), ("8", "1")])
+def test_block_mlp_launch_variants(device, monkeypatch, C, waves, hs):
+    """Every workgroup shape sfx_block_mlp can launch (SFX_MLP_WAVES: 128- / 256-point workgroups at C <= 128;
+    SFX_MLP_HS: the hidden split -- a wave pair per 32 points, partial fc2 sums added through LDS -- at no C, the
+    default C = 128 / 256, every C) at the fp64 bar of test_block_mlp_matches_fp64, on a ragged point count."""
+    monkeypatch.setenv("SFX_MLP_WAVES", waves)
+    monkeypatch.setenv("SFX_MLP_HS", hs)
+    M = 3001
+    ln, fc1, fc2 = _mods(C, 7 * C)
+    x = torch.randn(M, C, generator=torch.Generator().manual_seed(C)) * 2.0
+    x[::3] *= 1e3
+    ref = _ref(x, ln, fc1, fc2, torch.float64)
+    r32 = _ref(x, ln, fc1, fc2, torch.float32).double()
+    y = ops.block_mlp(x.to(device), ln.to(device), fc1.to(device), fc2.to(device)).cpu().double()
+    br, bh, b32 = ref - x.double(), y - x.double(), r32 - x.double()
+    assert torch.isfinite(y).all()
+    assert rel_l2(bh, br) <= max(2e-6, 2 * rel_l2(b32, br)), (rel_l2(bh, br), rel_l2(b32, br))
+    e_row = (bh - br).norm(dim=1) / br.norm(dim=1).clamp_min(1e-30)
+    e32 = (b32 - br).norm(dim=1) / br.norm(dim=1).clamp_min(1e-30)
+    assert bool((e_row <= 4 * e32 + 1e-6).all()), float((e_row - 4 * e32).max())
