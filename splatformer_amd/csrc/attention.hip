@@ -26,6 +26,10 @@
 
 #include "common.h"
 
+#ifndef SFX_ATTN_OCC16
+#define SFX_ATTN_OCC16 4  // workgroups per CU the d = 16 split kernel is compiled for
+#endif
+
 namespace {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
@@ -487,7 +491,7 @@ flash_bwd_key_kernel(const float* __restrict__ qkv, const int* __restrict__ orde
 // terms each (sfx::split2h), three term products per block on v_mfma_f32_32x32x16_f16; S and O are unscaled
 // in registers.  Same fp32-level accuracy, half the MFMAs and two-thirds of the LDS images.
 template <int D, bool F16>
-__global__ void __launch_bounds__(256, D == 16 ? 4 : 3)
+__global__ void __launch_bounds__(256, D == 16 ? SFX_ATTN_OCC16 : 3)
 window_attn_split_kernel(const float* __restrict__ qkv, const int* __restrict__ order, const int* __restrict__ win,
                          int Kwin, int C, float scale, float* __restrict__ out,
                          const unsigned long long* __restrict__ qkv_amax, unsigned qkv_tag, int nwin) {
