@@ -31,7 +31,10 @@ constexpr int MAXH = 6;               // heads
 constexpr int SLAB = 8192;            // [2 unit blocks][2 terms][32 rows][32 positions] fp16
 constexpr int PHASE = 2 * SLAB;
 constexpr int WAVES = 8;
-constexpr int RING = 4;
+#ifndef SFX_HEADS_RING
+#define SFX_HEADS_RING 4
+#endif
+constexpr int RING = SFX_HEADS_RING;  // LDS ring phases
 constexpr int PIECES = PHASE / 1024 / WAVES;  // 1 KB LDS-DMA pieces per wave per phase
 
 struct HeadsArgs {

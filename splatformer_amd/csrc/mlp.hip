@@ -35,6 +35,10 @@
 
 #include "gemm_common.h"
 
+#ifndef SFX_MLP_RING256
+#define SFX_MLP_RING256 8  // LDS ring phases of the C = 256 kernel
+#endif
+
 namespace {
 
 using namespace sfxg;
@@ -506,8 +510,8 @@ int sfx_block_mlp(int M, int C, const float* x, long long ldx, const float* stre
     case 128: return waves == 4 ? (hs >= 1 ? run_impl<128, 4, 4, true>(M, x, ldx, stream, params, eps, y, ldy, st)
                                           : run_impl<128, 4, 4>(M, x, ldx, stream, params, eps, y, ldy, st))
                                 : run_impl<128, 8, 4>(M, x, ldx, stream, params, eps, y, ldy, st);
-    default: return hs ? run_impl<256, 4, 8, true>(M, x, ldx, stream, params, eps, y, ldy, st)
-                       : run_impl<256, 4, 8>(M, x, ldx, stream, params, eps, y, ldy, st);
+    default: return hs ? run_impl<256, 4, SFX_MLP_RING256, true>(M, x, ldx, stream, params, eps, y, ldy, st)
+                       : run_impl<256, 4, SFX_MLP_RING256>(M, x, ldx, stream, params, eps, y, ldy, st);
   }
 }
 
