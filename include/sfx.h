@@ -35,9 +35,18 @@ const char* sfx_last_error(void);
  * inside gsplat rasterize_gaussians (called at utils/gs_utils.py:96).
  * (ABI v11) int32: one single-pass launch with decoupled look-back on a
  * library-owned ticket + tile-word area per (device, stream), epoch-tagged so
- * it needs no reset between scans (`ws` is still size-checked, unused);
- * in place (in == out) allowed. */
+ * it needs no reset between scans (`ws` is unused by the int32 form and may be
+ * NULL / 0); in place (in == out) allowed.  The first scan on a stream (or a
+ * larger one) allocates the area (hipMalloc + stream-ordered zeroing; growing it
+ * synchronises the stream): make one scan of the largest size before capturing
+ * scans or sorts into a HIP graph. */
 size_t sfx_scan_workspace_bytes(long long n);
+/* (ABI v12) Look-back waits on this stream's area that hit the spin cap (each one a wrong scan / radix prefix,
+ * never a hang) since the area was allocated; -1 when the stream has no area.  Synchronises the stream. */
+long long sfx_lookback_timeouts(void* stream);
+/* (ABI v12) Free this stream's look-back area after its pending work (call before destroying a stream that
+ * scanned or sorted; a later scan on the stream allocates a new one). */
+int sfx_lookback_release(void* stream);
 int sfx_scan_i32(long long n, const int32_t* in, int32_t* out, int inclusive, void* ws, size_t ws_bytes,
                  int32_t* total, void* stream);
 int sfx_scan_i64(long long n, const int64_t* in, int64_t* out, int inclusive, void* ws, size_t ws_bytes,

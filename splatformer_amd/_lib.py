@@ -27,6 +27,8 @@ SIGNATURES: dict[str, list] = {
     "sfx_abi_version": [],
     "sfx_last_error": [],
     "sfx_scan_workspace_bytes": [L],
+    "sfx_lookback_timeouts": [P],
+    "sfx_lookback_release": [P],
     "sfx_scan_i32": [L, P, P, I, P, Z, P, P],
     "sfx_scan_i64": [L, P, P, I, P, Z, P, P],
     "sfx_sort_workspace_bytes": [L],
@@ -47,6 +49,7 @@ _RESTYPES = {
     "sfx_abi_version": C.c_int,
     "sfx_last_error": C.c_char_p,
     "sfx_scan_workspace_bytes": C.c_size_t,
+    "sfx_lookback_timeouts": C.c_longlong,
     "sfx_sort_workspace_bytes": C.c_size_t,
 }
 

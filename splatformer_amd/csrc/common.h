@@ -181,33 +181,19 @@ __device__ __forceinline__ unsigned long long lb_load(const unsigned long long* 
 __device__ __forceinline__ unsigned lb_tag(unsigned long long w) { return (unsigned)(w >> 34); }
 __device__ __forceinline__ unsigned lb_status(unsigned long long w) { return (unsigned)(w >> 32) & 3u; }
 __device__ __forceinline__ int lb_value(unsigned long long w) { return (int)(unsigned)w; }
-// Exclusive prefix of tile `tile` by one thread walking its predecessors' words (stride `stride` words apart):
-// adds aggregates until an inclusive prefix; spins (s_sleep) on words that do not carry `tag` yet.
-// Every wait is bounded (kLbSpinCap polls, far above any real wait): a broken hand-off ends the kernel with a
-// wrong prefix (the parity tests catch it) instead of hanging the GPU.
+// Exclusive prefix of tile `tile` by a whole wave (uniform call): lanes read 64 predecessors at once, nearest first,
+// adding aggregates until an inclusive prefix; spins (s_sleep) on words that do not carry `tag` yet.
+// Every wait is bounded (kLbSpinCap polls, far above any real wait), so a broken hand-off cannot hang the GPU; a
+// wait that reaches the cap goes on with the stale word and counts itself in `*timeouts` (the look-back area's
+// header word, read by sfx_lookback_timeouts), so a wrong prefix is never silent.
 constexpr int kLbSpinCap = 1 << 22;
-__device__ __forceinline__ int lb_lookback_thread(const unsigned long long* flags, long long stride, int tile,
-                                                  unsigned tag) {
-  int excl = 0;
-  int spins = 0;
-  for (int j = tile - 1; j >= 0;) {
-    const unsigned long long w = lb_load(flags + (long long)j * stride);
-    if (lb_tag(w) != tag && ++spins < kLbSpinCap) {
-      __builtin_amdgcn_s_sleep(1);
-      continue;
-    }
-    excl += lb_value(w);
-    if (lb_status(w) == kLbPrefix) break;
-    --j;
-  }
-  return excl;
-}
-// The same by a whole wave (uniform call): lanes read 64 predecessors at once, nearest first.
-__device__ __forceinline__ int lb_lookback_wave(const unsigned long long* flags, int tile, unsigned tag) {
+__device__ __forceinline__ int lb_lookback_wave(const unsigned long long* flags, int tile, unsigned tag,
+                                                unsigned* timeouts) {
   const int lane = __lane_id();
   int excl = 0;
   int j = tile - 1;
   int spins = 0;
+  bool counted = false;
   while (j >= 0) {
     const int idx = j - lane;
     unsigned st = kLbPrefix;
@@ -221,9 +207,13 @@ __device__ __forceinline__ int lb_lookback_wave(const unsigned long long* flags,
     // nearest predecessor with a prefix (idx < 0 counts as one); none in this window: all 64 are aggregates
     const int stop = pre ? __ffsll((long long)pre) - 1 : 63;
     const unsigned long long need = (stop == 63) ? ~0ull : ((2ull << stop) - 1ull);
-    if ((__ballot(st == 0u) & need) && ++spins < kLbSpinCap) {  // a needed predecessor has not published yet
-      __builtin_amdgcn_s_sleep(1);
-      continue;
+    if (__ballot(st == 0u) & need) {  // a needed predecessor has not published yet
+      if (++spins < kLbSpinCap) {
+        __builtin_amdgcn_s_sleep(1);
+        continue;
+      }
+      if (!counted && lane == 0) atomicAdd(timeouts, 1u);  // giving up: the prefix will be wrong, say so
+      counted = true;
     }
     int v = (lane <= stop) ? val : 0;
 #pragma unroll

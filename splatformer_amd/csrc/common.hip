@@ -141,6 +141,7 @@ int scan_impl(long long n, const T* in, T* out, int inclusive, void* ws, size_t 
 constexpr int LB_ITEMS = 8;
 constexpr int LB_TILE = SCAN_THREADS * LB_ITEMS;
 constexpr size_t LB_HEADER = 256;  // ticket counter, then the tile words
+constexpr int kLbTimeoutWord = 16;  // header word (u32 index) counting look-back waits that hit the spin cap
 
 __global__ void __launch_bounds__(SCAN_THREADS)
 scan_lookback_i32(const int32_t* __restrict__ in, int32_t* __restrict__ out, long long n, int inclusive, int tiles,
@@ -175,7 +176,7 @@ scan_lookback_i32(const int32_t* __restrict__ in, int32_t* __restrict__ out, lon
       if (threadIdx.x == 0) sfx::lb_store(flags, sfx::lb_word(tag, sfx::kLbPrefix, agg));
     } else {
       if (threadIdx.x == 0) sfx::lb_store(flags + tile, sfx::lb_word(tag, sfx::kLbAgg, agg));
-      prefix = sfx::lb_lookback_wave(flags, tile, tag);
+      prefix = sfx::lb_lookback_wave(flags, tile, tag, ticket + kLbTimeoutWord);
       if (threadIdx.x == 0) sfx::lb_store(flags + tile, sfx::lb_word(tag, sfx::kLbPrefix, prefix + agg));
     }
     if (threadIdx.x == 0) {
@@ -199,12 +200,9 @@ int scan_lookback_impl(long long n, const int32_t* in, int32_t* out, int inclusi
     if (total) hipMemsetAsync(total, 0, sizeof(int32_t), st);
     return sfx::check_launch("scan");
   }
+  (void)ws;  // the look-back words live in the stream's library-owned area (sfx::lookback_state)
+  (void)ws_bytes;
   const long long tiles = (n + LB_TILE - 1) / LB_TILE;
-  const size_t need = LB_HEADER + (size_t)tiles * sizeof(unsigned long long);
-  if (ws_bytes < need || (reinterpret_cast<uintptr_t>(ws) & 7)) {
-    sfx::set_error("scan: workspace too small or misaligned (%zu < %zu)", ws_bytes, need);
-    return SFX_ERR_WORKSPACE;
-  }
   unsigned* ticket;
   unsigned long long* flags;
   unsigned tag;
@@ -262,6 +260,39 @@ int lookback_state(hipStream_t st, long long words, unsigned** ticket, unsigned 
   return SFX_OK;
 }
 
+// Look-back waits of this (device, stream)'s area that reached the spin cap since its allocation (0 = every scan
+// and radix pass on it was exact); -1: no area (nothing scanned on the stream yet).  Synchronous (host read).
+long long lookback_timeouts(hipStream_t st) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return -1;
+  unsigned* t = nullptr;
+  {
+    std::lock_guard<std::mutex> lock(g_lb_mu);
+    auto it = g_lb.find({dev, st});
+    if (it == g_lb.end()) return -1;
+    t = it->second.ticket;
+  }
+  unsigned v = 0;
+  if (hipStreamSynchronize(st) != hipSuccess ||
+      hipMemcpy(&v, t + kLbTimeoutWord, sizeof(v), hipMemcpyDeviceToHost) != hipSuccess)
+    return -1;
+  return v;
+}
+
+// Frees this (device, stream)'s area after the stream's pending work (a caller that destroys a stream it scanned
+// on releases its area first; otherwise the area lives as long as the library).
+int lookback_release(hipStream_t st) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return check_launch("look-back release (device)");
+  std::lock_guard<std::mutex> lock(g_lb_mu);
+  auto it = g_lb.find({dev, st});
+  if (it == g_lb.end()) return SFX_OK;
+  if (hipStreamSynchronize(st) != hipSuccess || hipFree(it->second.ticket) != hipSuccess)
+    return check_launch("look-back release");
+  g_lb.erase(it);
+  return SFX_OK;
+}
+
 // The look-back scan on a given area: `ticket` zero (the kernel puts it back to zero), `flags`
 // (lookback_scan_words(n) words) holding no word with this call's `tag` (sfx::lookback_state hands out both).
 long long lookback_scan_words(long long n) { return (n + LB_TILE - 1) / LB_TILE; }
@@ -278,7 +309,11 @@ extern "C" {
 
 const char* sfx_last_error(void) { return sfx::g_err; }
 
-int sfx_abi_version(void) { return 11; }
+int sfx_abi_version(void) { return 12; }
+
+long long sfx_lookback_timeouts(void* stream) { return sfx::lookback_timeouts(sfx::as_stream(stream)); }
+
+int sfx_lookback_release(void* stream) { return sfx::lookback_release(sfx::as_stream(stream)); }
 
 size_t sfx_scan_workspace_bytes(long long n) {
   // int64: one sum per 1024-element tile; int32: the look-back header + one word per 2048-element tile

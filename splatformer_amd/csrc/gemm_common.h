@@ -120,9 +120,13 @@ __device__ __forceinline__ float gelu_erf(float x) {
   q = __builtin_fmaf(q, t, 0.459207207f);
   q = __builtin_fmaf(q, t, 1.15110528f);
   const float half_tail = 0.5f * __builtin_amdgcn_exp2f(-(t * q));
-  return x * (x >= 0.f ? 1.f - half_tail : half_tail);
+  // below -5.65 the clamped tail would leave x * 4e-9, growing with |x|: exact GELU is 0 there (to below fp32's
+  // rounding of the product), so the negative branch selects 0 (one v_cndmask)
+  return x >= 0.f ? x * (1.f - half_tail) : (x < -5.65f ? 0.f : x * half_tail);
 }
-// d/dx of the erf GELU (torch GeluBackward, approximate='none')
+// d/dx of the erf GELU (torch GeluBackward, approximate='none').  Exact erff / expf, while the forward epilogues use
+// the fitted gelu_erf above: the two differ by the fit's 6e-8 on Phi, far inside the training gradient bars
+// (the backward's derivative is not the derivative of the fitted forward, by that margin)
 __device__ __forceinline__ float gelu_erf_grad(float x) {
   const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
   const float pdf = 0.39894228040143268f * expf(-0.5f * x * x);

@@ -41,5 +41,7 @@ def evaluate_scenes(model, scenes: Sequence[dict], cameras: Sequence[dict],
         psnr_sum += psnr.sum()
         ssim_sum += ssim(pred, gt, quantize_u8=True).double().sum().cpu()
         num_images += pred.shape[0]
+        if not evaluate_input and hasattr(model, "check_refine"):
+            model.check_refine()  # the refine's deferred pooling checks, at the readback that consumes it
     return dist.reduce_metrics({"psnr": psnr_sum, "ssim": ssim_sum}, num_images, len(mine),
                                device=device if ws > 1 and device.type == "cuda" else None)

@@ -175,6 +175,12 @@ class FeaturePredictor(nn.Module):
             h = ops.grouped_linear(h, wm, bm, len(self.output_features), act=ops.ACT_RELU)
         return ops.linear(h, wl, bl, act=ops.ACT_TANH, act_ncols=n_tanh, residual=feat)
 
+    def check_refine(self, wait: bool = True) -> None:
+        """Validate the pooled run counts of the refines issued so far (PointTransformerV3.check_deferred): call
+        where a refined result is consumed on the host (evaluate_scenes does, at its metric readback).  Raises once
+        per failing forward, naming it; the model stays usable."""
+        self.backbone.backbone.check_deferred(wait=wait)
+
     def _fused_heads(self):
         """(slab stream, parameter table, output columns, out_dim) of the fused heads kernel, rebuilt with the
         packed heads (when a head parameter changes)."""

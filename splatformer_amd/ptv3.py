@@ -436,6 +436,7 @@ class PointTransformerV3(nn.Module):
             shifts.append(3 * cum)
         counts_rd = ops.pool_counts_begin(point.codes_phys, point.order_phys, shifts) if POOL_COUNTS_UPFRONT else None
         self.check_deferred(wait=True)  # the previous forward's pooling checks (long complete by now)
+        self._forward_id = self.__dict__.get("_forward_id", 0) + 1
         deferred: list = []
         k = 1
         for s in range(self.num_stages):
@@ -459,22 +460,34 @@ class PointTransformerV3(nn.Module):
                     conv_in = point.pop("stale_conv_feat", None)
                     last = di == len(dec_names) - 1 and ci == len(children) - 1
                     point = mod.run(point, conv_in=conv_in, out=out if last else None)
-        # the pooling run-count checks whose reads have landed run now; the rest at the next forward (or
-        # check_deferred()): waiting here would hold back the launches the caller enqueues after the backbone
-        # (the heads, the render) until the whole backbone has run -- a drained queue at every refine
-        self._deferred = deferred
+        # the pooling run-count checks whose reads have landed run now; the rest when the caller consumes the
+        # result (FeaturePredictor.check_refine, evaluate_scenes) or at the next forward: waiting here would hold
+        # back the launches the caller enqueues after the backbone (the heads, the render) until the whole
+        # backbone has run -- a drained queue at every refine
+        fid = self._forward_id
+        self._deferred = self.__dict__.get("_deferred", []) + [(rd, m, fid, i + 1) for i, (rd, m) in
+                                                                enumerate(deferred)]
         self.check_deferred(wait=False)
         return point
 
     def check_deferred(self, wait: bool = True) -> None:
-        """Validate the pooled run counts read back asynchronously by forward (pool_geometry_end's `deferred`)."""
-        pending = []
-        for rd, m in self.__dict__.get("_deferred", []):
-            if wait or rd.ready():
+        """Validate the pooled run counts read back asynchronously by forward (pool_geometry_end's `deferred`).
+
+        Every entry is taken off the pending list before it is validated, so a failing forward raises exactly
+        once (naming its forward id and pooling) and later forwards are checked on their own.  An entry whose
+        read has not landed stays pending unless `wait`."""
+        pending, errors = [], []
+        for rd, m, fid, k in self.__dict__.get("_deferred", []):
+            if not (wait or rd.ready()):
+                pending.append((rd, m, fid, k))
+                continue
+            try:
                 ops.check_pool_runs(rd.get(), m)
-            else:
-                pending.append((rd, m))
+            except RuntimeError as e:
+                errors.append(f"forward {fid}, pooling {k}: {e}")
         self._deferred = pending
+        if errors:
+            raise RuntimeError("; ".join(errors))
 
 
 class PointTransformerV3Model(nn.Module):

@@ -266,7 +266,8 @@ def test_config_d_optimizer_step(ranks, oracle32, oracle64):
           f"{bool((~noisy[bad]).sum() == 0)}; weights rel {rel_l2(hip_w, ref64):.2e}")
     assert e_own <= 1e-6
     assert int((bad & ~noisy).sum()) == 0
-    assert int(bad.sum()) <= 2 * int(bad32.sum()) + 100
+    # no more sign disagreements than the fp32 oracle's own (4289 vs 4286 measured, gpurun_out r04c/r04d logs)
+    assert int(bad.sum()) <= 1.01 * int(bad32.sum()) + 1
 
 
 def test_config_d_next_forward(ranks, oracle32):

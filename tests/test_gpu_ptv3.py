@@ -88,10 +88,12 @@ def test_linear_narrow_cases(device, M, N, K):
 
 def test_gelu_fitted_tail_accuracy(device):
     """The GEMM epilogue's GELU (gemm_common.h gelu_erf: Phi from one fitted tail exponent, shared by the fused
-    MLP) against fp64 erf-GELU over [-12, 12] and at 0 / +-tiny: |dGELU| <= 4e-7 max(1, |x|) -- the fit's 6e-8 on Phi
-    plus the fp16x2 split of the identity product's input (x = h + l to 2^-22 = 2.4e-7 relative)."""
+    MLP) against fp64 erf-GELU over [-12, 12], at 0 / +-tiny, and far in the tails (one row of |x| up to 1e4: the
+    negative tail is exactly 0 below -5.65): |dGELU| <= 4e-7 max(1, |x|) -- the fit's 6e-8 on Phi plus the
+    fp16x2 split of the identity product's input (x = h + l to 2^-22 = 2.4e-7 relative)."""
     x = torch.linspace(-12.0, 12.0, 4096 * 64, dtype=torch.float64)
     x[:8] = torch.tensor([0.0, 1e-30, -1e-30, 1e-8, -1e-8, 5.65, -5.65, 0.5])
+    x[64:128] = torch.cat([-torch.logspace(0.8, 4, 32, dtype=torch.float64), torch.logspace(0.8, 4, 32, dtype=torch.float64)])
     x32 = x.float().reshape(4096, 64)
     eye = torch.eye(64)
     y = ops.linear(x32.to(device), eye.to(device), None, act=ops.ACT_GELU).cpu().double().flatten()
@@ -100,6 +102,7 @@ def test_gelu_fitted_tail_accuracy(device):
     err = (y - ref).abs() / xd.abs().clamp_min(1.0)
     assert float(err.max()) <= 4e-7, (float(err.max()), float(xd[int(err.argmax())]))
     assert float(y[0]) == 0.0 and torch.isfinite(y).all()
+    assert bool((y[64:96] == 0.0).all()), y[64:96]  # x <= -6.3: GELU underflows to exactly 0, as fp32 erf does
 
 
 @pytest.mark.parametrize("scale", [1.0, 1e-30, 1e30])

@@ -147,6 +147,14 @@ def test_lookback_scan_and_onesweep_sort_cases(device):
         order = np.argsort(sk, kind="stable")
         assert np.array_equal(vo.cpu().numpy(), order.astype(np.int32)), (n, lo, hi)
         assert np.array_equal(ko.cpu().numpy().view("uint64"), ku[order]), (n, lo, hi)
+    # no look-back wait of any of these scans / passes reached the spin cap (ABI v12 counter); a
+    # released area is reallocated by the next scan with a fresh counter
+    assert _lib.fn("sfx_lookback_timeouts")(_lib.stream()) == 0
+    _lib.call("sfx_lookback_release", _lib.stream())
+    assert _lib.fn("sfx_lookback_timeouts")(_lib.stream()) == -1
+    xd = torch.ones(5000, device=device, dtype=torch.int32)
+    _lib.call("sfx_scan_i32", 5000, xd.data_ptr(), xd.data_ptr(), 1, None, 0, None, _lib.stream())
+    assert int(xd[-1]) == 5000 and _lib.fn("sfx_lookback_timeouts")(_lib.stream()) == 0
 
 
 def test_bin_and_sort_exact(device):
