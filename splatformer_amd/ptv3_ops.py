@@ -46,7 +46,9 @@ _lib.register("sfx_subm_conv_partials_pairs", [I, I, I, P, L, P, P, P, P, P, P, 
 _lib.register("sfx_subm_pair_pos", [I, L, P, P, P, P])
 _lib.register("sfx_subm_cpe_pack_bytes", [I], Z)
 _lib.register("sfx_subm_cpe_pack", [I, P, P, P, P, P])
-_lib.register("sfx_subm_cpe_ln", [I, I, P, P, P, P, P, P, P, P, P, P, F, P, P, P])
+_lib.register("sfx_subm_cpe_ln", [I, I, P, P, P, P, P, P, P, P, P, P, P, P, F, P, P, P])
+_lib.register("sfx_subm_order_keys", [I, P, P, P])
+_lib.register("sfx_subm_rowexp", [I, I, P, P, P])
 _lib.register("sfx_gs_pack", [I, P, L, P, L, P, L, P, L, P, L, P, L, I, F, P, L, P, P, P])
 _lib.register("sfx_offsets_to_batch", [I, I, P, P, P])
 _lib.register("sfx_point_embed", [I, I, I, P, L, P, P, P, P, P, L, P])
@@ -584,6 +586,7 @@ class SubmMap:
         self._off = None
         self._off_c = None
         self._pos = None
+        self._order = None
 
     def ensure_pairs(self) -> "SubmMap":
         if self._pairs is None:
@@ -616,6 +619,17 @@ class SubmMap:
             call("sfx_subm_pair_pos", n, self.num_pairs, ptr(self.pair_out), ptr(off_dev), ptr(pos), stream())
             self._pos = pos
         return self._pos
+
+    @property
+    def order(self) -> Tensor:
+        """The fused conv's row order (sfx_subm_order_keys + a 2-pass radix sort): rows grouped by neighbour mask,
+        built once per map (every conv of the stage shares it)."""
+        if self._order is None:
+            n = self.nbr.shape[0]
+            keys = torch.empty(n, device=self.nbr.device, dtype=torch.int64)
+            call("sfx_subm_order_keys", n, ptr(self.nbr), ptr(keys), stream())
+            _, self._order = _sort(keys, None, 0, 16)
+        return self._order
 
     def pair_off_ready(self) -> bool:
         """Whether the pair offsets are already on the host (reading them costs no wait)."""
@@ -675,12 +689,12 @@ def subm_partials_ok(x: Tensor, smap: "SubmMap", cout: int) -> bool:
                                             or smap.num_pairs * cout * 4 + 64 < 0x7ffffff0))
 
 
-# Block.cpe + shortcut + norm1 of the eval forward in one launch with the pair products summed on chip
-# (csrc/subm_fused.hip) for these channel counts -- opt-in (SFX_SUBM_FUSED=1): measured slower than the pair GEMM +
-# pair-sum LayerNorm it replaces (config B 513 vs 568 renders/s, profiles/r04_ab_bench.txt)
+# Block.cpe + shortcut + norm1 of the eval forward in one launch, the conv summed in MFMA registers over all 27
+# offsets (csrc/subm_fused.hip) -- opt-in (SFX_SUBM_FUSED=1): measured slower than the offset-major pair GEMM +
+# pair-sum LayerNorm on every config-B stage (profiles/r05_subm_fused_stages.txt)
 SUBM_FUSED = os.environ.get("SFX_SUBM_FUSED", "0") == "1"
-SUBM_FUSED_KERNELS = (64, 96, 128)  # the channel counts sfx_subm_cpe_ln has kernels for
-SUBM_FUSED_CHANNELS = tuple(int(c) for c in os.environ.get("SFX_SUBM_FUSED_CHANNELS", "64,96,128").split(",")
+SUBM_FUSED_KERNELS = (64, 96, 128, 256)  # the channel counts sfx_subm_cpe_ln has kernels for
+SUBM_FUSED_CHANNELS = tuple(int(c) for c in os.environ.get("SFX_SUBM_FUSED_CHANNELS", "64,96,128,256").split(",")
                             if c and int(c) in SUBM_FUSED_KERNELS)
 
 
@@ -701,16 +715,24 @@ def subm_cpe_pack(wf: Tensor) -> Tuple[Tensor, Tensor]:
     return wpk, winv
 
 
+def subm_rowexp(x: Tensor) -> Tensor:
+    """Per-row fp16x2 exponents of a conv input (sfx_subm_rowexp): x_j * 2^e_j has its maximum in [2^14, 2^15)."""
+    n, C = x.shape
+    e = torch.empty(n, device=x.device, dtype=torch.int32)
+    call("sfx_subm_rowexp", n, C, ptr(x), ptr(e), stream())
+    return e
+
+
 def subm_cpe_ln(xc: Tensor, x: Tensor, smap: "SubmMap", wpk: Tensor, winv: Tensor, bias: Tensor, g_cpe: Tensor,
                 b_cpe: Tensor, g1: Tensor, b1: Tensor, eps: float) -> Tuple[Tensor, Tensor]:
-    """x1 = x + LN_cpe(SubMConv'(xc)), h = LN1(x1) in one launch (csrc/subm_fused.hip; C in SUBM_FUSED_CHANNELS)."""
+    """x1 = x + LN_cpe(SubMConv'(xc)), h = LN1(x1) in one launch (csrc/subm_fused.hip; C in SUBM_FUSED_KERNELS)."""
     n, C = x.shape
     if xc.shape != x.shape or not (xc.is_contiguous() and x.is_contiguous()):
         raise RuntimeError("subm_cpe_ln: contiguous [n, C] inputs expected")
     x1 = torch.empty_like(x)
     h = torch.empty_like(x)
-    call("sfx_subm_cpe_ln", n, C, ptr(xc), ptr(x), ptr(smap.nbr), ptr(wpk), ptr(winv), ptr(bias), ptr(g_cpe),
-         ptr(b_cpe), ptr(g1), ptr(b1), float(eps), ptr(x1), ptr(h), stream())
+    call("sfx_subm_cpe_ln", n, C, ptr(xc), ptr(x), ptr(smap.nbr), ptr(smap.order), ptr(subm_rowexp(xc)), ptr(wpk),
+         ptr(winv), ptr(bias), ptr(g_cpe), ptr(b_cpe), ptr(g1), ptr(b1), float(eps), ptr(x1), ptr(h), stream())
     return x1, h
 
 

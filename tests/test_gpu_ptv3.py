@@ -215,14 +215,16 @@ def test_subm_conv_partials_atomic_free(device):
         assert torch.equal(xo, xo2) and torch.equal(h, h2)
 
 
-@pytest.mark.parametrize("C", [64, 96, 128])
-@pytest.mark.parametrize("n,unique,sep", [(6000, True, False), (4133, False, True), (1, True, False)])
+@pytest.mark.parametrize("C", [64, 96, 128, 256])
+@pytest.mark.parametrize("n,unique,sep", [(6000, True, False), (4133, False, True), (1, True, False),
+                                          (20011, False, False)])
 def test_subm_cpe_ln_fused(device, C, n, unique, sep):
-    """sfx_subm_cpe_ln (conv + LN_cpe + shortcut + norm1 in one launch, pair products summed on chip) against the
-    fp64 oracle (ptv3_ref.subm_conv then the two LayerNorms) -- relative L2 <= 2e-6 on x1 and h -- and against the
-    pair-GEMM path; duplicate voxels, a row count not a multiple of the 128-row block, a separate conv input (the
-    first decoder Block's stale skip feature), a single point; rows of very different magnitude (per-row fp16x2
-    scales); two runs bitwise equal."""
+    """sfx_subm_cpe_ln (the eval CPE: conv summed over all 27 offsets in MFMA registers + LN_cpe + shortcut + norm1
+    in one launch, the default path) against the fp64 oracle (ptv3_ref.subm_conv then the two LayerNorms) --
+    relative L2 <= 2e-6 on x1 and h -- and against the pair-GEMM path; duplicate voxels, row counts not a multiple
+    of the workgroup's points, a separate conv input (the first decoder Block's stale skip feature), a single
+    point; rows of very different magnitude (one fp16x2 scale per output point over its neighbours' rows); two runs
+    bitwise equal."""
     s = make_scene(max(n, 64), 1, seed=n + C, unique_voxels=unique)
     grid = torch.floor(s["means"][:n] * 256).int()
     n = grid.shape[0]
