@@ -281,6 +281,12 @@ int sfx_window_attention_varlen(int num_windows, int max_window, int heads, int 
  * the keys into order[R][n] / inverse[R][n]. */
 int sfx_serialize_keys(int n, const int* grid_coord, const int* batch, int depth, int num_orders, int t0, int t1,
                        int t2, int t3, int code_bits, int64_t* codes, uint64_t* keys, void* stream);
+/* (ABI v12) Renumber a serialized point set by its first order (new point i = old point order[0][i]): codes,
+ * orders and inverses [R][n] re-expressed in the new numbering, grid [n][3] int32 and coord [n][3] float gathered --
+ * the refiner's stage-0 locality permutation (sfx_move_rows). */
+int sfx_serialize_permute(int n, int num_orders, const int* order, const int* inverse, const int64_t* codes,
+                          const int* grid, const float* coord, int64_t* codes_p, int* order_p, int* inverse_p,
+                          int* grid_p, float* coord_p, void* stream);
 int sfx_serialize_finalize(int n, int num_orders, const int* sorted_pos, int* order, int* inverse, void* stream);
 
 /* SerializedPooling (reference models/pointtransformer_v3.py:290-299 -> upstream Pointcept), sort-free: the parent's serialized
@@ -358,6 +364,12 @@ int sfx_gs_pack(int n, const float* means, long long ld_means, const float* scal
                 void* stream);
 /* Pointcept offset2batch */
 int sfx_offsets_to_batch(int n, int B, const long long* offsets, int* batch, void* stream);
+/* (ABI v12) Row moves by index, rows of `words` 32-bit words (leading dimensions in words): scatter = 0 gathers
+ * dst[i] = src[idx[i]], scatter = 1 scatters dst[idx[i]] = src[i].  The refiner's stage-0 z-order row permutation
+ * (PointTransformerV3Model reorder: the input Gaussians enter in file order; the backbone runs them in serialized
+ * order so every stage-0 gather is local, and the features go back to file order before the heads). */
+int sfx_move_rows(long long n, int words, const void* src, long long src_ld, const int* idx, void* dst,
+                  long long dst_ld, int scatter, void* stream);
 
 /* ---- batched views: the eval path of gs_utils.rasterize_gaussians_to_multiimgs (gs_utils.py:20-27) ------
  * V cameras with shared intrinsics: records laid out [V, n, ...]; intersections of all views sorted once

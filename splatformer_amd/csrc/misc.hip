@@ -107,6 +107,20 @@ __global__ void offsets_to_batch_kernel(int n, int B, const long long* __restric
 
 }  // namespace
 
+// Row moves by an index (32-bit words): gather dst[i] = src[idx[i]] / scatter dst[idx[i]] = src[i]; one thread per
+// word, consecutive threads along a row (coalesced on the contiguous side).
+__global__ void __launch_bounds__(256) move_rows_kernel(long long n, int words, const unsigned* __restrict__ src,
+                                                        long long sld, const int* __restrict__ idx,
+                                                        unsigned* __restrict__ dst, long long dld, int scatter) {
+  const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= n * words) return;
+  const long long i = e / words;
+  const int w = (int)(e - i * words);
+  const long long j = idx[i];
+  if (scatter) dst[j * dld + w] = src[i * sld + w];
+  else dst[i * dld + w] = src[j * sld + w];
+}
+
 extern "C" {
 
 int sfx_gs_pack(int n, const float* means, long long ld_means, const float* scales, long long ld_scales,
@@ -139,6 +153,19 @@ int sfx_point_embed(int n, int K, int N, const float* x, long long ldx, const fl
   else
     point_embed_kernel<32><<<sfx::ceil_div(n, 64), 256, 0, st>>>(n, K, x, ldx, w, b, scale, shift, y, ldy);
   return sfx::check_launch("sfx_point_embed");
+}
+
+// dst[i, :] = src[idx[i], :] (scatter = 0) or dst[idx[i], :] = src[i, :] (scatter = 1) for rows of `words` 32-bit words,
+// leading dimensions in words; idx a permutation (scatter) or any in-range rows (gather)
+int sfx_move_rows(long long n, int words, const void* src, long long src_ld, const int* idx, void* dst,
+                  long long dst_ld, int scatter, void* stream) {
+  SFX_REQUIRE(n >= 0 && words > 0 && src_ld >= words && dst_ld >= words, "sfx_move_rows: bad shape");
+  if (n == 0) return SFX_OK;
+  SFX_REQUIRE(src && idx && dst && src != dst, "sfx_move_rows: null or aliased buffer");
+  move_rows_kernel<<<sfx::ceil_div(n * words, 256), 256, 0, sfx::as_stream(stream)>>>(
+      n, words, reinterpret_cast<const unsigned*>(src), src_ld, idx, reinterpret_cast<unsigned*>(dst), dst_ld,
+      scatter);
+  return sfx::check_launch("sfx_move_rows");
 }
 
 int sfx_offsets_to_batch(int n, int B, const long long* offsets, int* batch, void* stream) {

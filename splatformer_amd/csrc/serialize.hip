@@ -190,6 +190,33 @@ __global__ void segment_mean_kernel(int m, int D, const int* __restrict__ idx_pt
   }
 }
 
+// The stage-0 renumbering of a serialized point set by its first serialized order: new point i = old point
+// perm[i] (perm = order row 0), so the backbone's stage-0 row gathers follow the serialization.  Codes, orders
+// and inverses are re-expressed in the new numbering (order row 0 becomes the identity); grid and coord gathered.
+__global__ void __launch_bounds__(256) serialize_permute_kernel(int n, int R, const int* __restrict__ order,
+                                                                const int* __restrict__ inverse,
+                                                                const int64_t* __restrict__ codes,
+                                                                const int* __restrict__ grid,
+                                                                const float* __restrict__ coord,
+                                                                int64_t* __restrict__ codes_p, int* __restrict__ order_p,
+                                                                int* __restrict__ inverse_p, int* __restrict__ grid_p,
+                                                                float* __restrict__ coord_p) {
+  const int i = (int)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int j = order[i];  // perm[i]: row 0 of order
+  for (int r = 0; r < R; ++r) {
+    const long long o = (long long)r * n;
+    codes_p[o + i] = codes[o + j];
+    inverse_p[o + i] = inverse[o + j];
+    order_p[o + i] = inverse[order[o + i]];  // the new index of the point at serialized position i of order r
+  }
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    grid_p[3ll * i + k] = grid[3ll * j + k];
+    coord_p[3ll * i + k] = coord[3ll * j + k];
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -206,6 +233,18 @@ int sfx_serialize_keys(int n, const int* grid_coord, const int* batch, int depth
   serialize_keys_kernel<<<sfx::ceil_div(n, 256), 256, 0, sfx::as_stream(stream)>>>(
       n, grid_coord, batch, depth, num_orders, make_int4(t0, t1, t2, t3), code_bits, codes, keys);
   return sfx::check_launch("sfx_serialize_keys");
+}
+
+int sfx_serialize_permute(int n, int num_orders, const int* order, const int* inverse, const int64_t* codes,
+                          const int* grid, const float* coord, int64_t* codes_p, int* order_p, int* inverse_p,
+                          int* grid_p, float* coord_p, void* stream) {
+  SFX_REQUIRE(n >= 0 && num_orders >= 1, "sfx_serialize_permute: bad sizes");
+  if (n == 0) return SFX_OK;
+  SFX_REQUIRE(order && inverse && codes && grid && coord && codes_p && order_p && inverse_p && grid_p && coord_p,
+              "sfx_serialize_permute: null buffer");
+  serialize_permute_kernel<<<sfx::ceil_div(n, 256), 256, 0, sfx::as_stream(stream)>>>(
+      n, num_orders, order, inverse, codes, grid, coord, codes_p, order_p, inverse_p, grid_p, coord_p);
+  return sfx::check_launch("sfx_serialize_permute");
 }
 
 int sfx_serialize_finalize(int n, int num_orders, const int* sorted_pos, int* order, int* inverse, void* stream) {

@@ -19,6 +19,7 @@ which the fused render prep (sfx_render_prep_project) reads in place.
 """
 from __future__ import annotations
 
+import os
 from collections import OrderedDict
 from typing import Dict, List, Optional
 
@@ -30,6 +31,9 @@ from . import _lib
 from . import ptv3_ops as ops
 from .ptv3 import PointTransformerV3Model
 
+# renumber the points by serialized order inside the backbone (ptv3.PointTransformerV3.prepare): opt-in
+# (SFX_REORDER=1), measured neutral on config B (profiles/r05_ab_reorder.txt)
+REORDER = os.environ.get("SFX_REORDER", "0") == "1"
 FEATURE2CHANNEL = {"means": 3, "features_dc": 3, "features_rest": 3, "opacities": 1, "scales": 3, "quats": 4}
 ALL_FEATURES = ["means", "features_dc", "features_rest", "opacities", "scales", "quats"]
 BASE_FEATURES = ["means", "scales", "opacities", "quats", "features_dc", "features_rest"]
@@ -158,7 +162,9 @@ class FeaturePredictor(nn.Module):
                 "serialized_depth": _lib.HostRead(gmax)}
         method = self.additional_info.get("downsample")
         if method is None:
-            self.backbone(data, perms=perms, out=h0[:, :cb])
+            # REORDER: the backbone runs on the points renumbered by serialized order and writes its features
+            # back in input order (result-neutral)
+            self.backbone(data, perms=perms, out=h0[:, :cb], reorder=REORDER)
         else:  # fork experiment (feature_predictor.py:159-196): backbone on the downsampled cloud, mapped back
             from .downsample import downsample_for_backbone
             c, f, g, mapper = downsample_for_backbone(method, self.additional_info, means, feat, grid)

@@ -379,8 +379,15 @@ class PointTransformerV3(nn.Module):
         chans = [self.enc_channels[s]] + ([self.dec_channels[s]] if s < len(self.dec_channels) else [])
         return not all(ops.subm_fused_ok(c) for c in chans)
 
-    def prepare(self, data_dict, perms: Optional[List[Sequence[int]]] = None, pairs: bool = True) -> Point:
-        """Point + serialization (randperm draw 0) + stage-0 neighbour map; `feat` is not embedded yet."""
+    def prepare(self, data_dict, perms: Optional[List[Sequence[int]]] = None, pairs: bool = True,
+                reorder: bool = False) -> Point:
+        """Point + serialization (randperm draw 0) + stage-0 neighbour map; `feat` is not embedded yet.
+
+        reorder: renumber the points by their first serialized order (sfx_serialize_permute; `point.perm[i]` is the
+        input row of point i) so every stage-0 gather -- SubM neighbours, attention windows, pooling clusters --
+        reads neighbouring rows; the caller permutes `feat` the same way and scatters the output back.  The
+        results are those of the input numbering: serialization ties (points of one voxel) keep their input
+        order, so the lowest-index voxel representative and every stable sort are unchanged."""
         feat = data_dict["feat"]
         _lib.require_gpu(feat)
         dev = feat.device
@@ -406,16 +413,26 @@ class PointTransformerV3(nn.Module):
         self.last_perms = []
         codes, order, inverse = ops.serialize(grid, batch, depth, code_bits, self.order)
         p0 = self._draw_perm(perms, 0)
-        point = Point(coord=data_dict["coord"].float().contiguous(), grid_coord=grid, offset=offset, codes_phys=codes,
+        coord = data_dict["coord"].float().contiguous()
+        perm = None
+        if reorder and batch is None:
+            perm = order[0]
+            codes, order, inverse, grid, coord = ops.serialize_permute(codes, order, inverse, grid, coord)
+        point = Point(coord=coord, grid_coord=grid, offset=offset, codes_phys=codes,
                       order_phys=order, inverse_phys=inverse, order_type=p0, serialized_depth=depth,
                       code_bits=code_bits)
+        if perm is not None:
+            point.perm = perm
         if batch is not None:
             point.batch = batch
         point.nbr = ops.subm_neighbors(grid, batch, with_pairs=pairs)
         return point
 
     @torch.no_grad()
-    def forward(self, data_dict, perms: Optional[List[Sequence[int]]] = None, out: Optional[Tensor] = None) -> Point:
+    def forward(self, data_dict, perms: Optional[List[Sequence[int]]] = None, out: Optional[Tensor] = None,
+                reorder: bool = False) -> Point:
+        """reorder (prepare): the backbone runs on the points renumbered by serialized order; the returned Point's
+        `perm` maps its rows to the input rows, and `out` (if given) receives the features in INPUT order."""
         feat = data_dict["feat"]
         _lib.require_gpu(feat)
         emb, bnm = self.embedding[0], self.embedding[1]
@@ -425,8 +442,12 @@ class PointTransformerV3(nn.Module):
             emb_feat = ops.point_embed(feat, emb.weight, emb.bias, sc, sh)
         else:
             emb_feat = ops.linear(feat, emb.weight, emb.bias, scale=sc, shift=sh, act=ops.ACT_GELU)
-        point = self.prepare(data_dict, perms, pairs=self.stage_needs_pairs(0))
-        point.feat = emb_feat
+        point = self.prepare(data_dict, perms, pairs=self.stage_needs_pairs(0), reorder=reorder)
+        perm = point.get("perm")
+        point.feat = emb_feat if perm is None else ops.move_rows(emb_feat, perm)
+        final_out = out
+        if perm is not None:
+            out = None  # the last Block writes the renumbered rows; scattered into final_out below
         # every pooling's cluster count from the stage-0 codes, read back while stage 0 runs: no pooling waits
         pools = [getattr(self.enc, f"enc{s}").down for s in range(1, self.num_stages)]
         shifts, depth, cum = [], point.serialized_depth, 0
@@ -468,6 +489,8 @@ class PointTransformerV3(nn.Module):
         self._deferred = self.__dict__.get("_deferred", []) + [(rd, m, fid, i + 1) for i, (rd, m) in
                                                                 enumerate(deferred)]
         self.check_deferred(wait=False)
+        if perm is not None and final_out is not None:
+            ops.move_rows(point.feat, perm, dst=final_out, scatter=True)
         return point
 
     def check_deferred(self, wait: bool = True) -> None:
@@ -530,5 +553,5 @@ class PointTransformerV3Model(nn.Module):
             load = {k: v for k, v in sd.items() if k in own and own[k].shape == v.shape}
             self.backbone.load_state_dict(load, strict=False)
 
-    def forward(self, x, perms=None, out=None):
-        return self.backbone(x, perms=perms, out=out)
+    def forward(self, x, perms=None, out=None, reorder=False):
+        return self.backbone(x, perms=perms, out=out, reorder=reorder)

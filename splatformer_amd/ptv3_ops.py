@@ -29,6 +29,7 @@ _lib.register("sfx_window_attention", [I, I, I, I, I, P, P, P, F, P, P, I, P])
 _lib.register("sfx_window_attention_varlen", [I, I, I, I, I, P, P, P, F, P, P, I, P])
 _lib.register("sfx_serialize_keys", [I, P, P, I, I, I, I, I, I, I, P, P, P])
 _lib.register("sfx_serialize_finalize", [I, I, P, P, P, P])
+_lib.register("sfx_serialize_permute", [I, I, P, P, P, P, P, P, P, P, P, P, P])
 _lib.register("sfx_pool_run_flags", [I, I, P, P, I, P, P])
 _lib.register("sfx_pool_assign_runs", [I, I, I, P, P, P, P, P, P, P, P])
 _lib.register("sfx_pool_reorder", [I, I, I, P, P, P, P, P, P, P])
@@ -51,6 +52,7 @@ _lib.register("sfx_subm_order_keys", [I, P, P, P])
 _lib.register("sfx_subm_rowexp", [I, I, P, P, P])
 _lib.register("sfx_gs_pack", [I, P, L, P, L, P, L, P, L, P, L, P, L, I, F, P, L, P, P, P])
 _lib.register("sfx_offsets_to_batch", [I, I, P, P, P])
+_lib.register("sfx_move_rows", [L, I, P, L, P, P, L, I, P])
 _lib.register("sfx_point_embed", [I, I, I, P, L, P, P, P, P, P, L, P])
 _lib.register("sfx_heads_stream_floats", [I, I], Z)
 _lib.register("sfx_heads_params_floats", [I], Z)
@@ -473,6 +475,18 @@ def serialize(grid_coord: Tensor, batch: Optional[Tensor], depth: int, code_bits
     return codes, order, inverse
 
 
+def serialize_permute(codes: Tensor, order: Tensor, inverse: Tensor, grid: Tensor, coord: Tensor):
+    """Renumber the points by serialized order row 0 (sfx_serialize_permute): -> (codes, order, inverse, grid,
+    coord) in the new numbering; new point i is old point order[0][i]."""
+    R, n = codes.shape
+    cp, op, ip = torch.empty_like(codes), torch.empty_like(order), torch.empty_like(inverse)
+    gp = torch.empty_like(grid)
+    xp = torch.empty(n, 3, device=coord.device, dtype=torch.float32)
+    call("sfx_serialize_permute", n, R, ptr(order, torch.int32), ptr(inverse, torch.int32), ptr(codes, torch.int64),
+         ptr(grid, torch.int32), ptr(coord, torch.float32), ptr(cp), ptr(op), ptr(ip), ptr(gp), ptr(xp), stream())
+    return cp, op, ip, gp, xp
+
+
 def scan_i32(x: Tensor, inclusive: bool = True, total: Optional[Tensor] = None) -> Tuple[Tensor, Tensor]:
     n = x.shape[0]
     out = torch.empty_like(x)
@@ -788,6 +802,25 @@ def subm_conv(x: Tensor, smap: "SubmMap", weight: Tensor, bias: Optional[Tensor]
          ptr(smap.pair_out), smap._off_host, po, ldo, *_slot_args(x_amax), *_slot_args(w_amax),
          *weight_split(weight), stream())
     return out
+
+
+def move_rows(src: Tensor, idx: Tensor, dst: Optional[Tensor] = None, scatter: bool = False) -> Tensor:
+    """dst[i] = src[idx[i]] (gather) or dst[idx[i]] = src[i] (scatter) for the rows of a 2-D (or 1-D) tensor of
+    4- or 8-byte elements (sfx_move_rows)."""
+    s2 = src if src.dim() == 2 else src.reshape(src.shape[0], -1)
+    esz = s2.element_size()
+    if esz not in (4, 8) or s2.stride(1) != 1:
+        raise RuntimeError("move_rows: rows of 4- or 8-byte elements, unit column stride")
+    n = idx.shape[0]
+    if dst is None:
+        if scatter:
+            raise RuntimeError("move_rows: scatter needs a destination")
+        dst = torch.empty((n,) + tuple(src.shape[1:]), device=src.device, dtype=src.dtype)
+    d2 = dst if dst.dim() == 2 else dst.reshape(dst.shape[0], -1)
+    words = s2.shape[1] * esz // 4
+    call("sfx_move_rows", n, words, s2.data_ptr(), s2.stride(0) * esz // 4, ptr(idx, torch.int32), d2.data_ptr(),
+         d2.stride(0) * esz // 4, 1 if scatter else 0, stream())
+    return dst
 
 
 def gs_pack(gs: dict, feat_out: Tensor, grid_resolution: float, grid_out: Optional[Tensor],

@@ -245,6 +245,24 @@ def test_config_a(wa):
     check_end_to_end(wa, range(4))
 
 
+def test_reorder_is_result_neutral(wa, device):
+    """SFX_REORDER=1 (backbone on the points renumbered by serialized order, features written back in input
+    order) refines the same Gaussians as the default input-order run, on the same shuffle permutations."""
+    from splatformer_amd import feature_predictor as fp
+    scene_d = to_device(wa.scene, device)
+    saved = fp.REORDER
+    fp.REORDER = True
+    try:
+        with torch.no_grad():
+            out = wa.model([scene_d], [0], perms=wa.perms)[0]
+        torch.cuda.synchronize()
+    finally:
+        fp.REORDER = saved
+    for k in KEYS:
+        got, exp = out[k].cpu(), wa.out[k]
+        assert torch.allclose(got, exp, rtol=1e-5, atol=1e-6), f"{k}: max |d| {(got - exp).abs().max().item():.3e}"
+
+
 # ---- config E: 500k SH3 (Cin 59), 1920x1080 -------------------------------------------------------------------
 @pytest.fixture(scope="module")
 def we(device):
