@@ -200,10 +200,12 @@ int sfx_subm_conv_bwd_data(int n, int cin, int cout, const float* dy, long long 
                            int* centre_ws, float* dx, long long lddx, const float* wt_split, const float* wt_inv,
                            void* stream);
 /* non-flash SerializedAttention backward (visualize.py:140-179 math): dout [N, C] = grad of the attention
- * output rows; dqkv [N, 3C] must be zero-filled (dK/dV accumulate across overlapping windows). */
+ * output rows; dqkv [N, 3C] must be zero-filled (dK/dV accumulate across overlapping windows).  (ABI v13)
+ * attn_out [N, C] = the forward's output (Delta = dO . O), stats = workspace of N * heads * 4 floats, 16-byte
+ * aligned (query pass -> key pass); both unused under SFX_ATTN_PREC=fp32 (the exact single-kernel backward). */
 int sfx_window_attention_bwd(int num_windows, int window, int heads, int head_dim, int channels, const float* qkv,
-                             const int* order, const int* win, float scale, const float* dout, float* dqkv,
-                             void* stream);
+                             const int* order, const int* win, float scale, const float* attn_out, const float* dout,
+                             float* dqkv, float* stats, void* stream);
 /* (ABI v7) enable_flash=True backward (windows as sfx_window_attention_varlen): dqkv [N, 3C] zero-filled,
  * stats = workspace of N * heads * 2 floats (per-query log-sum-exp and dO.O). */
 int sfx_window_attention_varlen_bwd(int num_windows, int max_window, int heads, int head_dim, int channels,

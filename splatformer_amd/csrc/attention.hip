@@ -1452,6 +1452,498 @@ window_attn_bwd_kernel(const float* __restrict__ qkv, const int* __restrict__ or
   }
 }
 
+// ---- fp16x2 backward (default) -----------------------------------------------------------------------------
+// The same autograd as window_attn_bwd_kernel in two passes over the (window, head) items, on
+// v_mfma_f32_32x32x16_f16 with every operand as two fp16 terms (sfx::split2h) of a power-of-two-scaled value and
+// three term products per block (the forward's F16 scheme):
+//   query pass (lanes = this wave's 32 queries):  S^T = K Q^T -> softmax max and 1/sum ; Delta_q = dO_q . O_q from
+//     the forward output (= rowsum(P o dP)) ; per 32-key block dP^T = V dO^T, dS^T = P^T (dP^T - Delta) and
+//     dQ^T += K^T dS^T with dS^T straight from registers as the B operand (as P^T in the forward) ; dQ stored plainly
+//     (each query belongs to one window) and (max, 1/sum, Delta) written per (query, head) for the key pass;
+//   key pass (lanes = this wave's 32 keys): per 32-query block S = Q K^T and dP = dO V^T recomputed, P from the
+//     stored statistics, dS = P (dP - Delta) ; dV^T += dO^T P and dK^T += Q^T dS from registers.
+// Scales: q, k, v and dO of an item by powers of two putting the item's largest magnitude in [2^14, 2^15); P (<= 1)
+// by 2^14; dS by one power of two per (lane column, 32-row block), its block product unscaled before it joins the
+// accumulator.  Every MFMA is a 16-deep step of 3 products, against 8 steps of v_mfma_f32_32x32x2_f32 per 16 in the
+// exact kernel; recomputing S and dP in the key pass is what keeps both passes' contractions on the register axis.
+// LDS per item: row images [2 terms][128][KD] (as the forward's K image) and transposed images [2][D][136] with the
+// keys (queries) of each 16-group in the B-operand register order (as the forward's V^T).
+template <int KD>
+__device__ __forceinline__ int bwd_row_off(int r, int c) {  // byte offset of 16-byte chunk c of term row r
+  return KD == 16 ? r * 48 + c * 16 : r * 64 + (((c ^ (r >> 2)) & 3) << 4);
+}
+// power of two s with m * s in [2^14, 2^15) (1 for m == 0 or non-finite m); inv = 1 / s
+__device__ __forceinline__ float bwd_pow2(float m, float& inv) {
+  int e = 0;
+  if (m > 0.f && m <= 3.4028235e38f) {
+    (void)frexpf(m, &e);
+    e = 15 - e;
+    e = e > 126 ? 126 : (e < -126 ? -126 : e);
+  }
+  inv = ldexpf(1.f, -e);
+  return ldexpf(1.f, e);
+}
+__device__ __forceinline__ float amax4(float4 v) {
+  return fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w)));
+}
+// workgroup-wide max of 4 values (256 threads, one barrier)
+__device__ __forceinline__ float4 bwd_wg_max4(float4 m, float4* red) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    m.x = fmaxf(m.x, __shfl_xor(m.x, o, 64));
+    m.y = fmaxf(m.y, __shfl_xor(m.y, o, 64));
+    m.z = fmaxf(m.z, __shfl_xor(m.z, o, 64));
+    m.w = fmaxf(m.w, __shfl_xor(m.w, o, 64));
+  }
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  float4 r = red[0];
+#pragma unroll
+  for (int i = 1; i < 4; ++i) {
+    const float4 t = red[i];
+    r = make_float4(fmaxf(r.x, t.x), fmaxf(r.y, t.y), fmaxf(r.z, t.z), fmaxf(r.w, t.w));
+  }
+  return r;
+}
+// two fp16 terms of 8 scaled values -> B-operand fragments
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ void bwd_frag(float4 a, float4 b, float s, f16x8 (&f)[2]) {
+  uint2 ta[2], tb[2];
+  sfx::split2h(a, s, ta);
+  sfx::split2h(b, s, tb);
+#pragma unroll
+  for (int t = 0; t < 2; ++t) f[t] = __builtin_bit_cast(f16x8, make_uint4(ta[t].x, ta[t].y, tb[t].x, tb[t].y));
+}
+__device__ __forceinline__ floatx16 mfma3(const f16x8 (&a)[2], const f16x8 (&b)[2], floatx16 c) {
+  c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[1], b[0], c, 0, 0, 0);  // smallest first
+  c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], b[1], c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], b[0], c, 0, 0, 0);
+}
+// a lane's 8 (or fewer, zero-padded past D) values of row `src`, columns d0 .. d0 + 7
+template <int D>
+__device__ __forceinline__ void bwd_load8(const float* p, int d0, bool ok, float4& a, float4& b) {
+  a = make_float4(0.f, 0.f, 0.f, 0.f);
+  b = a;
+  if (ok && d0 < D) {
+    a = *reinterpret_cast<const float4*>(p + d0);
+    if (d0 + 4 < D) b = *reinterpret_cast<const float4*>(p + d0 + 4);
+  }
+}
+// row image + transposed image of a pair of rows (2p, 2p + 1), float4 column chunk ch, terms of x * s
+template <int D, int KD>
+__device__ __forceinline__ void bwd_stage_pair(char* rimg, unsigned short* timg, int row, int ch, float4 v0, float4 v1,
+                                               float s) {
+  constexpr int QROW = KD == 16 ? 48 : 64, VST = 136;
+  uint2 t0[2], t1[2];
+  sfx::split2h(v0, s, t0);
+  sfx::split2h(v1, s, t1);
+  const int o0 = bwd_row_off<KD>(row, ch >> 1) + ((ch & 1) << 3);
+  const int o1 = bwd_row_off<KD>(row + 1, ch >> 1) + ((ch & 1) << 3);
+  const int kk = row & 15;  // even: rows row, row + 1 land on adjacent positions
+  const int pos = (row & ~15) + 8 * ((kk >> 2) & 1) + (((kk >> 3) << 2) | (kk & 3));
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    *reinterpret_cast<uint2*>(rimg + q * KMAX * QROW + o0) = t0[q];
+    *reinterpret_cast<uint2*>(rimg + q * KMAX * QROW + o1) = t1[q];
+    unsigned* vt = reinterpret_cast<unsigned*>(timg + (q * D + 4 * ch) * VST + pos);
+    vt[0] = (t0[q].x & 0xffffu) | (t1[q].x << 16);
+    vt[VST / 2] = (t0[q].x >> 16) | (t1[q].x & 0xffff0000u);
+    vt[VST] = (t0[q].y & 0xffffu) | (t1[q].y << 16);
+    vt[3 * VST / 2] = (t0[q].y >> 16) | (t1[q].y & 0xffff0000u);
+  }
+}
+template <int KD>
+__device__ __forceinline__ void bwd_stage_row(char* rimg, int row, int ch, float4 v, float s) {
+  constexpr int QROW = KD == 16 ? 48 : 64;
+  uint2 t[2];
+  sfx::split2h(v, s, t);
+  const int o = bwd_row_off<KD>(row, ch >> 1) + ((ch & 1) << 3);
+#pragma unroll
+  for (int q = 0; q < 2; ++q) *reinterpret_cast<uint2*>(rimg + q * KMAX * QROW + o) = t[q];
+}
+template <int KD>
+__device__ __forceinline__ void bwd_row_frag(const char* rimg, int row, int c, f16x8 (&f)[2]) {
+  constexpr int QROW = KD == 16 ? 48 : 64;
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+    f[q] = __builtin_bit_cast(f16x8, *reinterpret_cast<const uint4*>(rimg + q * KMAX * QROW + bwd_row_off<KD>(row, c)));
+}
+// A fragment of a transposed image: lane row dd = l32 (zero past D), 8 keys of 16-step `step` from half h
+template <int D>
+__device__ __forceinline__ void bwd_tr_frag(const unsigned short* timg, int l32, int step, int h, f16x8 (&f)[2]) {
+  constexpr int VST = 136;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (l32 < D) v = *reinterpret_cast<const uint4*>(timg + (q * D + l32) * VST + step * 16 + 8 * h);
+    f[q] = __builtin_bit_cast(f16x8, v);
+  }
+}
+
+template <int D>
+__global__ void __launch_bounds__(256, 3)
+window_attn_bwd_q_kernel(const float* __restrict__ qkv, const int* __restrict__ order, const int* __restrict__ win,
+                         int Kwin, int C, float scale, const float* __restrict__ attn_out,
+                         const float* __restrict__ dout, float* __restrict__ dqkv, float4* __restrict__ stats,
+                         int nwin) {
+  constexpr int KD = D == 16 ? 16 : 32, NKS = KD / 16, QROW = KD == 16 ? 48 : 64, VST = 136;
+  constexpr int RB = 2 * KMAX * QROW, TB = 2 * D * VST * 2;
+  constexpr int CH = D / 4, NE = (KMAX / 2) * CH, NIT = (NE + 255) / 256;
+  __shared__ __attribute__((aligned(16))) char lds[2 * RB + TB];
+  __shared__ int rows[KMAX];
+  __shared__ float4 red[4];
+  char* Kr = lds;
+  char* Vr = lds + RB;
+  unsigned short* Kt = reinterpret_cast<unsigned short*>(lds + 2 * RB);
+
+  const int heads = C / D;
+  const int nb = (int)gridDim.x;
+  const int L = (int)(blockIdx.x % 8) * (nb / 8) + (int)(blockIdx.x / 8);  // XCD-aware, as the forward
+  if (L >= nwin * heads) return;
+  const int w = L / heads, head = L - w * heads;
+  const int key_start = win[2 * w], query_start = win[2 * w + 1];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, h = lane >> 5, l32 = lane & 31;
+  const long long ld = 3ll * C;
+
+  if (tid < KMAX) rows[tid] = tid < Kwin ? order[key_start + tid] : -1;
+  if (D < KD)  // zero K / V columns D..KD-1
+    for (int rr = tid; rr < 4 * KMAX; rr += 256)
+      *reinterpret_cast<uint4*>(lds + (rr >> 8) * RB + ((rr >> 7) & 1) * KMAX * QROW + bwd_row_off<KD>(rr & 127, D / 8)) =
+          make_uint4(0, 0, 0, 0);
+  __syncthreads();
+  // this lane's query: q and dO slices dd = 16 ks + 8h .. +7 (B operands of S^T and dP^T) and Delta = dO . O
+  const int qi = 32 * wid + l32;
+  const int qsrc = rows[qi];
+  const bool qown = qsrc >= 0 && key_start + qi >= query_start;
+  float4 qa[NKS][2], ga[NKS][2];
+  float delta = 0.f;
+  float4 mx4 = make_float4(0.f, 0.f, 0.f, 0.f);  // (q, k, v, dO)
+#pragma unroll
+  for (int ks = 0; ks < NKS; ++ks) {
+    const int d0 = 16 * ks + 8 * h;
+    bwd_load8<D>(qkv + (long long)(qsrc < 0 ? 0 : qsrc) * ld + head * D, d0, qsrc >= 0, qa[ks][0], qa[ks][1]);
+    bwd_load8<D>(dout + (long long)(qsrc < 0 ? 0 : qsrc) * C + head * D, d0, qown, ga[ks][0], ga[ks][1]);
+    float4 oa, ob;
+    bwd_load8<D>(attn_out + (long long)(qsrc < 0 ? 0 : qsrc) * C + head * D, d0, qown, oa, ob);
+    delta += ga[ks][0].x * oa.x + ga[ks][0].y * oa.y + ga[ks][0].z * oa.z + ga[ks][0].w * oa.w +
+             ga[ks][1].x * ob.x + ga[ks][1].y * ob.y + ga[ks][1].z * ob.z + ga[ks][1].w * ob.w;
+    mx4.x = fmaxf(mx4.x, fmaxf(amax4(qa[ks][0]), amax4(qa[ks][1])));
+    mx4.w = fmaxf(mx4.w, fmaxf(amax4(ga[ks][0]), amax4(ga[ks][1])));
+  }
+  delta += __shfl_xor(delta, 32, 64);
+  // this thread's K / V elements: row pairs x float4 column chunks
+  float4 k0[NIT], k1[NIT], v0[NIT], v1[NIT];
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int e = tid + 256 * it;
+    k0[it] = k1[it] = v0[it] = v1[it] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (e < NE) {
+      const int kp = e / CH, ch = e - kp * CH;
+      const int s0 = rows[2 * kp], s1 = rows[2 * kp + 1];
+      if (s0 >= 0) {
+        k0[it] = *reinterpret_cast<const float4*>(qkv + (long long)s0 * ld + C + head * D + 4 * ch);
+        v0[it] = *reinterpret_cast<const float4*>(qkv + (long long)s0 * ld + 2 * C + head * D + 4 * ch);
+      }
+      if (s1 >= 0) {
+        k1[it] = *reinterpret_cast<const float4*>(qkv + (long long)s1 * ld + C + head * D + 4 * ch);
+        v1[it] = *reinterpret_cast<const float4*>(qkv + (long long)s1 * ld + 2 * C + head * D + 4 * ch);
+      }
+    }
+    mx4.y = fmaxf(mx4.y, fmaxf(amax4(k0[it]), amax4(k1[it])));
+    mx4.z = fmaxf(mx4.z, fmaxf(amax4(v0[it]), amax4(v1[it])));
+  }
+  mx4 = bwd_wg_max4(mx4, red);
+  float iQ, iK, iV, iG;
+  const float sQ = bwd_pow2(mx4.x, iQ), sK = bwd_pow2(mx4.y, iK), sV = bwd_pow2(mx4.z, iV),
+              sG = bwd_pow2(mx4.w, iG);
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int e = tid + 256 * it;
+    if (e < NE) {
+      const int kp = e / CH, ch = e - kp * CH;
+      bwd_stage_pair<D, KD>(Kr, Kt, 2 * kp, ch, k0[it], k1[it], sK);
+      bwd_stage_row<KD>(Vr, 2 * kp, ch, v0[it], sV);
+      bwd_stage_row<KD>(Vr, 2 * kp + 1, ch, v1[it], sV);
+    }
+  }
+  f16x8 qf[NKS][2], gf[NKS][2];
+#pragma unroll
+  for (int ks = 0; ks < NKS; ++ks) {
+    bwd_frag(qa[ks][0], qa[ks][1], sQ, qf[ks]);
+    bwd_frag(ga[ks][0], ga[ks][1], sG, gf[ks]);
+  }
+  __syncthreads();
+
+  // S^T[key][query] (log2 units, as the forward: scale * log2(e) folded in)
+  floatx16 s[4];
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s[kb][r] = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      f16x8 kf[2];
+      bwd_row_frag<KD>(Kr, kb * 32 + l32, 2 * ks + h, kf);
+      s[kb] = mfma3(kf, qf[ks], s[kb]);
+    }
+  }
+  const float cS = scale * 1.4426950408889634f * iQ * iK;
+  float mx = -INFINITY;
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int key = kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+      s[kb][r] = key < Kwin ? s[kb][r] * cS : -INFINITY;
+      mx = fmaxf(mx, s[kb][r]);
+    }
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  float sum = 0.f;
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float e = __builtin_amdgcn_exp2f(s[kb][r] - mx);
+      s[kb][r] = e;
+      sum += e;
+    }
+  sum += __shfl_xor(sum, 32, 64);
+  const float rinv = 1.f / sum;
+  if (h == 0 && qown) stats[(long long)qsrc * heads + head] = make_float4(mx, rinv, delta, 0.f);
+
+  // per key block: dP^T = V dO^T, dS^T = P^T (dP^T - Delta), dQ^T += K^T dS^T
+  const float cP = iV * iG;
+  floatx16 dq;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) dq[r] = 0.f;
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb) {
+    floatx16 dp;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dp[r] = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      f16x8 vf[2];
+      bwd_row_frag<KD>(Vr, kb * 32 + l32, 2 * ks + h, vf);
+      dp = mfma3(vf, gf[ks], dp);
+    }
+    float m = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      dp[r] = s[kb][r] * rinv * (dp[r] * cP - delta);  // dS^T
+      m = fmaxf(m, fabsf(dp[r]));
+    }
+    m = fmaxf(m, __shfl_xor(m, 32, 64));
+    float isd;
+    const float sd = bwd_pow2(m, isd);
+    floatx16 t;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) t[r] = 0.f;
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      f16x8 bf[2], kt[2];
+      bwd_frag(make_float4(dp[8 * st + 0], dp[8 * st + 1], dp[8 * st + 2], dp[8 * st + 3]),
+               make_float4(dp[8 * st + 4], dp[8 * st + 5], dp[8 * st + 6], dp[8 * st + 7]), sd, bf);
+      bwd_tr_frag<D>(Kt, l32, 2 * kb + st, h, kt);
+      t = mfma3(kt, bf, t);
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dq[r] += t[r] * isd;
+  }
+  if (qown) {
+    const float cQ = scale * iK;
+    float* dst = dqkv + (long long)qsrc * ld + head * D;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int dd = 8 * g + 4 * h;
+      if (dd + 3 < D)
+        *reinterpret_cast<float4*>(dst + dd) =
+            make_float4(dq[4 * g + 0] * cQ, dq[4 * g + 1] * cQ, dq[4 * g + 2] * cQ, dq[4 * g + 3] * cQ);
+    }
+  }
+}
+
+template <int D>
+__global__ void __launch_bounds__(256, 3)
+window_attn_bwd_kv_kernel(const float* __restrict__ qkv, const int* __restrict__ order, const int* __restrict__ win,
+                          int Kwin, int C, float scale, const float* __restrict__ dout, float* __restrict__ dqkv,
+                          const float4* __restrict__ stats, int nwin) {
+  constexpr int KD = D == 16 ? 16 : 32, NKS = KD / 16, QROW = KD == 16 ? 48 : 64, VST = 136;
+  constexpr int RB = 2 * KMAX * QROW, TB = 2 * D * VST * 2;
+  constexpr int CH = D / 4, NE = (KMAX / 2) * CH, NIT = (NE + 255) / 256;
+  constexpr int DP = D + 4;  // fp32 output staging row stride
+  static_assert(2 * KMAX * DP * 4 <= 2 * RB + 2 * TB, "output staging must fit the operand images");
+  __shared__ __attribute__((aligned(16))) char lds[2 * RB + 2 * TB];
+  __shared__ int rows[KMAX];
+  __shared__ float4 stat[KMAX];
+  __shared__ float4 red[4];
+  char* Qr = lds;
+  char* Gr = lds + RB;
+  unsigned short* Qt = reinterpret_cast<unsigned short*>(lds + 2 * RB);
+  unsigned short* Gt = reinterpret_cast<unsigned short*>(lds + 2 * RB + TB);
+
+  const int heads = C / D;
+  const int nb = (int)gridDim.x;
+  const int L = (int)(blockIdx.x % 8) * (nb / 8) + (int)(blockIdx.x / 8);
+  if (L >= nwin * heads) return;
+  const int w = L / heads, head = L - w * heads;
+  const int key_start = win[2 * w], query_start = win[2 * w + 1];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, h = lane >> 5, l32 = lane & 31;
+  const long long ld = 3ll * C;
+
+  if (tid < KMAX) {
+    const int src = tid < Kwin ? order[key_start + tid] : -1;
+    rows[tid] = src;
+    // queries of this window that another window owns (the ragged last window's padding) or past Kwin: P = 0
+    // (exp2(s - inf) = 0, 1/sum = 0) and Delta = 0, exactly as their zero dO in the reference
+    stat[tid] = (src >= 0 && key_start + tid >= query_start) ? stats[(long long)src * heads + head]
+                                                               : make_float4(INFINITY, 0.f, 0.f, 0.f);
+  }
+  if (D < KD)
+    for (int rr = tid; rr < 4 * KMAX; rr += 256)
+      *reinterpret_cast<uint4*>(lds + (rr >> 8) * RB + ((rr >> 7) & 1) * KMAX * QROW + bwd_row_off<KD>(rr & 127, D / 8)) =
+          make_uint4(0, 0, 0, 0);
+  __syncthreads();
+  // this lane's key: k and v slices (B operands of S and dP)
+  const int kk = 32 * wid + l32;
+  const int ksrc = rows[kk];
+  const bool key_ok = ksrc >= 0;
+  float4 ka[NKS][2], va[NKS][2];
+  float4 mx4 = make_float4(0.f, 0.f, 0.f, 0.f);  // (q, k, v, dO)
+#pragma unroll
+  for (int ks = 0; ks < NKS; ++ks) {
+    const int d0 = 16 * ks + 8 * h;
+    const float* base = qkv + (long long)(key_ok ? ksrc : 0) * ld + head * D;
+    bwd_load8<D>(base + C, d0, key_ok, ka[ks][0], ka[ks][1]);
+    bwd_load8<D>(base + 2 * C, d0, key_ok, va[ks][0], va[ks][1]);
+    mx4.y = fmaxf(mx4.y, fmaxf(amax4(ka[ks][0]), amax4(ka[ks][1])));
+    mx4.z = fmaxf(mx4.z, fmaxf(amax4(va[ks][0]), amax4(va[ks][1])));
+  }
+  float4 q0[NIT], q1[NIT], g0[NIT], g1[NIT];
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int e = tid + 256 * it;
+    q0[it] = q1[it] = g0[it] = g1[it] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (e < NE) {
+      const int qp = e / CH, ch = e - qp * CH;
+      const int r0 = 2 * qp, s0 = rows[r0], s1 = rows[r0 + 1];
+      if (s0 >= 0) {
+        q0[it] = *reinterpret_cast<const float4*>(qkv + (long long)s0 * ld + head * D + 4 * ch);
+        if (key_start + r0 >= query_start)
+          g0[it] = *reinterpret_cast<const float4*>(dout + (long long)s0 * C + head * D + 4 * ch);
+      }
+      if (s1 >= 0) {
+        q1[it] = *reinterpret_cast<const float4*>(qkv + (long long)s1 * ld + head * D + 4 * ch);
+        if (key_start + r0 + 1 >= query_start)
+          g1[it] = *reinterpret_cast<const float4*>(dout + (long long)s1 * C + head * D + 4 * ch);
+      }
+    }
+    mx4.x = fmaxf(mx4.x, fmaxf(amax4(q0[it]), amax4(q1[it])));
+    mx4.w = fmaxf(mx4.w, fmaxf(amax4(g0[it]), amax4(g1[it])));
+  }
+  mx4 = bwd_wg_max4(mx4, red);
+  float iQ, iK, iV, iG;
+  const float sQ = bwd_pow2(mx4.x, iQ), sK = bwd_pow2(mx4.y, iK), sV = bwd_pow2(mx4.z, iV),
+              sG = bwd_pow2(mx4.w, iG);
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int e = tid + 256 * it;
+    if (e < NE) {
+      const int qp = e / CH, ch = e - qp * CH;
+      bwd_stage_pair<D, KD>(Qr, Qt, 2 * qp, ch, q0[it], q1[it], sQ);
+      bwd_stage_pair<D, KD>(Gr, Gt, 2 * qp, ch, g0[it], g1[it], sG);
+    }
+  }
+  f16x8 kf[NKS][2], vf[NKS][2];
+#pragma unroll
+  for (int ks = 0; ks < NKS; ++ks) {
+    bwd_frag(ka[ks][0], ka[ks][1], sK, kf[ks]);
+    bwd_frag(va[ks][0], va[ks][1], sV, vf[ks]);
+  }
+  __syncthreads();
+
+  const float cS = scale * 1.4426950408889634f * iQ * iK, cP = iG * iV;
+  floatx16 dk, dv;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) dk[r] = dv[r] = 0.f;
+#pragma unroll 1
+  for (int qb = 0; qb < 4; ++qb) {
+    floatx16 sb, pb;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sb[r] = pb[r] = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      f16x8 a[2];
+      bwd_row_frag<KD>(Qr, qb * 32 + l32, 2 * ks + h, a);
+      sb = mfma3(a, kf[ks], sb);
+      bwd_row_frag<KD>(Gr, qb * 32 + l32, 2 * ks + h, a);
+      pb = mfma3(a, vf[ks], pb);
+    }
+    // rows r: query qb*32 + (r&3) + 8(r>>2) + 4h ; P (<= 1) into sb, dS into pb
+    float m = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float4 st = stat[qb * 32 + (r & 3) + 8 * (r >> 2) + 4 * h];
+      const float P = key_ok ? __builtin_amdgcn_exp2f(sb[r] * cS - st.x) * st.y : 0.f;
+      sb[r] = P;
+      pb[r] = P * (pb[r] * cP - st.z);
+      m = fmaxf(m, fabsf(pb[r]));
+    }
+    m = fmaxf(m, __shfl_xor(m, 32, 64));
+    float isd;
+    const float sd = bwd_pow2(m, isd);
+    floatx16 t;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) t[r] = 0.f;
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      f16x8 bp[2], bd[2], at[2];
+      bwd_frag(make_float4(sb[8 * st + 0], sb[8 * st + 1], sb[8 * st + 2], sb[8 * st + 3]),
+               make_float4(sb[8 * st + 4], sb[8 * st + 5], sb[8 * st + 6], sb[8 * st + 7]), 16384.f, bp);
+      bwd_tr_frag<D>(Gt, l32, 2 * qb + st, h, at);
+      dv = mfma3(at, bp, dv);
+      bwd_frag(make_float4(pb[8 * st + 0], pb[8 * st + 1], pb[8 * st + 2], pb[8 * st + 3]),
+               make_float4(pb[8 * st + 4], pb[8 * st + 5], pb[8 * st + 6], pb[8 * st + 7]), sd, bd);
+      bwd_tr_frag<D>(Qt, l32, 2 * qb + st, h, at);
+      t = mfma3(at, bd, t);
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dk[r] += t[r] * isd;
+  }
+  // dK / dV leave through LDS (whole row segments per store); keys shared with the neighbouring window (the ragged
+  // last window's overlap) are added atomically, every other key is owned by this window and stored plainly
+  const float cK = scale * iQ, cV = iG * (1.f / 16384.f);
+  __syncthreads();  // all waves done with the operand images
+  float* Ok = reinterpret_cast<float*>(lds);
+  float* Ov = Ok + KMAX * DP;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int dd = (r & 3) + 8 * (r >> 2) + 4 * h;
+    if (dd < D) {
+      Ok[kk * DP + dd] = dk[r] * cK;
+      Ov[kk * DP + dd] = dv[r] * cV;
+    }
+  }
+  __syncthreads();
+  const int next_ks = (w + 1 < nwin) ? win[2 * (w + 1)] : 0x7fffffff;
+  for (int e = tid; e < Kwin * 2 * CH; e += 256) {
+    const int row = e / (2 * CH);
+    const int rem = e - row * 2 * CH;
+    const int mat = rem / CH, ch = rem - mat * CH;
+    const float4 v = *reinterpret_cast<const float4*>(&(mat == 0 ? Ok : Ov)[row * DP + 4 * ch]);
+    float* dst = dqkv + (long long)rows[row] * ld + (mat + 1) * C + head * D + 4 * ch;
+    const int pos = key_start + row;
+    if (pos < query_start || pos >= next_ks) {
+      atomicAdd(dst + 0, v.x);
+      atomicAdd(dst + 1, v.y);
+      atomicAdd(dst + 2, v.z);
+      atomicAdd(dst + 3, v.w);
+    } else {
+      *reinterpret_cast<float4*>(dst) = v;
+    }
+  }
+}
+
 // SFX_ATTN_SEQ=1: the pipelined kernel (window_attn_seq_kernel) on at most 512 workgroups, SFX_ATTN_SEQ=<n>
 // (n > 1) on at most n; default and 0: one (window, head) item per workgroup (window_attn_split_kernel), which
 // measured faster (config B 568 vs 553 renders/s at 768 / 1024 workgroups, profiles/r04_ab_bench.txt)
@@ -1598,10 +2090,12 @@ int sfx_window_attention_varlen_bwd(int num_windows, int max_window, int heads, 
   return sfx::check_launch("sfx_window_attention_varlen_bwd");
 }
 
-// dout [N, C] = d(attention output); dqkv [N, 3C] zero-filled by the caller (dK/dV accumulate)
+// dout [N, C] = d(attention output); attn_out [N, C] = the forward's output; dqkv [N, 3C] zero-filled by the caller
+// (dK/dV accumulate); stats: workspace of N * heads float4 (query pass -> key pass).  SFX_ATTN_PREC=fp32: the exact
+// single-kernel backward (attn_out and stats unused)
 int sfx_window_attention_bwd(int num_windows, int window, int heads, int head_dim, int channels, const float* qkv,
-                             const int* order, const int* win, float scale, const float* dout, float* dqkv,
-                             void* stream) {
+                             const int* order, const int* win, float scale, const float* attn_out, const float* dout,
+                             float* dqkv, float* stats, void* stream) {
   SFX_REQUIRE(num_windows >= 0, "sfx_window_attention_bwd: num_windows < 0");
   SFX_REQUIRE(window >= 1 && window <= KMAX, "sfx_window_attention_bwd: window must be in [1, 128]");
   SFX_REQUIRE(heads * head_dim == channels, "sfx_window_attention_bwd: heads * head_dim != channels");
@@ -1609,8 +2103,31 @@ int sfx_window_attention_bwd(int num_windows, int window, int heads, int head_di
               "sfx_window_attention_bwd: head_dim %d unsupported (16, 24, 32)", head_dim);
   if (num_windows == 0) return SFX_OK;
   SFX_REQUIRE(qkv && order && win && dout && dqkv, "sfx_window_attention_bwd: null buffer");
-  dim3 grid(num_windows, heads);
   hipStream_t st = sfx::as_stream(stream);
+  static int exact = -1;
+  if (exact < 0) {
+    const char* e = getenv("SFX_ATTN_PREC");
+    exact = (e && e[0] == 'f') ? 1 : 0;
+  }
+  if (!exact) {
+    SFX_REQUIRE(attn_out && stats, "sfx_window_attention_bwd: null attn_out / stats");
+    const long long nblk = ((long long)num_windows * heads + 7) / 8 * 8;
+    SFX_REQUIRE(nblk < (1ll << 31), "sfx_window_attention_bwd: too many windows");
+    float4* st4 = reinterpret_cast<float4*>(stats);
+#define SFX_ABWD(DD)                                                                                              \
+  do {                                                                                                            \
+    window_attn_bwd_q_kernel<DD><<<dim3((unsigned)nblk), 256, 0, st>>>(qkv, order, win, window, channels, scale,  \
+                                                                       attn_out, dout, dqkv, st4, num_windows);  \
+    window_attn_bwd_kv_kernel<DD><<<dim3((unsigned)nblk), 256, 0, st>>>(qkv, order, win, window, channels, scale, \
+                                                                        dout, dqkv, st4, num_windows);          \
+  } while (0)
+    if (head_dim == 16) SFX_ABWD(16);
+    else if (head_dim == 24) SFX_ABWD(24);
+    else SFX_ABWD(32);
+#undef SFX_ABWD
+    return sfx::check_launch("sfx_window_attention_bwd");
+  }
+  dim3 grid(num_windows, heads);
   if (head_dim == 16)
     window_attn_bwd_kernel<16><<<grid, 256, 0, st>>>(qkv, order, win, window, channels, scale, dout, dqkv);
   else if (head_dim == 24)

@@ -85,15 +85,14 @@ def block_forward(blk: Block, name: str, point: Point, masks: MaskFn, conv_in: O
         a = ops.window_attention(qkv, order, win, nw, K, blk.attn.num_heads, C)
     ma = masks(name + ".attn", n, blk.drop_prob, x.device)
     x2 = ops.linear(a, blk.attn.proj.weight, blk.attn.proj.bias, residual=x1, rowscale=ma)
-    del a
     h2 = ops.layernorm(x2, ln2.weight, ln2.bias, ln2.eps)
     z = torch.empty(n, mlp.fc1.weight.shape[0], device=x.device, dtype=torch.float32)
     m = ops.linear(h2, mlp.fc1.weight, mlp.fc1.bias, act=ops.ACT_GELU, pre_out=z, pre_before_act=True)
     del h2
     mm = masks(name + ".mlp", n, blk.drop_prob, x.device)
     point.feat = ops.linear(m, mlp.fc2.weight, mlp.fc2.bias, residual=x2, rowscale=mm, out=out)
-    return dict(kind="block", blk=blk, name=name, u=u, x1=x1, h=h, qkv=qkv, x2=x2, z=z, ma=ma, mm=mm, order=order,
-                win=win, nw=nw, K=K, smap=point.nbr, sep_conv_in=conv_in is not None)
+    return dict(kind="block", blk=blk, name=name, u=u, x1=x1, h=h, qkv=qkv, a=a, x2=x2, z=z, ma=ma, mm=mm,
+                order=order, win=win, nw=nw, K=K, smap=point.nbr, sep_conv_in=conv_in is not None)
 
 
 _TRACE: Optional[list] = None  # debugging: set to a list to record (tag, tensor) of the backward
@@ -123,8 +122,12 @@ def block_backward(rec: dict, dy: Tensor, need_input: bool):
     _trace(f"{nm}.dx2", dx2)
     del dh2
     da = tops.linear_bwd_data(dx2, wt(blk.attn.proj.weight), rowscale=rec["ma"])
-    bwd = tops.window_attention_varlen_bwd if blk.attn.enable_flash else tops.window_attention_bwd
-    dqkv = bwd(rec["qkv"], rec["order"], rec["win"], rec["nw"], rec["K"], blk.attn.num_heads, C, da)
+    if blk.attn.enable_flash:
+        dqkv = tops.window_attention_varlen_bwd(rec["qkv"], rec["order"], rec["win"], rec["nw"], rec["K"],
+                                                blk.attn.num_heads, C, da)
+    else:
+        dqkv = tops.window_attention_bwd(rec["qkv"], rec["order"], rec["win"], rec["nw"], rec["K"],
+                                         blk.attn.num_heads, C, da, attn_out=rec["a"])
     _trace(f"{nm}.da", da)
     _trace(f"{nm}.dqkv", dqkv)
     del da

@@ -22,7 +22,7 @@ _lib.register("sfx_linear_bwd_data", [I, I, I, P, L, P, L, P, I, I, P, L, P, L, 
 _lib.register("sfx_linear_wgrad", [I, I, I, P, L, P, L, P, L, P, P])
 _lib.register("sfx_transpose", [I, I, P, L, P, L, P])
 _lib.register("sfx_subm_conv_bwd_data", [I, I, I, P, L, P, P, P, P, P, P, P, L, P, P, P])
-_lib.register("sfx_window_attention_bwd", [I, I, I, I, I, P, P, P, F, P, P, P])
+_lib.register("sfx_window_attention_bwd", [I, I, I, I, I, P, P, P, F, P, P, P, P, P])
 _lib.register("sfx_window_attention_varlen_bwd", [I, I, I, I, I, P, P, P, F, P, P, P, P])
 _lib.register("sfx_layernorm_bwd", [I, I, P, L, P, P, L, P, L, F, P, L, P])
 _lib.register("sfx_cpe_ln_bwd", [I, I, P, P, P, P, P, P, F, P, P, P])
@@ -93,11 +93,22 @@ def subm_conv_bwd_data(dy: Tensor, smap, weight_t: Tensor, dx: Tensor) -> Tensor
 
 
 def window_attention_bwd(qkv: Tensor, order: Tensor, win: Tensor, num_windows: int, K: int, heads: int,
-                         channels: int, dout: Tensor) -> Tensor:
+                         channels: int, dout: Tensor, attn_out: Optional[Tensor] = None) -> Tensor:
+    """Backward of ptv3_ops.window_attention: query pass (dQ, per-query softmax statistics and dO.O from the
+    forward output `attn_out`, recomputed here when not given) then key pass (dK, dV), attention.hip."""
+    n = qkv.shape[0]
+    if qkv.shape != (n, 3 * channels) or dout.shape != (n, channels) or tuple(win.shape) != (num_windows, 2):
+        raise ValueError("window_attention_bwd: shape mismatch")
+    if attn_out is None:
+        from .ptv3_ops import window_attention
+        attn_out = window_attention(qkv, order, win, num_windows, K, heads, channels)
+    elif attn_out.shape != (n, channels) or not attn_out.is_contiguous():
+        raise ValueError("window_attention_bwd: attn_out must be a contiguous [N, C] tensor")
     dqkv = torch.zeros_like(qkv)
+    stats = torch.empty(max(n, 1) * heads * 4, device=qkv.device, dtype=torch.float32)
     d = channels // heads
     call("sfx_window_attention_bwd", num_windows, K, heads, d, channels, ptr(qkv), ptr(order, torch.int32),
-         ptr(win, torch.int32), float(d ** -0.5), ptr(dout), ptr(dqkv), stream())
+         ptr(win, torch.int32), float(d ** -0.5), ptr(attn_out), ptr(dout), ptr(dqkv), ptr(stats), stream())
     return dqkv
 
 

@@ -79,10 +79,16 @@ def test_subm_conv_bwd_data(device, n, cin, cout, dup):
     assert rel_l2(dx, x.grad + base) < 1e-5
 
 
-@pytest.mark.parametrize("n,heads,C", [(1000, 2, 64), (777, 4, 96), (300, 8, 128), (100, 2, 32), (1500, 16, 256)])
-def test_window_attention_bwd(device, n, heads, C):
+@pytest.mark.parametrize("n,heads,C,mag,gmag", [(1000, 2, 64, 1.0, 1.0), (777, 4, 96, 1.0, 1.0), (300, 8, 128, 1.0, 1.0),
+                                               (100, 2, 32, 1.0, 1.0), (1500, 16, 256, 1.0, 1.0),
+                                               (1000, 4, 64, 2.5, 1e4), (640, 4, 96, 1e-3, 1e-5),
+                                               (129, 4, 128, 1.0, 1.0)])
+def test_window_attention_bwd(device, n, heads, C, mag, gmag):
+    """Default (fp16x2 two-pass) backward vs fp32 autograd of the reference math: ragged last windows (keys in two
+    windows), a single short window (n < 128), peaked softmax (|qkv| x 2.5: logits std 6, large dO) and tiny operands (the
+    per-item power-of-two scales)."""
     g = torch.Generator().manual_seed(n + C)
-    qkv = torch.randn(n, 3 * C, generator=g, requires_grad=True)
+    qkv = (torch.randn(n, 3 * C, generator=g) * mag).requires_grad_()
     order = torch.randperm(n, generator=g)
     inverse = torch.empty_like(order)
     inverse[order] = torch.arange(n)
@@ -91,7 +97,7 @@ def test_window_attention_bwd(device, n, heads, C):
     q, k, v = qkv[order[pad]].reshape(-1, K, 3, heads, C // heads).permute(2, 0, 3, 1, 4).unbind(0)
     att = torch.softmax((q * (C // heads) ** -0.5) @ k.transpose(-2, -1), -1)
     ref = (att @ v).transpose(1, 2).reshape(-1, C)[unpad[inverse]]
-    dout = torch.randn(n, C, generator=g)
+    dout = torch.randn(n, C, generator=g) * gmag
     ref.backward(dout)
     tab = ops.window_table([n], K)
     win = torch.tensor(tab, dtype=torch.int32).to(device)

@@ -1,24 +1,16 @@
-"""Summarise a rocprofv3 rocpd SQLite database: per-kernel calls / total / avg (us)."""
-import sqlite3
+"""Summarise a rocprofv3 kernel_stats.csv: per-step ms, calls, average us, top-N kernels.
+usage: python tools/kstats.py <run_kernel_stats.csv> <steps> [top] [filter]"""
+import csv
 import sys
 
-
-def main(db, steps=None, top=40):
-    c = sqlite3.connect(db)
-    cols = [r[1] for r in c.execute("pragma table_info(kernels)")]
-    name_col = "kernel_name" if "kernel_name" in cols else ("name" if "name" in cols else cols[0])
-    rows = c.execute(f"select {name_col}, start, end from kernels").fetchall()
-    agg = {}
-    for n, s, e in rows:
-        a = agg.setdefault(n, [0, 0.0])
-        a[0] += 1
-        a[1] += (e - s) / 1e3
-    tot = sum(v[1] for v in agg.values())
-    print(f"{'calls':>7} {'total_us':>12} {'avg_us':>10} {'pct':>6}  kernel")
-    for n, (k, t) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:top]:
-        print(f"{k:7d} {t:12.1f} {t / k:10.2f} {100 * t / tot:6.2f}  {n[:110]}")
-    print(f"total kernel time {tot / 1e3:.2f} ms over {sum(v[0] for v in agg.values())} dispatches")
-
-
-if __name__ == "__main__":
-    main(sys.argv[1])
+rows = list(csv.DictReader(open(sys.argv[1])))
+steps = float(sys.argv[2])
+top = int(sys.argv[3]) if len(sys.argv) > 3 else 30
+flt = sys.argv[4] if len(sys.argv) > 4 else ""
+tot = sum(float(r["TotalDurationNs"]) for r in rows)
+print(f"total {tot / 1e6:.2f} ms, {tot / 1e6 / steps:.2f} ms per step")
+for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:top]:
+    if flt and flt not in r["Name"]:
+        continue
+    print(f"{float(r['TotalDurationNs']) / 1e6 / steps:8.2f} ms/step {int(r['Calls']) / steps:7.1f} calls "
+          f"{float(r['AverageNs']) / 1e3:8.1f} us  {r['Name'][:100]}")
