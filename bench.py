@@ -93,6 +93,8 @@ def parse(argv=None):
     ap.add_argument("--profile-only", action="store_true", help="skip roofline probe, traffic and CPU baseline")
     ap.add_argument("--markers", action="store_true",
                     help="launch sfx_profile_marker before every timed step and after the last (PMC passes)")
+    ap.add_argument("--gemm-calls", type=str, default=None,
+                    help="write the roofline probe's per-launch list (kind, shape, ms, TF/s; median pass) to this file")
     ap.add_argument("--dry-launch", action="store_true", help=argparse.SUPPRESS)  # launcher test: no GPU work
     a = ap.parse_args(argv)
     dflt = DEFAULTS[a.config]
@@ -242,7 +244,7 @@ class GemmTimer:
         return per
 
 
-def roofline_probe(unit_fn, passes=3):
+def roofline_probe(unit_fn, passes=3, dump=None):
     """achieved = algorithmic FLOP of every GEMM-family launch of one unit of work / their summed in-context
     durations; median over `passes` passes of the unit."""
     runs = []
@@ -254,6 +256,11 @@ def roofline_probe(unit_fn, passes=3):
     tot = [(sum(p[0] for p in r), r) for r in runs]
     tot.sort(key=lambda x: x[0])
     ms, per = tot[len(tot) // 2]
+    if dump:
+        with open(dump, "w") as f:
+            for p in per:
+                f.write(json.dumps({"kind": p[1], "shape": list(p[2]), "ms": round(p[0], 4),
+                                    "tflops": round(p[3] / max(p[0], 1e-9) / 1e9, 2)}) + "\n")
     fl = sum(p[3] for p in per)
     by = sum(p[4] for p in per)
     achieved = fl / (ms * 1e-3) / 1e12
@@ -583,7 +590,7 @@ def main(argv=None):
     if not args.profile_only:
         if not train:
             model.eval()
-        roof = roofline_probe(unit)
+        roof = roofline_probe(unit, dump=args.gemm_calls if rank == 0 else None)
         if rank == 0 and world == 1 and not args.no_traffic:
             tr_res, err = measure_traffic(args)
             if tr_res is not None:

@@ -200,9 +200,10 @@ int sfx_subm_conv_bwd_data(int n, int cin, int cout, const float* dy, long long 
                            int* centre_ws, float* dx, long long lddx, const float* wt_split, const float* wt_inv,
                            void* stream);
 /* non-flash SerializedAttention backward (visualize.py:140-179 math): dout [N, C] = grad of the attention
- * output rows; dqkv [N, 3C] must be zero-filled (dK/dV accumulate across overlapping windows).  (ABI v13)
- * attn_out [N, C] = the forward's output (Delta = dO . O), stats = workspace of N * heads * 4 floats, 16-byte
- * aligned (query pass -> key pass); both unused under SFX_ATTN_PREC=fp32 (the exact single-kernel backward). */
+ * output rows.  (ABI v13) attn_out [N, C] = the forward's output (Delta = dO . O), stats = workspace of
+ * N * heads * 4 floats, 16-byte aligned (query pass -> key pass); every element of dqkv [N, 3C] is written.
+ * Under SFX_ATTN_PREC=fp32 (the exact single-kernel backward) attn_out and stats are unused and dqkv must be
+ * zero-filled (dK/dV accumulate across overlapping windows). */
 int sfx_window_attention_bwd(int num_windows, int window, int heads, int head_dim, int channels, const float* qkv,
                              const int* order, const int* win, float scale, const float* attn_out, const float* dout,
                              float* dqkv, float* stats, void* stream);
@@ -243,6 +244,9 @@ int sfx_segment_sum(int m, int C, const int* idx_ptr, const int* sorted_idx, con
 /* dX = dY * act'(pre) on cols < ncols (1 GELU pre-act, 2 ReLU, 3 tanh given its output) */
 int sfx_act_bwd(int M, int N, const float* dY, long long ldgy, const float* pre, long long ldp, int act, int ncols,
                 float* dX, long long lddx, void* stream);
+/* (ABI v13) DropPath keep mask of n points (timm DropPath, pointtransformer_v3.py:145): out[i] = 1/keep or 0,
+ * Bernoulli(keep) from a counter-based hash of (seed, i) -- deterministic for a given seed */
+int sfx_drop_mask(long long n, float keep, unsigned long long seed, float* out, void* stream);
 /* clip_grad_norm_(max_norm) + torch.optim.Adam (train.py:292-302, utils/optimizers.py) */
 int sfx_sumsq(long long n, const float* x, double* out, void* stream);
 int sfx_clip_coef(const double* sumsq, float max_norm, float* coef, float* norm_out, void* stream);

@@ -1611,6 +1611,15 @@ window_attn_bwd_q_kernel(const float* __restrict__ qkv, const int* __restrict__ 
       *reinterpret_cast<uint4*>(lds + (rr >> 8) * RB + ((rr >> 7) & 1) * KMAX * QROW + bwd_row_off<KD>(rr & 127, D / 8)) =
           make_uint4(0, 0, 0, 0);
   __syncthreads();
+  // dqkv is not zero-filled by the caller: the key pass stores every key's dK / dV plainly except the keys a ragged
+  // last window shares with its predecessor (positions key_start .. query_start - 1), which both windows add
+  // atomically -- this window zeroes this head's slice of them here, a launch ahead of every key-pass add
+  for (int e = tid; e < (query_start - key_start) * 2 * (D / 4); e += 256) {
+    const int row = e / (2 * (D / 4)), rem = e - row * 2 * (D / 4);
+    const int mat = rem / (D / 4), ch = rem - mat * (D / 4);
+    *reinterpret_cast<float4*>(dqkv + (long long)rows[row] * ld + (mat + 1) * C + head * D + 4 * ch) =
+        make_float4(0.f, 0.f, 0.f, 0.f);
+  }
   // this lane's query: q and dO slices dd = 16 ks + 8h .. +7 (B operands of S^T and dP^T) and Delta = dO . O
   const int qi = 32 * wid + l32;
   const int qsrc = rows[qi];
@@ -2090,9 +2099,9 @@ int sfx_window_attention_varlen_bwd(int num_windows, int max_window, int heads, 
   return sfx::check_launch("sfx_window_attention_varlen_bwd");
 }
 
-// dout [N, C] = d(attention output); attn_out [N, C] = the forward's output; dqkv [N, 3C] zero-filled by the caller
-// (dK/dV accumulate); stats: workspace of N * heads float4 (query pass -> key pass).  SFX_ATTN_PREC=fp32: the exact
-// single-kernel backward (attn_out and stats unused)
+// dout [N, C] = d(attention output); attn_out [N, C] = the forward's output; dqkv [N, 3C] (every element written;
+// the exact kernel needs it zero-filled by the caller); stats: workspace of N * heads float4 (query pass -> key
+// pass).  SFX_ATTN_PREC=fp32: the exact single-kernel backward (attn_out and stats unused, dqkv zero-filled)
 int sfx_window_attention_bwd(int num_windows, int window, int heads, int head_dim, int channels, const float* qkv,
                              const int* order, const int* win, float scale, const float* attn_out, const float* dout,
                              float* dqkv, float* stats, void* stream) {

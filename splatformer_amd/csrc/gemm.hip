@@ -1313,6 +1313,119 @@ __global__ void __launch_bounds__(THREADS) wgrad_kernel(int M, int N, int K, con
   }
 }
 
+// bf16x3 form (default): the same reduction on v_mfma_f32_32x32x16_bf16 with both operands as three bf16 terms
+// (sfx::split3, the six leading term products: fp32 accuracy, no scaling) and 128 x 128 output tiles -- at 64 x 64
+// every dY column block is re-read K/64 times and every X column block N/64 times, which bound the exact kernel
+// (the (768, 256, 37759) qkv gradient moved ~0.93 GB for 0.15 GB of operands).  Staging: a thread loads 8 points
+// x 4 columns (coalesced row segments) and writes, per column and term, the 8 points as one 16-byte chunk of a
+// [column][32 points] bf16 image with 64-byte rows (chunk c of row r at c ^ ((r >> 2) & 3)), i.e. already in the
+// MFMA fragment order (lane = output row / column, 8 consecutive points per half-wave); the next slab's loads
+// are in flight while the current one is multiplied.
+constexpr int WG2_T = 128;  // output tile rows (n) and columns (k)
+constexpr int WG2_PLANE = WG2_T * 64;  // bytes of one term image
+
+__global__ void __launch_bounds__(256, 2) wgrad2_kernel(int M, int N, int K, const float* __restrict__ dY,
+                                                        long long ldy, const float* __restrict__ X, long long ldx,
+                                                        float* __restrict__ dW, long long ldw, int chunk,
+                                                        float* __restrict__ db) {
+  typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+  __shared__ __attribute__((aligned(16))) char img[2 * 3 * WG2_PLANE];  // [dY, X][term][128 rows][64 B]
+  const int tiles_k = (K + WG2_T - 1) / WG2_T;
+  const int n0 = (blockIdx.x / tiles_k) * WG2_T, k0 = (blockIdx.x % tiles_k) * WG2_T;
+  const int m_begin = blockIdx.y * chunk;
+  const int m_end = min(M, m_begin + chunk);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, h = lane >> 5, l32 = lane & 31;
+  const int wn = wid & 1, wk = wid >> 1;  // wave sub-tile: rows wn*64.., columns wk*64..
+  // staging role: operand op (0 dY, 1 X), column group c4 (4 columns), point group mg (8 points)
+  const int op = tid >> 7, c4 = tid & 31, mg = (tid >> 5) & 3;
+  const int col = (op ? k0 : n0) + 4 * c4;
+  const bool col_ok = col < (op ? K : N);
+  const __amdgpu_buffer_rsrc_t rS = rsrc(op ? X : dY);
+  const unsigned ld32 = (unsigned)(op ? ldx : ldy);
+  auto chunk_off = [](int r, int c) -> int { return r * 64 + (((c ^ (r >> 2)) & 3) << 4); };
+  const bool do_db = db != nullptr && k0 == 0 && op == 0;
+  float dbs[4] = {0.f, 0.f, 0.f, 0.f};
+
+  floatx16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  float4 v[8];
+  auto load = [&](int m0) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const int m = m0 + 8 * mg + r;
+      v[r] = bload4(rS, (m < m_end && col_ok) ? ((unsigned)m * ld32 + (unsigned)col) * 4u : OOB);
+    }
+  };
+  load(m_begin);
+  for (int m0 = m_begin; m0 < m_end; m0 += BK) {
+    __syncthreads();  // the previous slab's fragments have been read
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float4 lo = make_float4(((const float*)&v[0])[j], ((const float*)&v[1])[j], ((const float*)&v[2])[j],
+                                    ((const float*)&v[3])[j]);
+      const float4 hi = make_float4(((const float*)&v[4])[j], ((const float*)&v[5])[j], ((const float*)&v[6])[j],
+                                    ((const float*)&v[7])[j]);
+      if (do_db) dbs[j] += ((lo.x + lo.y) + (lo.z + lo.w)) + ((hi.x + hi.y) + (hi.z + hi.w));
+      uint2 t0[3], t1[3];
+      sfx::split3(lo, t0);
+      sfx::split3(hi, t1);
+      const int row = 4 * c4 + j;
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+        *reinterpret_cast<uint4*>(img + (op * 3 + q) * WG2_PLANE + chunk_off(row, mg)) =
+            make_uint4(t0[q].x, t0[q].y, t1[q].x, t1[q].y);
+    }
+    __syncthreads();
+    if (m0 + BK < m_end) load(m0 + BK);  // next slab in flight during the products
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {  // 16-point steps
+      bf16x8 af[2][3], bf[2][3];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+          af[i][q] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(
+                                                    img + q * WG2_PLANE + chunk_off(wn * 64 + i * 32 + l32, 2 * s + h)));
+          bf[i][q] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(
+                                                    img + (3 + q) * WG2_PLANE + chunk_off(wk * 64 + i * 32 + l32, 2 * s + h)));
+        }
+      constexpr int QA[6] = {2, 1, 0, 1, 0, 0}, QB[6] = {0, 1, 2, 0, 1, 0};  // smallest products first
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int p = 0; p < 6; ++p)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][QA[p]], bf[j][QB[p]], acc[i][j], 0, 0, 0);
+    }
+  }
+  if (do_db) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (col + j < N) atomicAdd(&db[col + j], dbs[j]);
+  }
+  const __amdgpu_buffer_rsrc_t rW = rsrc(dW);
+  const unsigned ldw32 = (unsigned)ldw;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int k = k0 + wk * 64 + j * 32 + l32;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int n = n0 + wn * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(
+            acc[i][j][r], rW, (n < N && k < K) ? ((unsigned)n * ldw32 + (unsigned)k) * 4u : OOB, 0, 0);
+      }
+    }
+}
+
 // dst[c][r] = src[r][c]
 __global__ void __launch_bounds__(256) transpose_kernel(int rows, int cols, const float* __restrict__ src,
                                                         long long lds, float* __restrict__ dst, long long ldd) {
@@ -1597,8 +1710,18 @@ int sfx_linear_wgrad(int M, int N, int K, const float* dY, long long ldy, const 
   SFX_REQUIRE(ldy >= N && ldx >= K && ldw >= K, "sfx_linear_wgrad: leading dim");
   SFX_REQUIRE(fits(M, ldy) && fits(M, ldx) && fits(N, ldw), "sfx_linear_wgrad: operand exceeds 2 GiB range");
   hipStream_t st = sfx::as_stream(stream);
-  const int tiles = (int)(sfx::ceil_div(N, WG_TILE) * sfx::ceil_div(K, WG_TILE));
   const int slabs = (int)sfx::ceil_div(M, BK);
+  if (split_mode(M) != 0) {  // bf16x3 terms, 128 x 128 tiles (SFX_GEMM_PREC=fp32: the exact kernel below)
+    const int tiles2 = (int)(sfx::ceil_div(N, WG2_T) * sfx::ceil_div(K, WG2_T));
+    int splits2 = (int)sfx::ceil_div(2 * num_cus(), tiles2);
+    if (splits2 > slabs) splits2 = slabs;
+    if (splits2 < 1) splits2 = 1;
+    const int chunk2 = (int)sfx::ceil_div(slabs, splits2) * BK;
+    splits2 = (int)sfx::ceil_div(M, chunk2);
+    wgrad2_kernel<<<dim3(tiles2, splits2), 256, 0, st>>>(M, N, K, dY, ldy, X, ldx, dW, ldw, chunk2, db);
+    return sfx::check_launch("sfx_linear_wgrad");
+  }
+  const int tiles = (int)(sfx::ceil_div(N, WG_TILE) * sfx::ceil_div(K, WG_TILE));
   int splits = (int)sfx::ceil_div(4 * num_cus(), tiles);
   if (splits > slabs) splits = slabs;
   if (splits < 1) splits = 1;

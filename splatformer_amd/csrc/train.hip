@@ -114,8 +114,114 @@ __global__ void __launch_bounds__(256) cpe_ln_bwd_kernel(int M, int C, const flo
   }
 }
 
+// Vectorised forms for C in {64, 96, 128, 256, 512} (norm.hip's layout): a row is held by G lanes, NV float4 per
+// lane, 64/G rows per wave -- 16-byte loads and log2(G)-step group reductions instead of one wave per row with
+// 4-byte loads and full-wave reductions (C = 64: 4x fewer reduction steps per row, no idle lanes).
+template <int G>
+__device__ __forceinline__ float gsum(float v) {
+#pragma unroll
+  for (int o = G / 2; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+template <int G, int NV>
+__device__ __forceinline__ void ln_bwd_row4(const float4 (&x)[NV], const float4 (&dy)[NV], const float* __restrict__ g,
+                                            float eps, int sub, float4 (&dx)[NV]) {
+  constexpr float inv_c = 1.f / (float)(4 * G * NV);
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) s += (x[i].x + x[i].y) + (x[i].z + x[i].w);
+  const float mean = gsum<G>(s) * inv_c;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const float a = x[i].x - mean, b = x[i].y - mean, c = x[i].z - mean, d = x[i].w - mean;
+    q += (a * a + b * b) + (c * c + d * d);
+  }
+  const float rstd = 1.f / sqrtf(gsum<G>(q) * inv_c + eps);
+  float4 xh[NV], gy[NV];
+  float a = 0.f, b = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const float4 gg = *reinterpret_cast<const float4*>(g + 4 * (sub + G * i));
+    xh[i] = make_float4((x[i].x - mean) * rstd, (x[i].y - mean) * rstd, (x[i].z - mean) * rstd,
+                        (x[i].w - mean) * rstd);
+    gy[i] = make_float4(dy[i].x * gg.x, dy[i].y * gg.y, dy[i].z * gg.z, dy[i].w * gg.w);
+    a += (gy[i].x + gy[i].y) + (gy[i].z + gy[i].w);
+    b += (gy[i].x * xh[i].x + gy[i].y * xh[i].y) + (gy[i].z * xh[i].z + gy[i].w * xh[i].w);
+  }
+  a = gsum<G>(a) * inv_c;
+  b = gsum<G>(b) * inv_c;
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+    dx[i] = make_float4(rstd * (gy[i].x - a - xh[i].x * b), rstd * (gy[i].y - a - xh[i].y * b),
+                        rstd * (gy[i].z - a - xh[i].z * b), rstd * (gy[i].w - a - xh[i].w * b));
+}
+__device__ __forceinline__ float4 add4(float4 a, float4 b) {
+  return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
+
+template <int G, int NV>
+__global__ void __launch_bounds__(256) layernorm_bwd4_kernel(int M, const float* __restrict__ X, long long ldx,
+                                                             const float* __restrict__ g, const float* __restrict__ dY,
+                                                             long long ldgy, const float* __restrict__ dR,
+                                                             long long ldr, float eps, float* __restrict__ dX,
+                                                             long long lddx) {
+  const int row = blockIdx.x * (256 / G) + threadIdx.x / G;
+  const int sub = threadIdx.x % G;
+  if (row >= M) return;
+  float4 x[NV], dy[NV], dx[NV];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    x[i] = *reinterpret_cast<const float4*>(X + (long long)row * ldx + 4 * (sub + G * i));
+    dy[i] = *reinterpret_cast<const float4*>(dY + (long long)row * ldgy + 4 * (sub + G * i));
+  }
+  ln_bwd_row4<G, NV>(x, dy, g, eps, sub, dx);
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    float4 o = dx[i];
+    if (dR) o = add4(o, *reinterpret_cast<const float4*>(dR + (long long)row * ldr + 4 * (sub + G * i)));
+    *reinterpret_cast<float4*>(dX + (long long)row * lddx + 4 * (sub + G * i)) = o;
+  }
+}
+
+template <int G, int NV>
+__global__ void __launch_bounds__(256) cpe_ln_bwd4_kernel(int M, const float* __restrict__ U,
+                                                          const float* __restrict__ X1, const float* __restrict__ g_cpe,
+                                                          const float* __restrict__ g1, const float* __restrict__ dX2,
+                                                          const float* __restrict__ dH, float eps,
+                                                          float* __restrict__ dX1, float* __restrict__ dU) {
+  constexpr int C = 4 * G * NV;
+  const int row = blockIdx.x * (256 / G) + threadIdx.x / G;
+  const int sub = threadIdx.x % G;
+  if (row >= M) return;
+  const long long o = (long long)row * C;
+  float4 x[NV], dy[NV], d1[NV], du[NV];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    x[i] = *reinterpret_cast<const float4*>(X1 + o + 4 * (sub + G * i));
+    dy[i] = *reinterpret_cast<const float4*>(dH + o + 4 * (sub + G * i));
+  }
+  ln_bwd_row4<G, NV>(x, dy, g1, eps, sub, d1);
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    d1[i] = add4(d1[i], *reinterpret_cast<const float4*>(dX2 + o + 4 * (sub + G * i)));
+    x[i] = *reinterpret_cast<const float4*>(U + o + 4 * (sub + G * i));
+  }
+  ln_bwd_row4<G, NV>(x, d1, g_cpe, eps, sub, du);
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    *reinterpret_cast<float4*>(dX1 + o + 4 * (sub + G * i)) = d1[i];
+    *reinterpret_cast<float4*>(dU + o + 4 * (sub + G * i)) = du[i];
+  }
+}
+
+__host__ __forceinline__ bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
 // ---- column reductions (BatchNorm statistics and its backward sums) ------------------------------------
-constexpr int COL_BLOCK_ROWS = 512;
+// 128 rows per workgroup: M / 128 workgroups (782 at 100k rows, > 3 per CU) with 8 independent loads in flight per
+// thread -- at 512 rows (196 workgroups for 100k rows, each thread a chain of 128 dependent-latency loads) the
+// reductions ran at ~0.3 of HBM bandwidth (12.6 ms per config-C step, profiles/r05_configC_kernel_top.txt)
+constexpr int COL_BLOCK_ROWS = 128;
 
 // mode 0: (sum x, sum x^2);  mode 1: (sum g, sum g*xhat) with g = dY * act'(BN(x)), xhat = (x-mean)*rstd
 __global__ void __launch_bounds__(256) colsum2_kernel(int mode, int M, int C, const float* __restrict__ X,
@@ -130,6 +236,7 @@ __global__ void __launch_bounds__(256) colsum2_kernel(int mode, int M, int C, co
   double s0 = 0.0, s1 = 0.0;
   if (c < C) {
     if (mode == 0) {
+#pragma unroll 8
       for (int m = m0 + sub; m < m1; m += 4) {
         const double v = X[(long long)m * ldx + c];
         s0 += v;
@@ -137,6 +244,7 @@ __global__ void __launch_bounds__(256) colsum2_kernel(int mode, int M, int C, co
       }
     } else {
       const float mu = mean[c], rs = rstd[c], ga = gamma[c], be = beta[c];
+#pragma unroll 8
       for (int m = m0 + sub; m < m1; m += 4) {
         const float xh = (X[(long long)m * ldx + c] - mu) * rs;
         float g = dY[(long long)m * ldgy + c];
@@ -291,6 +399,22 @@ __global__ void __launch_bounds__(256) act_bwd_kernel(int M, int N, const float*
   dX[(long long)m * lddx + c] = g;
 }
 
+// ---- DropPath keep masks ------------------------------------------------------------------------------
+// timm DropPath per point (reference pointtransformer_v3.py:145, drop_path=0.3 schedule): out[i] = 1/keep when
+// u_i < keep, else 0, with u_i uniform on [0, 1) in 2^-24 steps from a counter-based hash of (seed, i) (splitmix64
+// finaliser) -- one launch per mask instead of torch's rand + compare + cast + scale.
+__global__ void __launch_bounds__(256) drop_mask_kernel(long long n, float keep, unsigned long long seed,
+                                                        float* __restrict__ out) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  unsigned long long z = seed + (unsigned long long)(i + 1) * 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  const float u = (float)(z >> 40) * (1.f / 16777216.f);
+  out[i] = u < keep ? 1.f / keep : 0.f;
+}
+
 // ---- optimiser -----------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) sumsq_kernel(long long n, const float* __restrict__ x, double* __restrict__ out) {
   double s = 0.0;
@@ -340,8 +464,20 @@ int sfx_layernorm_bwd(int M, int C, const float* X, long long ldx, const float* 
   SFX_REQUIRE(M >= 0 && C > 0 && C <= 64 * MAXV, "sfx_layernorm_bwd: C must be in [1, 512]");
   if (M == 0) return SFX_OK;
   SFX_REQUIRE(X && gamma && dY && dX, "sfx_layernorm_bwd: null buffer");
-  layernorm_bwd_kernel<<<sfx::ceil_div(M, 4), 256, 0, sfx::as_stream(stream)>>>(M, C, X, ldx, gamma, dY, ldgy, dR,
-                                                                                 ldr, eps, dX, lddx);
+  hipStream_t st = sfx::as_stream(stream);
+  const bool v4 = al16(X) && al16(gamma) && al16(dY) && al16(dX) && (!dR || al16(dR)) && ldx % 4 == 0 &&
+                  ldgy % 4 == 0 && lddx % 4 == 0 && (!dR || ldr % 4 == 0);
+#define SFX_LNB4(G, NV)                                                                                      \
+  layernorm_bwd4_kernel<G, NV><<<sfx::ceil_div(M, 256 / G), 256, 0, st>>>(M, X, ldx, gamma, dY, ldgy, dR, ldr, \
+                                                                          eps, dX, lddx)
+  if (v4 && C == 64) SFX_LNB4(16, 1);
+  else if (v4 && C == 96) SFX_LNB4(8, 3);
+  else if (v4 && C == 128) SFX_LNB4(32, 1);
+  else if (v4 && C == 256) SFX_LNB4(64, 1);
+  else if (v4 && C == 512) SFX_LNB4(64, 2);
+  else
+    layernorm_bwd_kernel<<<sfx::ceil_div(M, 4), 256, 0, st>>>(M, C, X, ldx, gamma, dY, ldgy, dR, ldr, eps, dX, lddx);
+#undef SFX_LNB4
   return sfx::check_launch("sfx_layernorm_bwd");
 }
 
@@ -350,8 +486,20 @@ int sfx_cpe_ln_bwd(int M, int C, const float* U, const float* X1, const float* g
   SFX_REQUIRE(M >= 0 && C > 0 && C <= 64 * MAXV, "sfx_cpe_ln_bwd: C must be in [1, 512]");
   if (M == 0) return SFX_OK;
   SFX_REQUIRE(U && X1 && gamma_cpe && gamma1 && dX2 && dH && dX1 && dU, "sfx_cpe_ln_bwd: null buffer");
-  cpe_ln_bwd_kernel<<<sfx::ceil_div(M, 4), 256, 0, sfx::as_stream(stream)>>>(M, C, U, X1, gamma_cpe, gamma1, dX2,
-                                                                              dH, eps, dX1, dU);
+  hipStream_t st = sfx::as_stream(stream);
+  const bool v4 = al16(U) && al16(X1) && al16(gamma_cpe) && al16(gamma1) && al16(dX2) && al16(dH) && al16(dX1) &&
+                  al16(dU);
+#define SFX_CPEB4(G, NV)                                                                                       \
+  cpe_ln_bwd4_kernel<G, NV><<<sfx::ceil_div(M, 256 / G), 256, 0, st>>>(M, U, X1, gamma_cpe, gamma1, dX2, dH, eps, \
+                                                                       dX1, dU)
+  if (v4 && C == 64) SFX_CPEB4(16, 1);
+  else if (v4 && C == 96) SFX_CPEB4(8, 3);
+  else if (v4 && C == 128) SFX_CPEB4(32, 1);
+  else if (v4 && C == 256) SFX_CPEB4(64, 1);
+  else if (v4 && C == 512) SFX_CPEB4(64, 2);
+  else
+    cpe_ln_bwd_kernel<<<sfx::ceil_div(M, 4), 256, 0, st>>>(M, C, U, X1, gamma_cpe, gamma1, dX2, dH, eps, dX1, dU);
+#undef SFX_CPEB4
   return sfx::check_launch("sfx_cpe_ln_bwd");
 }
 
@@ -472,6 +620,14 @@ int sfx_clip_coef(const double* sumsq, float max_norm, float* coef, float* norm_
   SFX_REQUIRE(sumsq && coef, "sfx_clip_coef: null buffer");
   clip_coef_kernel<<<1, 1, 0, sfx::as_stream(stream)>>>(sumsq, max_norm, coef, norm_out);
   return sfx::check_launch("sfx_clip_coef");
+}
+
+int sfx_drop_mask(long long n, float keep, unsigned long long seed, float* out, void* stream) {
+  SFX_REQUIRE(n >= 0 && keep > 0.f && keep <= 1.f, "sfx_drop_mask: bad args");
+  if (n == 0) return SFX_OK;
+  SFX_REQUIRE(out, "sfx_drop_mask: null buffer");
+  drop_mask_kernel<<<sfx::ceil_div(n, 256), 256, 0, sfx::as_stream(stream)>>>(n, keep, seed, out);
+  return sfx::check_launch("sfx_drop_mask");
 }
 
 int sfx_adam_step(long long n, float* param, const float* grad, float* exp_avg, float* exp_avg_sq,

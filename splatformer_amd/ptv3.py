@@ -149,7 +149,7 @@ class Block(nn.Module):
         ln_c = self.cpe[2]
         ln1 = self.norm1[0]
         xc = x if conv_in is None else conv_in
-        if ops.subm_fused_ok(C):
+        if ops.subm_fused_ok(C, x.shape[0]):
             # conv + LN_cpe + shortcut + norm1 in one launch, pair products summed on chip (csrc/subm_fused.hip)
             wpk, winv, bf = self.cpe_packed()
             x1, h = ops.subm_cpe_ln(xc, x, point.nbr, wpk, winv, bf, ln_c.weight, ln_c.bias, ln1.weight, ln1.bias,
@@ -373,11 +373,11 @@ class PointTransformerV3(nn.Module):
         self.last_perms.append(p)
         return p
 
-    def stage_needs_pairs(self, s: int) -> bool:
-        """Whether an eval forward reads stage s's SubM pair lists: not when every Block on that map (encoder stage
-        s, decoder stage s) runs the fused conv, which reads the neighbour table only."""
+    def stage_needs_pairs(self, s: int, n: Optional[int] = None) -> bool:
+        """Whether an eval forward reads stage s's SubM pair lists (n points): not when every Block on that map
+        (encoder stage s, decoder stage s) runs the fused conv, which reads the neighbour table only."""
         chans = [self.enc_channels[s]] + ([self.dec_channels[s]] if s < len(self.dec_channels) else [])
-        return not all(ops.subm_fused_ok(c) for c in chans)
+        return not all(ops.subm_fused_ok(c, n) for c in chans)
 
     def prepare(self, data_dict, perms: Optional[List[Sequence[int]]] = None, pairs: bool = True,
                 reorder: bool = False) -> Point:
@@ -442,7 +442,7 @@ class PointTransformerV3(nn.Module):
             emb_feat = ops.point_embed(feat, emb.weight, emb.bias, sc, sh)
         else:
             emb_feat = ops.linear(feat, emb.weight, emb.bias, scale=sc, shift=sh, act=ops.ACT_GELU)
-        point = self.prepare(data_dict, perms, pairs=self.stage_needs_pairs(0), reorder=reorder)
+        point = self.prepare(data_dict, perms, pairs=self.stage_needs_pairs(0, feat.shape[0]), reorder=reorder)
         perm = point.get("perm")
         point.feat = emb_feat if perm is None else ops.move_rows(emb_feat, perm)
         final_out = out
@@ -466,7 +466,7 @@ class PointTransformerV3(nn.Module):
                 if name == "down":
                     m = counts_rd.get()[k - 1] if counts_rd is not None else None
                     point = mod.run(point, self._draw_perm(perms, k), m=m, deferred=deferred,
-                                    pairs=self.stage_needs_pairs(s))
+                                    pairs=self.stage_needs_pairs(s, m))
                     k += 1
                 else:
                     point = mod.run(point)

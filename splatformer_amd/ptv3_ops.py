@@ -704,16 +704,26 @@ def subm_partials_ok(x: Tensor, smap: "SubmMap", cout: int) -> bool:
 
 
 # Block.cpe + shortcut + norm1 of the eval forward in one launch, the conv summed in MFMA registers over all 27
-# offsets (csrc/subm_fused.hip) -- opt-in (SFX_SUBM_FUSED=1): measured slower than the offset-major pair GEMM +
-# pair-sum LayerNorm on every config-B stage (profiles/r05_subm_fused_stages.txt)
-SUBM_FUSED = os.environ.get("SFX_SUBM_FUSED", "0") == "1"
+# offsets (csrc/subm_fused.hip).  Default ("auto"): on maps of at least SUBM_FUSED_MIN_ROWS points at C <= 128, where
+# it beats the offset-major pair GEMM + pair-sum LayerNorm (config-E stages 0-2: 12-28 % faster per conv; the smaller
+# maps of config B and every C = 256 map measured slower -- profiles/r05_subm_fused_sizes.txt).
+# SFX_SUBM_FUSED=1: on every map whose C is in SFX_SUBM_FUSED_CHANNELS; SFX_SUBM_FUSED=0: never.
+SUBM_FUSED_MODE = os.environ.get("SFX_SUBM_FUSED", "auto")
+SUBM_FUSED_MIN_ROWS = int(os.environ.get("SFX_SUBM_FUSED_MIN_ROWS", "120000"))
+SUBM_FUSED_AUTO_MAX_C = 128
 SUBM_FUSED_KERNELS = (64, 96, 128, 256)  # the channel counts sfx_subm_cpe_ln has kernels for
 SUBM_FUSED_CHANNELS = tuple(int(c) for c in os.environ.get("SFX_SUBM_FUSED_CHANNELS", "64,96,128,256").split(",")
                             if c and int(c) in SUBM_FUSED_KERNELS)
 
 
-def subm_fused_ok(C: int) -> bool:
-    return SUBM_FUSED and C in SUBM_FUSED_CHANNELS
+def subm_fused_ok(C: int, n: Optional[int] = None) -> bool:
+    """Whether an eval Block on a map of n points with C channels runs sfx_subm_cpe_ln (n None: unknown size,
+    the auto rule then says no)."""
+    if SUBM_FUSED_MODE == "0" or C not in SUBM_FUSED_CHANNELS:
+        return False
+    if SUBM_FUSED_MODE == "1":
+        return True
+    return n is not None and n >= SUBM_FUSED_MIN_ROWS and C <= SUBM_FUSED_AUTO_MAX_C
 
 
 def subm_cpe_pack(wf: Tensor) -> Tuple[Tensor, Tensor]:

@@ -46,14 +46,18 @@ def wt(w: Tensor) -> Tensor:
 
 
 def device_drop_masks(generator: Optional[torch.Generator] = None) -> MaskFn:
-    """timm DropPath per point: keep ~ Bernoulli(1-p), scaled by 1/(1-p); None when p == 0 (Identity)."""
+    """timm DropPath per point: keep ~ Bernoulli(1-p), scaled by 1/(1-p); None when p == 0 (Identity).  One
+    sfx_drop_mask launch per mask; the hash seeds come from the generator's seed and a host-side draw counter
+    (reproducible for a seeded generator, no device read)."""
+    base = int(generator.initial_seed()) if generator is not None else int(torch.initial_seed())
+    state = {"k": 0}
 
     def fn(name: str, n: int, p: float, device=None) -> Optional[Tensor]:
         if p <= 0.0:
             return None
-        keep = 1.0 - p
-        r = torch.rand(n, device=device, generator=generator)
-        return (r < keep).float().div_(keep)
+        state["k"] += 1
+        seed = (base * 0x9E3779B97F4A7C15 + state["k"] * 0xD1B54A32D192ED03) & 0xFFFFFFFFFFFFFFFF
+        return tops.drop_mask(n, 1.0 - p, seed, device)
     return fn
 
 

@@ -7,6 +7,7 @@ Same rules as ptv3_ops: torch allocates, HIP computes, no CPU fallback.
 from __future__ import annotations
 
 import ctypes as C
+import os
 from typing import Optional, Tuple
 
 import torch
@@ -39,8 +40,10 @@ _lib.register("sfx_act_bwd", [I, I, P, L, P, L, I, I, P, L, P])
 _lib.register("sfx_sumsq", [L, P, P, P])
 _lib.register("sfx_clip_coef", [P, F, P, P, P])
 _lib.register("sfx_adam_step", [L, P, P, P, P, P, F, F, F, F, F, I, P])
+_lib.register("sfx_drop_mask", [L, F, C.c_ulonglong, P, P])
 
 DACT_NONE, DACT_GELU, DACT_RELU, DACT_TANH_OUT = 0, 1, 2, 3
+_ATTN_EXACT = os.environ.get("SFX_ATTN_PREC", "")[:1] == "f"  # (read once, as attention.hip does)
 
 
 def transpose(x: Tensor) -> Tensor:
@@ -104,7 +107,8 @@ def window_attention_bwd(qkv: Tensor, order: Tensor, win: Tensor, num_windows: i
         attn_out = window_attention(qkv, order, win, num_windows, K, heads, channels)
     elif attn_out.shape != (n, channels) or not attn_out.is_contiguous():
         raise ValueError("window_attention_bwd: attn_out must be a contiguous [N, C] tensor")
-    dqkv = torch.zeros_like(qkv)
+    # the two-pass backward writes every element; the exact kernel (SFX_ATTN_PREC=fp32) accumulates into zeros
+    dqkv = torch.zeros_like(qkv) if _ATTN_EXACT else torch.empty_like(qkv)
     stats = torch.empty(max(n, 1) * heads * 4, device=qkv.device, dtype=torch.float32)
     d = channels // heads
     call("sfx_window_attention_bwd", num_windows, K, heads, d, channels, ptr(qkv), ptr(order, torch.int32),
@@ -279,6 +283,13 @@ def act_bwd(dy: Tensor, pre: Tensor, act: int, ncols: int = -1, out: Optional[Te
     pp, ldp = _rows(pre)
     po, ldo = _rows(out)
     call("sfx_act_bwd", M, N, pd, ldd, pp, ldp, act, N if ncols < 0 else ncols, po, ldo, stream())
+    return out
+
+
+def drop_mask(n: int, keep: float, seed: int, device) -> Tensor:
+    """DropPath keep mask [n]: 1/keep with probability keep, else 0 (sfx_drop_mask, deterministic in seed)."""
+    out = torch.empty(n, device=device, dtype=torch.float32)
+    call("sfx_drop_mask", n, float(keep), seed & 0xFFFFFFFFFFFFFFFF, ptr(out), stream())
     return out
 
 

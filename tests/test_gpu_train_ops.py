@@ -45,7 +45,8 @@ def test_linear_bwd_data(device, M, N, K, dact):
     assert rel_l2(out, ref + base) < 2e-6
 
 
-@pytest.mark.parametrize("M,N,K", [(100000, 192, 64), (777, 384, 128), (33, 1536, 512)])
+@pytest.mark.parametrize("M,N,K", [(100000, 192, 64), (777, 384, 128), (33, 1536, 512), (37759, 768, 256),
+                                   (5003, 100, 36), (40, 288, 96)])
 def test_linear_wgrad(device, M, N, K):
     g = torch.Generator().manual_seed(N)
     dy = torch.randn(M, N, generator=g)
@@ -133,7 +134,7 @@ def test_window_attention_varlen_bwd(device, K, heads, C):
 
 def test_layernorm_bwd_ops(device):
     g = torch.Generator().manual_seed(3)
-    for C in (64, 96, 256, 512):
+    for C in (64, 96, 128, 256, 512, 48):
         M = 999
         x = (torch.randn(M, C, generator=g) * 2 + 0.5).requires_grad_()
         ga, be = torch.randn(C, generator=g), torch.randn(C, generator=g)
@@ -238,3 +239,21 @@ def test_act_bwd_and_adam(device):
             tops.adam_step(p, gr, a, b, step, 3e-5, eps=1e-15, grad_scale=coef)
     for p, r in zip(dev_p, ref_p):
         assert rel_l2(p, r) < 1e-6
+
+
+def test_drop_mask(device):
+    """sfx_drop_mask: values in {0, 1/keep}, keep fraction within 5 sigma, deterministic per seed."""
+    n, keep = 200_000, 0.7
+    a = tops.drop_mask(n, keep, 12345, device)
+    b = tops.drop_mask(n, keep, 12345, device)
+    c = tops.drop_mask(n, keep, 12346, device)
+    assert torch.equal(a, b) and not torch.equal(a, c)
+    vals = set(torch.unique(a).tolist())
+    assert vals <= {0.0, float(torch.tensor(1.0) / torch.tensor(keep))}
+    frac = float((a > 0).float().mean())
+    sigma = (keep * (1 - keep) / n) ** 0.5
+    assert abs(frac - keep) < 5 * sigma, frac
+    # neighbouring elements are not correlated (the hash decorrelates consecutive counters)
+    k = (a > 0).float()
+    both = float((k[1:] * k[:-1]).mean())
+    assert abs(both - keep * keep) < 0.01

@@ -1,7 +1,7 @@
 """Eval-path SubM CPE on the config-B stage geometries: the register-summed fused kernel (sfx_subm_cpe_ln, with its
 per-conv row-exponent pass) against the offset-major pair GEMM + pair-sum LayerNorm, per stage (HIP events, median
 of 20), plus the map's row-order build and the active (16-point group, offset) fraction of the fused kernel.
-usage: python tools/subm_bench.py [--only C]"""
+usage: python tools/subm_bench.py [--only C] [--n POINTS]"""
 import argparse
 import os
 import statistics
@@ -35,11 +35,12 @@ def timeit(fn, reps=20):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", type=int, default=None)
+    ap.add_argument("--n", type=int, default=100000)
     args = ap.parse_args()
     _lib.load()
     dev = torch.device("cuda:0")
     g = torch.Generator().manual_seed(0)
-    grid0 = torch.floor(make_scene(100000, 1, seed=0)["means"] * 384).long()
+    grid0 = torch.floor(make_scene(args.n, 1, seed=0)["means"] * 384).long()
     for s, shift, chans in STAGES:
         grid = grid0 if shift is None else torch.unique(grid0 >> shift, dim=0)
         n = grid.shape[0]
