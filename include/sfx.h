@@ -470,6 +470,16 @@ int sfx_mlp_pack(int C, const float* w1, const float* b1, const float* w2, const
                  const float* beta, float* stream, float* params, int* workspace, void* stream_);
 int sfx_block_mlp(int M, int C, const float* x, long long ldx, const float* stream, const float* params, float eps,
                   float* y, long long ldy, void* stream_);
+/* (ABI v13) training forward of the same tail (train.py:240-289, model.train()): also stores z [M][4C] (contiguous)
+ * = fc1(LN2(x)), the pre-activation the backward needs, and applies the DropPath keep factor rowscale [M] (NULL:
+ * none) to the branch: y = x + rowscale * (fc2(GELU(z)) + b2). */
+int sfx_block_mlp_train(int M, int C, const float* x, long long ldx, const float* stream, const float* params,
+                        float eps, const float* rowscale, float* z, float* y, long long ldy, void* stream_);
+/* (ABI v13) its backward up to LN2: dh2 = W1^T (GELU'(z) o W2^T (rowscale * dy)), stream / params packed by
+ * sfx_mlp_pack(C, W2^T [4C][C], zeros(4C), W1^T [C][4C], zeros(C), gamma, beta); LN2's backward + the residual are
+ * the caller's (sfx_layernorm_bwd with dR = dy). */
+int sfx_block_mlp_bwd(int M, int C, const float* dy, long long lddy, const float* stream, const float* params,
+                      const float* rowscale, const float* z, float* dh2, long long lddh, void* stream_);
 
 /* (ABI v11) Block.cpe + shortcut + norm1 in one launch (reference calflops.py:45-53: x1 = x + LN_cpe(Linear(
  * SubMConv3d(x))), h = norm1(x1); Pointcept Block.cpe = spconv SubMConv3d k=3 -> Linear -> LayerNorm), the

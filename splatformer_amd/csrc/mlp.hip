@@ -91,10 +91,37 @@ __device__ __forceinline__ void wait_vm_lgkm() {
 // LDS at the end (cn 0 + cn 1, a fixed order).  Twice the waves per point: at C = 256 (37759 points, one 512-register
 // wave per SIMD) 1180 whole-tile waves over 1024 SIMDs take two full rounds, 2360 half-work waves take three half
 // rounds.
-template <int C, int WAVES, int RING, bool HS = false>
+// KIND (training, configs C/D -- the same dataflow, other operands):
+//   MLP_EVAL  Y = X + fc2(GELU(fc1(LN2(X))));
+//   MLP_TRAIN the training forward: also stores the pre-activation Z = fc1(LN2(X)) [M, 4C] for the backward, and
+//             scales the branch by the DropPath keep mask: Y = X + rs[p] (fc2(GELU(Z)) + b2);
+//   MLP_BWD   the branch's input gradient before LN2's backward: Y = W1^T (GELU'(Z) o (W2^T (rs[p] dY))) -- packed
+//             with W2^T in fc1's place and W1^T in fc2's (zero biases, sfx_block_mlp_bwd_pack), X = dY, no
+//             LayerNorm, Z read back instead of stored; hidden bound ||rs dY|| max_u ||W2[:, u]|| max|GELU'|.
+enum MlpKind { MLP_EVAL = 0, MLP_TRAIN = 1, MLP_BWD = 2 };
+
+// GELU'(z) = Phi(z) + z phi(z) with gelu_erf's fitted Phi (one exp2 for the tail, one for the density): ~20 VALU,
+// branch-free, against erff + expf (gelu_erf_grad) whose branches and temporaries spill the C = 96 backward tile
+__device__ __forceinline__ float gelu_grad_fit(float x) {
+  const float t = fminf(fabsf(x), 5.65f);
+  float q = 2.79405867e-06f;
+  q = __builtin_fmaf(q, t, -3.89084234e-05f);
+  q = __builtin_fmaf(q, t, 0.000184072458f);
+  q = __builtin_fmaf(q, t, 0.000141672252f);
+  q = __builtin_fmaf(q, t, -0.00706906663f);
+  q = __builtin_fmaf(q, t, 0.0524996631f);
+  q = __builtin_fmaf(q, t, 0.459207207f);
+  q = __builtin_fmaf(q, t, 1.15110528f);
+  const float half_tail = 0.5f * __builtin_amdgcn_exp2f(-(t * q));
+  const float phi_cdf = x >= 0.f ? 1.f - half_tail : half_tail;
+  return phi_cdf + x * (0.39894228040143268f * __builtin_amdgcn_exp2f(-0.72134752044448170f * x * x));
+}
+
+template <int C, int WAVES, int RING, bool HS = false, int KIND = MLP_EVAL>
 __global__ void __launch_bounds__(WAVES * 64, (WAVES == 4 && C > 128) ? 1 : 2)
     mlp_kernel(int M, const float* __restrict__ X, long long ldx, const float* __restrict__ stream,
-               const float* __restrict__ par, float eps, float* __restrict__ Y, long long ldy, int rot) {
+               const float* __restrict__ par, float eps, float* __restrict__ Y, long long ldy, int rot,
+               const float* __restrict__ rowscale, float* __restrict__ Z) {
   using G = MlpGeom<C>;
   constexpr int PTS = HS ? WAVES * 16 : WAVES * 32;  // points per workgroup
   constexpr int NB = G::NB, NP = G::NP, PPC = G::PPC, NT = C / 16;  // NT: fc1 k-steps
@@ -143,19 +170,24 @@ __global__ void __launch_bounds__(WAVES * 64, (WAVES == 4 && C > 128) ? 1 : 2)
     v[2 * t] = bload4(rX, pok ? (xr + c) * 4u : OOB);
     v[2 * t + 1] = bload4(rX, pok ? (xr + c + 4u) * 4u : OOB);
   }
-  float sm = 0.f;
+  // the DropPath keep factor of this point (training kinds; 1 without a mask, 0 past M)
+  const float rsp = (KIND != MLP_EVAL && rowscale) ? (pok ? rowscale[prow] : 0.f) : 1.f;
+  float mean = 0.f, rstd = 1.f;
+  if constexpr (KIND != MLP_BWD) {
+    float sm = 0.f;
 #pragma unroll
-  for (int i = 0; i < 2 * NT; ++i) sm += (v[i].x + v[i].y) + (v[i].z + v[i].w);
-  sm += __shfl_xor(sm, 32, 64);
-  const float mean = sm / (float)C;
-  float q2 = 0.f;
+    for (int i = 0; i < 2 * NT; ++i) sm += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+    sm += __shfl_xor(sm, 32, 64);
+    mean = sm / (float)C;
+    float q2 = 0.f;
 #pragma unroll
-  for (int i = 0; i < 2 * NT; ++i) {
-    const float a = v[i].x - mean, b = v[i].y - mean, c = v[i].z - mean, d = v[i].w - mean;
-    q2 += (a * a + b * b) + (c * c + d * d);
+    for (int i = 0; i < 2 * NT; ++i) {
+      const float a = v[i].x - mean, b = v[i].y - mean, c = v[i].z - mean, d = v[i].w - mean;
+      q2 += (a * a + b * b) + (c * c + d * d);
+    }
+    q2 += __shfl_xor(q2, 32, 64);
+    rstd = 1.f / sqrtf(q2 / (float)C + eps);
   }
-  q2 += __shfl_xor(q2, 32, 64);
-  const float rstd = 1.f / sqrtf(q2 / (float)C + eps);
   __syncthreads();  // s_par visible (no DMA is waited for here: only plain stores precede it)
   float mx = 0.f, nrm = 0.f;
 #pragma unroll
@@ -163,11 +195,15 @@ __global__ void __launch_bounds__(WAVES * 64, (WAVES == 4 && C > 128) ? 1 : 2)
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int c = 16 * t + 8 * h + 4 * u;
-      const float4 g = *reinterpret_cast<const float4*>(s_par + c);
-      const float4 b = *reinterpret_cast<const float4*>(s_par + C + c);
       float4& w = v[2 * t + u];
-      w = make_float4((w.x - mean) * rstd * g.x + b.x, (w.y - mean) * rstd * g.y + b.y,
-                      (w.z - mean) * rstd * g.z + b.z, (w.w - mean) * rstd * g.w + b.w);
+      if constexpr (KIND != MLP_BWD) {
+        const float4 g = *reinterpret_cast<const float4*>(s_par + c);
+        const float4 b = *reinterpret_cast<const float4*>(s_par + C + c);
+        w = make_float4((w.x - mean) * rstd * g.x + b.x, (w.y - mean) * rstd * g.y + b.y,
+                        (w.z - mean) * rstd * g.z + b.z, (w.w - mean) * rstd * g.w + b.w);
+      } else {  // dY of the branch output = rs[p] * dY
+        w = make_float4(w.x * rsp, w.y * rsp, w.z * rsp, w.w * rsp);
+      }
       mx = fmaxf(mx, fmaxf(fmaxf(fabsf(w.x), fabsf(w.y)), fmaxf(fabsf(w.z), fabsf(w.w))));
       nrm += (w.x * w.x + w.y * w.y) + (w.z * w.z + w.w * w.w);
     }
@@ -176,8 +212,10 @@ __global__ void __launch_bounds__(WAVES * 64, (WAVES == 4 && C > 128) ? 1 : 2)
   int e = 0;
   if (mx > 0.f && mx <= 3.4028235e38f) e = row_exp(mx) + 1;  // row max in [2^13, 2^14)
   const float sc = ldexpf(1.f, e), sinv = ldexpf(1.f, -e);
-  // hidden bound: |GELU(z)| <= max(|z|, 0.17), |z| <= ||h2|| max||W1_u|| + max|b1| (1.001: the sums' rounding)
-  const float U = fmaxf((sqrtf(nrm) * s_par[12 * C] + s_par[12 * C + 1]) * 1.001f, 0.17f);
+  // hidden bound: |GELU(z)| <= max(|z|, 0.17), |z| <= ||h2|| max||W1_u|| + max|b1| (1.001: the sums' rounding);
+  // backward: |GELU'(z) (W2^T dy)_u| <= 1.13 ||dy|| max_u ||W2[:, u]|| (max GELU' = 1.129 at z = sqrt 2)
+  const float U = KIND == MLP_BWD ? fmaxf(sqrtf(nrm) * s_par[12 * C] * (1.13f * 1.001f), 1e-30f)
+                                  : fmaxf((sqrtf(nrm) * s_par[12 * C] + s_par[12 * C + 1]) * 1.001f, 0.17f);
   int et = 0;
   if (U <= 3.4028235e38f) et = row_exp(U) + 2;  // bound in [2^14, 2^15)
   const float tsc = ldexpf(1.f, et), tinv = ldexpf(1.f, -et);
@@ -234,11 +272,37 @@ __global__ void __launch_bounds__(WAVES * 64, (WAVES == 4 && C > 128) ? 1 : 2)
           const float4* pp =
               reinterpret_cast<const float4*>(s_par + 2 * C + 2 * fc1_par_index(j, HS ? cn : cb, h, 0));
           float g[16];
+          // Z row of this lane's point: registers 4 q .. 4 q + 3 are units 64 j + 32 cb' + 8 q + 4 h + 0..3
+          float* zrow = Z + (size_t)(pok ? prow : 0) * (4 * C) + 64 * j + 32 * (HS ? cn : cb) + 4 * h;
+          if constexpr (KIND == MLP_BWD) {
+            float4 zq[4];
 #pragma unroll
-          for (int i2 = 0; i2 < 8; ++i2) {
-            const float4 wb = pp[i2];  // (1/s_u, b1_u) of registers 2 i2, 2 i2 + 1
-            g[2 * i2 + 0] = gelu_erf(acc1[cb][2 * i2 + 0] * (sinv * wb.x) + wb.y) * tsc;
-            g[2 * i2 + 1] = gelu_erf(acc1[cb][2 * i2 + 1] * (sinv * wb.z) + wb.w) * tsc;
+            for (int q = 0; q < 4; ++q)
+              zq[q] = pok ? *reinterpret_cast<const float4*>(zrow + 8 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+            for (int i2 = 0; i2 < 8; ++i2) {
+              const float4 wb = pp[i2];  // (1/s_u, 0) of registers 2 i2, 2 i2 + 1
+              const float4 zz = zq[i2 >> 1];
+              g[2 * i2 + 0] = acc1[cb][2 * i2 + 0] * (sinv * wb.x) * gelu_grad_fit((i2 & 1) ? zz.z : zz.x) * tsc;
+              g[2 * i2 + 1] = acc1[cb][2 * i2 + 1] * (sinv * wb.z) * gelu_grad_fit((i2 & 1) ? zz.w : zz.y) * tsc;
+            }
+          } else {
+            float pre[16];
+#pragma unroll
+            for (int i2 = 0; i2 < 8; ++i2) {
+              const float4 wb = pp[i2];  // (1/s_u, b1_u) of registers 2 i2, 2 i2 + 1
+              pre[2 * i2 + 0] = acc1[cb][2 * i2 + 0] * (sinv * wb.x) + wb.y;
+              pre[2 * i2 + 1] = acc1[cb][2 * i2 + 1] * (sinv * wb.z) + wb.w;
+            }
+            if constexpr (KIND == MLP_TRAIN) {
+              if (pok)
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                  *reinterpret_cast<float4*>(zrow + 8 * q) =
+                      make_float4(pre[4 * q], pre[4 * q + 1], pre[4 * q + 2], pre[4 * q + 3]);
+            }
+#pragma unroll
+            for (int i = 0; i < 16; ++i) g[i] = gelu_erf(pre[i]) * tsc;
           }
 #pragma unroll
           for (int st = 0; st < 2; ++st) {
@@ -324,12 +388,19 @@ __global__ void __launch_bounds__(WAVES * 64, (WAVES == 4 && C > 128) ? 1 : 2)
     for (int g4 = 0; g4 < 4; ++g4) {
       const float4 w01 = pp[2 * g4], w23 = pp[2 * g4 + 1];  // (1/s_c, b2_c) of registers 4 g4 .. 4 g4 + 3
       const unsigned c0 = (unsigned)(32 * b + 8 * g4 + 4 * h);
-      const float4 xres = bload4(rX, pok ? (xr + c0) * 4u : OOB);
       float4 y;
-      y.x = xres.x + (acc2[b][4 * g4 + 0] * (tinv * w01.x) + w01.y);
-      y.y = xres.y + (acc2[b][4 * g4 + 1] * (tinv * w01.z) + w01.w);
-      y.z = xres.z + (acc2[b][4 * g4 + 2] * (tinv * w23.x) + w23.y);
-      y.w = xres.w + (acc2[b][4 * g4 + 3] * (tinv * w23.z) + w23.w);
+      if constexpr (KIND == MLP_BWD) {  // the branch's input gradient: no bias, no residual
+        y.x = acc2[b][4 * g4 + 0] * (tinv * w01.x);
+        y.y = acc2[b][4 * g4 + 1] * (tinv * w01.z);
+        y.z = acc2[b][4 * g4 + 2] * (tinv * w23.x);
+        y.w = acc2[b][4 * g4 + 3] * (tinv * w23.z);
+      } else {
+        const float4 xres = bload4(rX, pok ? (xr + c0) * 4u : OOB);
+        y.x = xres.x + rsp * (acc2[b][4 * g4 + 0] * (tinv * w01.x) + w01.y);
+        y.y = xres.y + rsp * (acc2[b][4 * g4 + 1] * (tinv * w01.z) + w01.w);
+        y.z = xres.z + rsp * (acc2[b][4 * g4 + 2] * (tinv * w23.x) + w23.y);
+        y.w = xres.w + rsp * (acc2[b][4 * g4 + 3] * (tinv * w23.z) + w23.w);
+      }
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, y), rY, pok ? (yr + c0) * 4u : OOB, 0, 0);
     }
   }
@@ -442,20 +513,50 @@ int pack_impl(const float* w1, const float* b1, const float* w2, const float* b2
   return sfx::check_launch("sfx_mlp_pack");
 }
 
-template <int C, int WAVES, int RING, bool HS = false>
+template <int C, int WAVES, int RING, bool HS = false, int KIND = MLP_EVAL>
 int run_impl(int M, const float* x, long long ldx, const float* stream, const float* par, float eps, float* y,
-             long long ldy, hipStream_t st) {
+             long long ldy, hipStream_t st, const float* rowscale = nullptr, float* z = nullptr) {
   static int rot = -1;
   if (rot < 0) {
     const char* e = getenv("SFX_MLP_ROT");
     rot = (e && *e) ? (atoi(e) != 0) : 1;
   }
-  mlp_kernel<C, WAVES, RING, HS><<<sfx::ceil_div(M, HS ? WAVES * 16 : WAVES * 32), WAVES * 64, 0, st>>>(
-      M, x, ldx, stream, par, eps, y, ldy, rot);
-  return sfx::check_launch("sfx_block_mlp");
+  mlp_kernel<C, WAVES, RING, HS, KIND><<<sfx::ceil_div(M, HS ? WAVES * 16 : WAVES * 32), WAVES * 64, 0, st>>>(
+      M, x, ldx, stream, par, eps, y, ldy, rot, rowscale, z);
+  return sfx::check_launch(KIND == MLP_EVAL ? "sfx_block_mlp" : KIND == MLP_TRAIN ? "sfx_block_mlp_train"
+                                                                                  : "sfx_block_mlp_bwd");
+}
+
+// the training kinds run the default eval geometry of each C (4 waves; hidden split at C = 128, 256, and for the
+// C = 96 backward, whose whole-chunk tile spills)
+template <int KIND>
+int run_train(int M, int C, const float* x, long long ldx, const float* stream, const float* par, float eps, float* y,
+              long long ldy, hipStream_t st, const float* rowscale, float* z) {
+  switch (C) {
+    case 64: return run_impl<64, 4, 4, false, KIND>(M, x, ldx, stream, par, eps, y, ldy, st, rowscale, z);
+    case 96: return run_impl<96, 4, 4, KIND == MLP_BWD, KIND>(M, x, ldx, stream, par, eps, y, ldy, st, rowscale, z);
+    case 128: return run_impl<128, 4, 4, true, KIND>(M, x, ldx, stream, par, eps, y, ldy, st, rowscale, z);
+    default: return run_impl<256, 4, SFX_MLP_RING256, true, KIND>(M, x, ldx, stream, par, eps, y, ldy, st, rowscale, z);
+  }
 }
 
 inline bool mlp_channels_ok(int C) { return C == 64 || C == 96 || C == 128 || C == 256; }
+
+int check_mlp_args(const char* what, int M, int C, const float* x, long long ldx, const float* stream,
+                   const float* params, const float* y, long long ldy, const float* z) {
+  SFX_REQUIRE(M >= 0 && mlp_channels_ok(C), "%s: C must be one of 64, 96, 128, 256 (got %d)", what, C);
+  if (M == 0) return SFX_OK;
+  SFX_REQUIRE(x && stream && params && y && z, "%s: null buffer", what);
+  SFX_REQUIRE(ldx >= C && ldy >= C && ldx % 4 == 0 && ldy % 4 == 0, "%s: leading dimensions", what);
+  SFX_REQUIRE(((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y) | reinterpret_cast<uintptr_t>(z) |
+                reinterpret_cast<uintptr_t>(stream) | reinterpret_cast<uintptr_t>(params)) & 15) == 0,
+              "%s: buffers must be 16-byte aligned", what);
+  SFX_REQUIRE((long long)M * ldx * 4 + 64 < (long long)OOB && (long long)M * ldy * 4 + 64 < (long long)OOB,
+              "%s: operand exceeds the 2 GiB buffer-descriptor range", what);
+  SFX_REQUIRE(x != y, "%s: in-place output is not supported", what);
+  return SFX_OK;
+}
+
 
 }  // namespace
 
@@ -513,6 +614,26 @@ int sfx_block_mlp(int M, int C, const float* x, long long ldx, const float* stre
     default: return hs ? run_impl<256, 4, SFX_MLP_RING256, true>(M, x, ldx, stream, params, eps, y, ldy, st)
                        : run_impl<256, 4, SFX_MLP_RING256>(M, x, ldx, stream, params, eps, y, ldy, st);
   }
+}
+
+// (ABI v13) training forward: as sfx_block_mlp, plus z [M, 4C] (contiguous) = the pre-activation fc1(LN2(x)) and
+// the DropPath keep factor rowscale [M] (NULL: 1) on the branch: y = x + rowscale * (fc2(GELU(z)) + b2)
+int sfx_block_mlp_train(int M, int C, const float* x, long long ldx, const float* stream, const float* params,
+                        float eps, const float* rowscale, float* z, float* y, long long ldy, void* stream_) {
+  const int rc = check_mlp_args("sfx_block_mlp_train", M, C, x, ldx, stream, params, y, ldy, z);
+  if (rc != SFX_OK || M == 0) return rc;
+  return run_train<MLP_TRAIN>(M, C, x, ldx, stream, params, eps, y, ldy, sfx::as_stream(stream_), rowscale, z);
+}
+
+// (ABI v13) training backward of the branch: dh2 = W1^T (GELU'(z) o W2^T (rowscale * dy)) (LN2's backward and the
+// residual are the caller's); stream / params from sfx_mlp_pack(C, W2^T, 0, W1^T, 0, gamma, beta) -- the
+// transposed weights in fc1's / fc2's places, zero biases
+int sfx_block_mlp_bwd(int M, int C, const float* dy, long long lddy, const float* stream, const float* params,
+                      const float* rowscale, const float* z, float* dh2, long long lddh, void* stream_) {
+  const int rc = check_mlp_args("sfx_block_mlp_bwd", M, C, dy, lddy, stream, params, dh2, lddh, z);
+  if (rc != SFX_OK || M == 0) return rc;
+  return run_train<MLP_BWD>(M, C, dy, lddy, stream, params, 0.f, dh2, lddh, sfx::as_stream(stream_), rowscale,
+                            const_cast<float*>(z));
 }
 
 }  // extern "C"

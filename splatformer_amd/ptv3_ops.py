@@ -63,6 +63,8 @@ _lib.register("sfx_mlp_stream_floats", [I], Z)
 _lib.register("sfx_mlp_params_floats", [I], Z)
 _lib.register("sfx_mlp_pack", [I, P, P, P, P, P, P, P, P, P, P])
 _lib.register("sfx_block_mlp", [I, I, P, L, P, P, F, P, L, P])
+_lib.register("sfx_block_mlp_train", [I, I, P, L, P, P, F, P, P, P, L, P])
+_lib.register("sfx_block_mlp_bwd", [I, I, P, L, P, P, P, P, P, L, P])
 
 ACT_NONE, ACT_GELU, ACT_RELU, ACT_TANH = 0, 1, 2, 3
 # gemm.hip kCfgs: 128x128, 128x96, 128x64, 64x128, 64x64 (4 waves, 2 per CU), 256x128, 128x256 (8 waves)
@@ -333,6 +335,62 @@ def block_mlp(x2: Tensor, ln2, fc1, fc2, out: Optional[Tensor] = None) -> Tensor
     px, ldx = _rows(x2)
     py, ldy = _rows(out)
     call("sfx_block_mlp", M, C, px, ldx, ptr(st), ptr(pr), float(ln2.eps), py, ldy, stream())
+    return out
+
+
+def block_mlp_train(x2: Tensor, ln2, fc1, fc2, z: Tensor, rowscale: Optional[Tensor] = None,
+                    out: Optional[Tensor] = None) -> Tensor:
+    """Training forward of the Block MLP tail in one launch (csrc/mlp.hip MLP_TRAIN): Y = x2 + rowscale *
+    (fc2(GELU(z)) + b2) with z = fc1(LN2(x2)) stored into `z` [M, 4C] for the backward."""
+    M, C = x2.shape
+    if z.shape != (M, 4 * C) or not z.is_contiguous():
+        raise ValueError("block_mlp_train: z must be a contiguous [M, 4C] tensor")
+    st, pr = mlp_pack(ln2, fc1, fc2)
+    if out is None:
+        out = torch.empty(M, C, device=x2.device, dtype=torch.float32)
+    px, ldx = _rows(x2)
+    py, ldy = _rows(out)
+    call("sfx_block_mlp_train", M, C, px, ldx, ptr(st), ptr(pr), float(ln2.eps), ptr(rowscale), ptr(z), py, ldy,
+         stream())
+    return out
+
+
+def mlp_bwd_pack(ln2, fc1, fc2) -> Tuple[Tensor, Tensor]:
+    """sfx_block_mlp_bwd's weight stream / table: sfx_mlp_pack of W2^T in fc1's place and W1^T in fc2's, zero
+    biases; cached on fc2 until a weight changes."""
+    ts = (fc1.weight, fc2.weight)
+    key = tuple((t.data_ptr(), t._version) for t in ts)
+    c = fc2.__dict__.get("_sfx_mlp_bwd")
+    if c is not None and c[0] == key:
+        return c[1], c[2]
+    C = fc1.weight.shape[1]
+    dev = fc1.weight.device
+    st = torch.empty(int(_lib.fn("sfx_mlp_stream_floats")(C)), device=dev, dtype=torch.float32)
+    pr = torch.empty(int(_lib.fn("sfx_mlp_params_floats")(C)), device=dev, dtype=torch.float32)
+    ws = torch.empty(9 * C, device=dev, dtype=torch.int32)
+    w1t = fc2.weight.detach().t().contiguous()  # [4C, C]: rows = hidden units (W2^T)
+    w2t = fc1.weight.detach().t().contiguous()  # [C, 4C]: rows = channels (W1^T)
+    z4, z1 = torch.zeros(4 * C, device=dev), torch.zeros(C, device=dev)
+    one = torch.ones(C, device=dev)
+    call("sfx_mlp_pack", C, ptr(w1t), ptr(z4), ptr(w2t), ptr(z1), ptr(one), ptr(z1), ptr(st), ptr(pr), ptr(ws),
+         stream())
+    fc2.__dict__["_sfx_mlp_bwd"] = (key, st, pr, (w1t, w2t, z4, z1, one))
+    return st, pr
+
+
+def block_mlp_bwd(dy: Tensor, ln2, fc1, fc2, z: Tensor, rowscale: Optional[Tensor] = None,
+                  out: Optional[Tensor] = None) -> Tensor:
+    """d(LN2 output) of the Block MLP branch in one launch (csrc/mlp.hip MLP_BWD): W1^T (GELU'(z) o W2^T
+    (rowscale * dy)) -- the [M, 4C] hidden gradient never reaches HBM."""
+    M, C = dy.shape
+    if z.shape != (M, 4 * C) or not z.is_contiguous():
+        raise ValueError("block_mlp_bwd: z must be a contiguous [M, 4C] tensor")
+    st, pr = mlp_bwd_pack(ln2, fc1, fc2)
+    if out is None:
+        out = torch.empty(M, C, device=dy.device, dtype=torch.float32)
+    pd, ldd = _rows(dy)
+    po, ldo = _rows(out)
+    call("sfx_block_mlp_bwd", M, C, pd, ldd, ptr(st), ptr(pr), ptr(rowscale), ptr(z), po, ldo, stream())
     return out
 
 

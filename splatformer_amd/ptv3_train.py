@@ -16,6 +16,7 @@ replays it in reverse.  Every op is a libsfx kernel (train_ops / ptv3_ops); torc
 """
 from __future__ import annotations
 
+import os
 from typing import Callable, Dict, List, Optional, Sequence
 
 import torch
@@ -70,6 +71,13 @@ def _grad_buffers(lin: torch.nn.Linear):
 
 
 # ---- Block ------------------------------------------------------------------------------------------------
+# SFX_MLP_TRAIN_FUSED=0: the training MLP tail as LayerNorm + two GEMMs forward and two GEMMs backward (the [n, 4C]
+# GELU output and hidden gradient through HBM) instead of sfx_block_mlp_train / sfx_block_mlp_bwd
+MLP_TRAIN_FUSED = os.environ.get("SFX_MLP_TRAIN_FUSED", "1") != "0"
+
+
+def mlp_train_fused_ok(x2: Tensor, C: int) -> bool:
+    return MLP_TRAIN_FUSED and C in ops.MLP_CHANNELS and x2.is_contiguous() and x2.data_ptr() % 16 == 0
 def block_forward(blk: Block, name: str, point: Point, masks: MaskFn, conv_in: Optional[Tensor] = None,
                   out: Optional[Tensor] = None) -> dict:
     x = point.feat
@@ -89,14 +97,18 @@ def block_forward(blk: Block, name: str, point: Point, masks: MaskFn, conv_in: O
         a = ops.window_attention(qkv, order, win, nw, K, blk.attn.num_heads, C)
     ma = masks(name + ".attn", n, blk.drop_prob, x.device)
     x2 = ops.linear(a, blk.attn.proj.weight, blk.attn.proj.bias, residual=x1, rowscale=ma)
-    h2 = ops.layernorm(x2, ln2.weight, ln2.bias, ln2.eps)
     z = torch.empty(n, mlp.fc1.weight.shape[0], device=x.device, dtype=torch.float32)
-    m = ops.linear(h2, mlp.fc1.weight, mlp.fc1.bias, act=ops.ACT_GELU, pre_out=z, pre_before_act=True)
-    del h2
     mm = masks(name + ".mlp", n, blk.drop_prob, x.device)
-    point.feat = ops.linear(m, mlp.fc2.weight, mlp.fc2.bias, residual=x2, rowscale=mm, out=out)
+    fused = mlp_train_fused_ok(x2, C)
+    if fused:  # LN2 + fc1 (z stored) + GELU + fc2 + mask + residual in one launch (csrc/mlp.hip MLP_TRAIN)
+        point.feat = ops.block_mlp_train(x2, ln2, mlp.fc1, mlp.fc2, z, rowscale=mm, out=out)
+    else:
+        h2 = ops.layernorm(x2, ln2.weight, ln2.bias, ln2.eps)
+        m = ops.linear(h2, mlp.fc1.weight, mlp.fc1.bias, act=ops.ACT_GELU, pre_out=z, pre_before_act=True)
+        del h2
+        point.feat = ops.linear(m, mlp.fc2.weight, mlp.fc2.bias, residual=x2, rowscale=mm, out=out)
     return dict(kind="block", blk=blk, name=name, u=u, x1=x1, h=h, qkv=qkv, a=a, x2=x2, z=z, ma=ma, mm=mm,
-                order=order, win=win, nw=nw, K=K, smap=point.nbr, sep_conv_in=conv_in is not None)
+                order=order, win=win, nw=nw, K=K, smap=point.nbr, sep_conv_in=conv_in is not None, mlp_fused=fused)
 
 
 _TRACE: Optional[list] = None  # debugging: set to a list to record (tag, tensor) of the backward
@@ -117,10 +129,13 @@ def block_backward(rec: dict, dy: Tensor, need_input: bool):
     C = blk.channels
     ln_c = blk.cpe[2]
     ln1, ln2, mlp = blk.norm1[0], blk.norm2[0], blk.mlp[0]
-    dm = tops.linear_bwd_data(dy, wt(mlp.fc2.weight), rowscale=rec["mm"], dact=tops.DACT_GELU, dact_pre=rec["z"])
-    dh2 = tops.linear_bwd_data(dm, wt(mlp.fc1.weight))
-    _trace(f"{nm}.dm", dm)
-    del dm
+    if rec.get("mlp_fused"):  # fc2^T, GELU', fc1^T in one launch: the [n, 4C] hidden gradient stays on chip
+        dh2 = ops.block_mlp_bwd(dy, ln2, mlp.fc1, mlp.fc2, rec["z"], rowscale=rec["mm"])
+    else:
+        dm = tops.linear_bwd_data(dy, wt(mlp.fc2.weight), rowscale=rec["mm"], dact=tops.DACT_GELU, dact_pre=rec["z"])
+        dh2 = tops.linear_bwd_data(dm, wt(mlp.fc1.weight))
+        _trace(f"{nm}.dm", dm)
+        del dm
     dx2 = tops.layernorm_bwd(rec["x2"], ln2.weight, dh2, ln2.eps, dres=dy)
     _trace(f"{nm}.dh2", dh2)
     _trace(f"{nm}.dx2", dx2)

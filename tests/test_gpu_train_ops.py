@@ -257,3 +257,44 @@ def test_drop_mask(device):
     k = (a > 0).float()
     both = float((k[1:] * k[:-1]).mean())
     assert abs(both - keep * keep) < 0.01
+
+
+@pytest.mark.parametrize("C,M", [(64, 3001), (96, 2050), (128, 1999), (256, 1037)])
+def test_block_mlp_train_fwd_bwd(device, C, M):
+    """Fused training MLP tail (csrc/mlp.hip MLP_TRAIN / MLP_BWD) vs fp64 autograd of LN2 -> fc1 -> GELU -> fc2 ->
+    DropPath row scale -> + shortcut: y, the stored pre-activation z, and the LN2-output gradient dh2."""
+    g = torch.Generator().manual_seed(C + M)
+    ln2 = torch.nn.LayerNorm(C)
+    fc1, fc2 = torch.nn.Linear(C, 4 * C), torch.nn.Linear(4 * C, C)
+    with torch.no_grad():
+        ln2.weight.copy_(torch.rand(C, generator=g) + 0.5)
+        ln2.bias.copy_(torch.randn(C, generator=g) * 0.1)
+        for lin in (fc1, fc2):
+            lin.weight.copy_(torch.randn(lin.weight.shape, generator=g) / lin.weight.shape[1] ** 0.5)
+            lin.bias.copy_(torch.randn(lin.bias.shape, generator=g) * 0.1)
+    x2 = torch.randn(M, C, generator=g) * 2 + 0.3
+    x2[7] *= 1e3  # rows far apart in magnitude (per-row scales)
+    rs = (torch.rand(M, generator=g) > 0.3).float() / 0.7
+    dy = torch.randn(M, C, generator=g)
+    # fp64 reference
+    xd = x2.double()
+    h2 = F.layer_norm(xd, (C,), ln2.weight.double(), ln2.bias.double(), ln2.eps).detach().requires_grad_()
+    z_ref = h2 @ fc1.weight.double().T + fc1.bias.double()
+    y_ref = xd + rs.double()[:, None] * (F.gelu(z_ref) @ fc2.weight.double().T + fc2.bias.double())
+    y_ref.backward(dy.double())
+    y1_ref = (xd + (F.gelu(z_ref) @ fc2.weight.double().T + fc2.bias.double())).detach()
+    dev_mods = [m.to(device) for m in (ln2, fc1, fc2)]
+    z = torch.empty(M, 4 * C, device=device)
+    y = ops.block_mlp_train(x2.to(device), *dev_mods, z, rowscale=rs.to(device))
+    # y vs fp64 on the whole output (fp32 rounding of x2 + branch included), and the branch alone on the rows of
+    # ordinary magnitude (row 7's 1e3-scale x2 leaves 6e-5 of output rounding in y - x2)
+    keep = torch.arange(M) != 7
+    assert rel_l2(z, z_ref) < 2e-6
+    assert rel_l2(y, y_ref) < 1e-6
+    assert rel_l2((y - x2.to(device))[keep.to(device)], (y_ref - xd)[keep]) < 2e-6
+    dh2 = ops.block_mlp_bwd(dy.to(device), *dev_mods, z, rowscale=rs.to(device))
+    assert rel_l2(dh2, h2.grad) < 2e-6
+    # no mask: rowscale None
+    y1 = ops.block_mlp_train(x2.to(device), *dev_mods, z)
+    assert rel_l2(y1, y1_ref) < 1e-6
+    assert rel_l2((y1 - x2.to(device))[keep.to(device)], (y1_ref - xd)[keep]) < 2e-6
