@@ -68,8 +68,13 @@ def rasterize_gaussians_to_multiimgs(gs_params: Dict[str, Tensor], cameras: Dict
     if len(c2ws) > 1 and not _needs_grad(gp) and "opacities_sigmoid" not in gp and "opacities" in gp:
         return _render_fused_views(gp, c2ws, cameras)
     rgbs, alphas = [], []
+    prep = None
+    if _needs_grad(gp) or "opacities_sigmoid" in gp:  # training: the view-independent glue once per scene
+        if "opacities" not in gp and "opacities_sigmoid" not in gp:
+            raise ValueError("No opacities found in gs_params")
+        prep = _autograd_prep(gp)
     for camera_to_world in cameras["camera_to_worlds"]:
-        rgb, alpha = rasterize_gaussians_to_singleimg(gs_params, camera_to_world, **cameras)
+        rgb, alpha = rasterize_gaussians_to_singleimg(gs_params, camera_to_world, _prep=prep, **cameras)
         rgbs.append(rgb)
         alphas.append(alpha)
     return rgbs, alphas
@@ -80,7 +85,7 @@ def _needs_grad(gs_params) -> bool:
 
 
 def rasterize_gaussians_to_singleimg(gs_params, camera_to_world, cx, cy, fx, fy, width, height, background_color,
-                                     **kwargs):
+                                     _prep=None, **kwargs):
     """gs_utils.py:29-114 -> (rgb [H,W,3] clamped <= 1, alpha [H,W,1])."""
     gs_params = {k: v.float() if v.dtype == torch.half else v for k, v in gs_params.items()}
     if "opacities" not in gs_params and "opacities_sigmoid" not in gs_params:
@@ -88,7 +93,7 @@ def rasterize_gaussians_to_singleimg(gs_params, camera_to_world, cx, cy, fx, fy,
     H, W = int(_scalar(height)), int(_scalar(width))
     fx, fy, cx, cy = _scalar(fx), _scalar(fy), _scalar(cx), _scalar(cy)
     if _needs_grad(gs_params) or "opacities_sigmoid" in gs_params:
-        return _render_autograd(gs_params, camera_to_world, cx, cy, fx, fy, W, H, background_color)
+        return _render_autograd(gs_params, camera_to_world, cx, cy, fx, fy, W, H, background_color, prep=_prep)
     return _render_fused(gs_params, camera_to_world, cx, cy, fx, fy, W, H, background_color)
 
 
@@ -239,8 +244,31 @@ def _render_fused_views(gs, c2ws, cameras, meta=None):
     return list(out.unbind(0)), list(alpha.unsqueeze(-1).unbind(0))
 
 
-def _render_autograd(gs_params, camera_to_world, cx, cy, fx, fy, W, H, background_color):
-    """Line-for-line the reference glue (gs_utils.py:32-112) over the HIP autograd ops."""
+def _autograd_prep(gs_params):
+    """The view-independent half of the reference glue (gs_utils.py:42-66): activated scales, normalised quaternions
+    (rows whose norm is off by > 1e-6 -> identity, as the reference's masked assignment, via torch.where: no host
+    read), opacities, SH coefficients.  Computed once per scene for all its views: the same ops, so the same values
+    and, through autograd, the same summed gradients as per view."""
+    means = gs_params["means"]
+    scales = torch.exp(gs_params["scales"])
+    quats = gs_params["quats"] / torch.norm(gs_params["quats"], dim=-1, keepdim=True)
+    mask = (quats.norm(dim=-1) - 1) < 1e-6
+    quats = torch.where(mask[:, None], quats, torch.tensor([0, 0, 0, 1.0], device=quats.device, dtype=quats.dtype))
+    if "opacities" in gs_params:
+        opacities = torch.sigmoid(gs_params["opacities"])
+    else:
+        opacities = gs_params["opacities_sigmoid"]
+    if "features_rest" in gs_params:
+        colors = torch.cat([gs_params["features_dc"].unsqueeze(1), gs_params["features_rest"]], dim=1)
+    else:
+        colors = gs_params["features_dc"].unsqueeze(1)
+    return means, scales, quats, opacities, colors
+
+
+def _render_autograd(gs_params, camera_to_world, cx, cy, fx, fy, W, H, background_color, prep=None):
+    """Line-for-line the reference glue (gs_utils.py:32-112) over the HIP autograd ops (`prep`: _autograd_prep of
+    the same Gaussians, shared by the views of a scene)."""
+    means, scales, quats, opacities, colors = prep if prep is not None else _autograd_prep(gs_params)
     R = camera_to_world[:3, :3]
     T = camera_to_world[:3, 3:4]
     R_edit = torch.diag(torch.tensor([1, -1, -1], device=R.device, dtype=R.dtype))
@@ -250,22 +278,6 @@ def _render_autograd(gs_params, camera_to_world, cx, cy, fx, fy, W, H, backgroun
     viewmat = torch.eye(4, device=R.device, dtype=R.dtype)
     viewmat[:3, :3] = R_inv
     viewmat[:3, 3:4] = T_inv
-    means = gs_params["means"]
-    scales = torch.exp(gs_params["scales"])
-    quats = gs_params["quats"] / torch.norm(gs_params["quats"], dim=-1, keepdim=True)
-    mask = (quats.norm(dim=-1) - 1) < 1e-6
-    inv_mask = ~mask
-    if inv_mask.any():
-        quats = quats.clone()
-        quats[inv_mask] = torch.tensor([0, 0, 0, 1.0], device=quats.device)
-    if "opacities" in gs_params:
-        opacities = torch.sigmoid(gs_params["opacities"])
-    else:
-        opacities = gs_params["opacities_sigmoid"]
-    if "features_rest" in gs_params:
-        colors = torch.cat([gs_params["features_dc"].unsqueeze(1), gs_params["features_rest"]], dim=1)
-    else:
-        colors = gs_params["features_dc"].unsqueeze(1)
     n = int(math.sqrt(colors.shape[1]) - 1)
     if n == 0:
         rgbs = torch.sigmoid(colors[:, 0, :])
@@ -273,10 +285,10 @@ def _render_autograd(gs_params, camera_to_world, cx, cy, fx, fy, W, H, backgroun
         viewdirs_ = means.detach() - camera_to_world.detach()[:3, 3]
         viewdirs_norm = viewdirs_.norm(dim=-1, keepdim=True)
         viewdirs = viewdirs_ / viewdirs_norm
-        bad = (viewdirs_norm == 0).squeeze(-1)
-        if bool(bad.any()):
-            viewdirs = viewdirs.clone()
-            viewdirs[bad] = torch.tensor([0.0, 0.0, 1.0], device=viewdirs.device)
+        # a Gaussian at the camera centre (zero norm): direction (0, 0, 1) instead of the reference's random one
+        # (INTEGRATION.md); torch.where, so no host read of the mask
+        viewdirs = torch.where(viewdirs_norm == 0,
+                               torch.tensor([0.0, 0.0, 1.0], device=viewdirs.device, dtype=viewdirs.dtype), viewdirs)
         rgbs = spherical_harmonics(n, viewdirs, colors)
         rgbs = torch.clamp(rgbs + 0.5, min=0.0)
     xys, depths, radii, conics, comp, num_tiles_hit, cov3d = project_gaussians(

@@ -137,10 +137,10 @@ class Trainer:
                 loss = image_l1(preds, imgs) / num_images / len(scenes) / self.accumulate_step
                 loss.backward()
             refine_backward(self.model, tape, leaf.grad)
-            total += float(loss.detach())
+            total = total + loss.detach()  # summed on the device: one host read per micro-step, not per scene
             del tape, packed, leaf, out_gs, preds
         self.micro += 1
-        return total
+        return float(total)
 
     def optimizer_step(self) -> None:
         if self.group is not None and self.world > 1:

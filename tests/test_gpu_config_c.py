@@ -70,6 +70,7 @@ def hip_c(device):
 
     def cap_raster(xys, depths, radii, conics, num_tiles_hit, colors, opacity, img_height, img_width, block_width,
                    background=None, return_alpha=False):
+        opacity = opacity.view_as(opacity)  # per-view node: the activated opacities are shared by the views
         for t in (xys, conics, colors, opacity):
             t.retain_grad()
         rgb, alpha = orig_r(xys, depths, radii, conics, num_tiles_hit, colors, opacity, img_height, img_width,
