@@ -36,6 +36,13 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 constexpr int KMAX = 128;
 
+// V^T chunk swizzle: the 16-byte chunk c (8 keys) of V^T row dd sits at chunk c ^ vt_swz(dd), 2 x the parity of
+// dd's 4-row group.  The staging's transposed dword stores (rows 4 ch .. 4 ch + 3 of 4-8 column chunks per 32
+// lanes) were 2- / 3- / 4-way bank conflicts at d = 16 / 24 / 32 (the stride-136 rows put every other chunk group on
+// one bank set); swizzled they are 1- / 2- / 2-way (free for ds_write_b32), and the fragment reads stay conflict-
+// free (tools/attn_banks.py)
+__device__ __forceinline__ int vt_swz(int dd) { return (__builtin_popcount((unsigned)(dd >> 2)) & 1) << 1; }
+
 template <int D>
 __global__ void __launch_bounds__(256, 2)
 window_attn_kernel(const float* __restrict__ qkv, const int* __restrict__ order, const int* __restrict__ win,
@@ -601,7 +608,7 @@ window_attn_split_kernel(const float* __restrict__ qkv, const int* __restrict__ 
     const int pos = (row & ~15) + 8 * ((kk >> 2) & 1) + (((kk >> 3) << 2) | (kk & 3));
 #pragma unroll
     for (int q = 0; q < NT; ++q) {
-      unsigned* vt = reinterpret_cast<unsigned*>(Vt + (q * D + 4 * ch) * VST + pos);
+      unsigned* vt = reinterpret_cast<unsigned*>(Vt + (q * D + 4 * ch) * VST + (pos ^ (8 * vt_swz(4 * ch))));
       vt[0] = (t0[q].x & 0xffffu) | (t1[q].x << 16);
       vt[VST / 2] = (t0[q].x >> 16) | (t1[q].x & 0xffff0000u);
       vt[VST] = (t0[q].y & 0xffffu) | (t1[q].y << 16);
@@ -687,7 +694,7 @@ window_attn_split_kernel(const float* __restrict__ qkv, const int* __restrict__ 
       for (int q = 0; q < NT; ++q) {
         pf[q] = __builtin_bit_cast(bf16x8, make_uint4(a[q].x, a[q].y, b[q].x, b[q].y));
         uint4 vv = make_uint4(0, 0, 0, 0);  // dd = l32 >= D: zero rows of V^T
-        if (l32 < D) vv = *reinterpret_cast<const uint4*>(Vt + (q * D + l32) * VST + (2 * kb + st) * 16 + 8 * h);
+        if (l32 < D) vv = *reinterpret_cast<const uint4*>(Vt + (q * D + l32) * VST + (((2 * (2 * kb + st) + h) ^ vt_swz(l32)) << 3));
         vf[q] = __builtin_bit_cast(bf16x8, vv);
       }
 #pragma unroll
@@ -839,7 +846,7 @@ window_attn_seq_kernel(const float* __restrict__ qkv, const int* __restrict__ or
         const int pos = (row & ~15) + 8 * ((kk >> 2) & 1) + (((kk >> 3) << 2) | (kk & 3));
 #pragma unroll
         for (int q = 0; q < NT; ++q) {
-          unsigned* vt = reinterpret_cast<unsigned*>(Vt + (q * D + 4 * ch) * VST + pos);
+          unsigned* vt = reinterpret_cast<unsigned*>(Vt + (q * D + 4 * ch) * VST + (pos ^ (8 * vt_swz(4 * ch))));
           vt[0] = (t0[q].x & 0xffffu) | (t1[q].x << 16);
           vt[VST / 2] = (t0[q].x >> 16) | (t1[q].x & 0xffff0000u);
           vt[VST] = (t0[q].y & 0xffffu) | (t1[q].y << 16);
@@ -943,7 +950,7 @@ window_attn_seq_kernel(const float* __restrict__ qkv, const int* __restrict__ or
         for (int q = 0; q < NT; ++q) {
           pf[q] = __builtin_bit_cast(bf16x8, make_uint4(a[q].x, a[q].y, bb[q].x, bb[q].y));
           uint4 v4 = make_uint4(0, 0, 0, 0);
-          if (l32 < D) v4 = *reinterpret_cast<const uint4*>(Vt + (q * D + l32) * VST + (2 * kb + st) * 16 + 8 * h);
+          if (l32 < D) v4 = *reinterpret_cast<const uint4*>(Vt + (q * D + l32) * VST + (((2 * (2 * kb + st) + h) ^ vt_swz(l32)) << 3));
           vf[q] = __builtin_bit_cast(bf16x8, v4);
         }
 #pragma unroll
@@ -1105,7 +1112,7 @@ window_attn_split_flash_kernel(const float* __restrict__ qkv, const int* __restr
       const int pos = (row & ~15) + 8 * ((kk >> 2) & 1) + (((kk >> 3) << 2) | (kk & 3));
 #pragma unroll
       for (int q = 0; q < NT; ++q) {
-        unsigned* vt = reinterpret_cast<unsigned*>(Vt + (q * D + 4 * ch) * VST + pos);
+        unsigned* vt = reinterpret_cast<unsigned*>(Vt + (q * D + 4 * ch) * VST + (pos ^ (8 * vt_swz(4 * ch))));
         vt[0] = (t0[q].x & 0xffffu) | (t1[q].x << 16);
         vt[VST / 2] = (t0[q].x >> 16) | (t1[q].x & 0xffff0000u);
         vt[VST] = (t0[q].y & 0xffffu) | (t1[q].y << 16);
@@ -1186,7 +1193,7 @@ window_attn_split_flash_kernel(const float* __restrict__ qkv, const int* __restr
         for (int q = 0; q < NT; ++q) {
           pf[q] = __builtin_bit_cast(bf16x8, make_uint4(a[q].x, a[q].y, b[q].x, b[q].y));
           uint4 vv = make_uint4(0, 0, 0, 0);  // dd = l32 >= D: zero rows of V^T
-          if (l32 < D) vv = *reinterpret_cast<const uint4*>(Vt + (q * D + l32) * VST + (2 * kb + st) * 16 + 8 * h);
+          if (l32 < D) vv = *reinterpret_cast<const uint4*>(Vt + (q * D + l32) * VST + (((2 * (2 * kb + st) + h) ^ vt_swz(l32)) << 3));
           vf[q] = __builtin_bit_cast(bf16x8, vv);
         }
 #pragma unroll
@@ -1545,7 +1552,7 @@ __device__ __forceinline__ void bwd_stage_pair(char* rimg, unsigned short* timg,
   for (int q = 0; q < 2; ++q) {
     *reinterpret_cast<uint2*>(rimg + q * KMAX * QROW + o0) = t0[q];
     *reinterpret_cast<uint2*>(rimg + q * KMAX * QROW + o1) = t1[q];
-    unsigned* vt = reinterpret_cast<unsigned*>(timg + (q * D + 4 * ch) * VST + pos);
+    unsigned* vt = reinterpret_cast<unsigned*>(timg + (q * D + 4 * ch) * VST + (pos ^ (8 * vt_swz(4 * ch))));
     vt[0] = (t0[q].x & 0xffffu) | (t1[q].x << 16);
     vt[VST / 2] = (t0[q].x >> 16) | (t1[q].x & 0xffff0000u);
     vt[VST] = (t0[q].y & 0xffffu) | (t1[q].y << 16);
@@ -1575,7 +1582,7 @@ __device__ __forceinline__ void bwd_tr_frag(const unsigned short* timg, int l32,
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     uint4 v = make_uint4(0, 0, 0, 0);
-    if (l32 < D) v = *reinterpret_cast<const uint4*>(timg + (q * D + l32) * VST + step * 16 + 8 * h);
+    if (l32 < D) v = *reinterpret_cast<const uint4*>(timg + (q * D + l32) * VST + (((2 * step + h) ^ vt_swz(l32)) << 3));
     f[q] = __builtin_bit_cast(f16x8, v);
   }
 }
