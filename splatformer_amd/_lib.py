@@ -97,8 +97,14 @@ def fn(name: str):
     return f
 
 
+_FNS: dict = {}  # name -> resolved ctypes function (one dict lookup per launch instead of lib() + getattr + checks)
+
+
 def call(name: str, *args) -> None:
-    rc = fn(name)(*args)
+    f = _FNS.get(name)
+    if f is None:
+        f = _FNS[name] = fn(name)
+    rc = f(*args)
     if rc != 0:
         msg = lib().sfx_last_error()
         raise RuntimeError(f"{name} failed ({rc}): {msg.decode() if msg else ''}")
@@ -148,13 +154,17 @@ def ptr(t: torch.Tensor | None, dtype: torch.dtype | None = None) -> int | None:
 
 
 _raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+_get_device = torch._C._cuda_getDevice
+_cuda_ready = [False]
 
 
 def stream() -> int:
     """The current HIP stream of the current device (torch's), as a pointer.  Called once per launch: the raw
     accessor costs ~0.3 us against ~8 us for torch.cuda.current_stream()'s Python wrapper (tools/host_profile.py)."""
-    if _raw_stream is not None and torch.cuda.is_initialized():
-        return _raw_stream(torch._C._cuda_getDevice())
+    if _raw_stream is not None:
+        if _cuda_ready[0] or torch.cuda.is_initialized():
+            _cuda_ready[0] = True
+            return _raw_stream(_get_device())
     return torch.cuda.current_stream().cuda_stream
 
 

@@ -297,46 +297,47 @@ struct PrepStrides {
   long long means, scales, quats, opac, dc, rest;
 };
 
-__global__ void render_prep_project_kernel(int n, int num_bases, const float* __restrict__ means,
-                                           const float* __restrict__ log_scales, const float* __restrict__ quats_raw,
-                                           const float* __restrict__ opac_logit, const float* __restrict__ dc,
-                                           const float* __restrict__ rest, PrepStrides ld, const float* __restrict__ c2w,
-                                           float fx, float fy, float cx, float cy, int img_h, int img_w, int bw,
-                                           float* __restrict__ viewmat_out, float* __restrict__ rgbs,
-                                           float* __restrict__ opac, float* __restrict__ xys,
-                                           float* __restrict__ depths, int* __restrict__ radii,
-                                           float* __restrict__ conics, int* __restrict__ num_tiles_hit) {
+// One thread per Gaussian, all views in a loop: the Gaussian's parameters (up to 75 SH floats) are read once into
+// registers and its view-independent terms (exp scales, normalised quaternion, sigmoid opacity -- fp64 exps) computed
+// once, instead of once per (Gaussian, view) thread re-reading them (config E: 9 views x 500k x 59 floats).  The
+// per-view arithmetic is unchanged expression for expression (bit-identical outputs).
+template <int DEG>
+__global__ void __launch_bounds__(256) render_prep_project_kernel(
+    int n, int nviews, const float* __restrict__ means, const float* __restrict__ log_scales,
+    const float* __restrict__ quats_raw, const float* __restrict__ opac_logit, const float* __restrict__ dc,
+    const float* __restrict__ rest, PrepStrides ld, const float* __restrict__ c2ws, float fx, float fy, float cx,
+    float cy, int img_h, int img_w, int bw, float* __restrict__ viewmat_out, float* __restrict__ rgbs,
+    float* __restrict__ opac, float* __restrict__ xys, float* __restrict__ depths, int* __restrict__ radii,
+    float* __restrict__ conics, int* __restrict__ num_tiles_hit) {
   // canonical glue arithmetic (oracle/render_ref.py glue_args(canonical=True)): exp / sigmoid in double rounded
   // once, norms as left-to-right sums with a correctly rounded sqrt, no contraction
 #pragma clang fp contract(off)
+  constexpr int NB = (DEG + 1) * (DEG + 1);
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  // batched views: blockIdx.y = view, cameras [V,4,4], every output offset by view * n records
-  const int view = blockIdx.y;
-  if (view > 0) {
-    const long long o = (long long)view * n;
-    c2w += 16 * view;
-    rgbs += 3 * o; opac += o; xys += 2 * o; depths += o; radii += o; conics += 3 * o; num_tiles_hit += o;
-    viewmat_out = nullptr;
-  }
-  // camera: R = c2w[:3,:3] diag(1,-1,-1); viewmat = [R^T | -R^T t]
-  float R[3][3], t[3];
+  // camera v: R = c2w[:3,:3] diag(1,-1,-1); viewmat = [R^T | -R^T t]
+  auto camera = [&](int v, float (&t)[3], float (&vm)[12]) {
+    const float* c2w = c2ws + 16 * v;
+    float R[3][3];
 #pragma unroll
-  for (int r = 0; r < 3; ++r) {
-    R[r][0] = c2w[4 * r + 0];
-    R[r][1] = -c2w[4 * r + 1];
-    R[r][2] = -c2w[4 * r + 2];
-    t[r] = c2w[4 * r + 3];
-  }
-  float vm[12];
+    for (int r = 0; r < 3; ++r) {
+      R[r][0] = c2w[4 * r + 0];
+      R[r][1] = -c2w[4 * r + 1];
+      R[r][2] = -c2w[4 * r + 2];
+      t[r] = c2w[4 * r + 3];
+    }
 #pragma unroll
-  for (int r = 0; r < 3; ++r) {
+    for (int r = 0; r < 3; ++r) {
 #pragma unroll
-    for (int c = 0; c < 3; ++c) vm[4 * r + c] = R[c][r];
-    vm[4 * r + 3] = -((R[0][r] * t[0] + R[1][r] * t[1]) + R[2][r] * t[2]);
-  }
-  if (i == 0 && viewmat_out)
+      for (int c = 0; c < 3; ++c) vm[4 * r + c] = R[c][r];
+      vm[4 * r + 3] = -((R[0][r] * t[0] + R[1][r] * t[1]) + R[2][r] * t[2]);
+    }
+  };
+  if (i == 0 && viewmat_out) {
+    float t[3], vm[12];
+    camera(0, t, vm);
 #pragma unroll
     for (int k = 0; k < 12; ++k) viewmat_out[k] = vm[k];
+  }
   if (i >= n) return;
   const float* mp = means + i * ld.means;
   const float* sp = log_scales + i * ld.scales;
@@ -350,53 +351,90 @@ __global__ void render_prep_project_kernel(int n, int num_bases, const float* __
   if (isnan(q0) || isnan(q1) || isnan(q2) || isnan(q3)) {
     q0 = 0.f; q1 = 0.f; q2 = 0.f; q3 = 1.f;
   }
-  opac[i] = (float)(1.0 / (1.0 + exp(-(double)opac_logit[i * ld.opac])));
-  // colours
-  const int degree = num_bases >= 25 ? 4 : num_bases >= 16 ? 3 : num_bases >= 9 ? 2 : num_bases >= 4 ? 1 : 0;
-  if (degree == 0) {
+  const float op = (float)(1.0 / (1.0 + exp(-(double)opac_logit[i * ld.opac])));
+  float d0[3];
 #pragma unroll
-    for (int ch = 0; ch < 3; ++ch) rgbs[3 * i + ch] = (float)(1.0 / (1.0 + exp(-(double)dcp[ch])));
-  } else {
-    float vx = px - t[0], vy = py - t[1], vz = pz - t[2];
-    const float vn = sqrtf((vx * vx + vy * vy) + vz * vz);
-    if (vn == 0.f) {  // reference draws a random direction here (gs_utils.py:72-76); we use +z
-      vx = 0.f; vy = 0.f; vz = 1.f;
+  for (int ch = 0; ch < 3; ++ch) d0[ch] = dcp[ch];
+  float c[3 * NB];  // c[3*k + ch] for k >= 1 (the rest coefficients), registers
+#pragma unroll
+  for (int k = 3; k < 3 * NB; ++k) c[k] = rest[i * ld.rest + (k - 3)];
+  float rgb0[3];
+  if constexpr (DEG == 0) {
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) rgb0[ch] = (float)(1.0 / (1.0 + exp(-(double)d0[ch])));
+  }
+  for (int v = 0; v < nviews; ++v) {
+    float t[3], vm[12];
+    camera(v, t, vm);
+    const long long o = (long long)v * n;
+    opac[o + i] = op;
+    if constexpr (DEG == 0) {
+#pragma unroll
+      for (int ch = 0; ch < 3; ++ch) rgbs[3 * (o + i) + ch] = rgb0[ch];
     } else {
-      vx /= vn; vy /= vn; vz /= vn;
-    }
-    const float nrm = sqrtf(vx * vx + vy * vy + vz * vz);
-    const float x = vx / nrm, y = vy / nrm, z = vz / nrm;
-    const float xx = x * x, xy = x * y, xz = x * z, yy = y * y, yz = y * z, zz = z * z;
-    const float* c = rest + i * ld.rest - 3;  // c[3*k + ch] for k >= 1
+      float vx = px - t[0], vy = py - t[1], vz = pz - t[2];
+      const float vn = sqrtf((vx * vx + vy * vy) + vz * vz);
+      if (vn == 0.f) {  // reference draws a random direction here (gs_utils.py:72-76); we use +z
+        vx = 0.f; vy = 0.f; vz = 1.f;
+      } else {
+        vx /= vn; vy /= vn; vz /= vn;
+      }
+      const float nrm = sqrtf(vx * vx + vy * vy + vz * vz);
+      const float x = vx / nrm, y = vy / nrm, z = vz / nrm;
+      const float xx = x * x, xy = x * y, xz = x * z, yy = y * y, yz = y * z, zz = z * z;
 #pragma unroll
-    for (int ch = 0; ch < 3; ++ch) {
-      float acc = SH_C0 * dcp[ch];
-      acc += SH_C1 * (-y * c[3 + ch] + z * c[6 + ch] - x * c[9 + ch]);
-      if (degree >= 2) {
-        acc += (SH_C2[0] * xy * c[12 + ch] + SH_C2[1] * yz * c[15 + ch] + SH_C2[2] * (2.f * zz - xx - yy) * c[18 + ch] +
-                SH_C2[3] * xz * c[21 + ch] + SH_C2[4] * (xx - yy) * c[24 + ch]);
-        if (degree >= 3) {
-          acc += (SH_C3[0] * y * (3.f * xx - yy) * c[27 + ch] + SH_C3[1] * xy * z * c[30 + ch] +
-                  SH_C3[2] * y * (4.f * zz - xx - yy) * c[33 + ch] +
-                  SH_C3[3] * z * (2.f * zz - 3.f * xx - 3.f * yy) * c[36 + ch] +
-                  SH_C3[4] * x * (4.f * zz - xx - yy) * c[39 + ch] + SH_C3[5] * z * (xx - yy) * c[42 + ch] +
-                  SH_C3[6] * x * (xx - 3.f * yy) * c[45 + ch]);
-          if (degree >= 4) {
-            acc += (SH_C4[0] * xy * (xx - yy) * c[48 + ch] + SH_C4[1] * yz * (3.f * xx - yy) * c[51 + ch] +
-                    SH_C4[2] * xy * (7.f * zz - 1.f) * c[54 + ch] + SH_C4[3] * yz * (7.f * zz - 3.f) * c[57 + ch] +
-                    SH_C4[4] * (zz * (35.f * zz - 30.f) + 3.f) * c[60 + ch] +
-                    SH_C4[5] * xz * (7.f * zz - 3.f) * c[63 + ch] +
-                    SH_C4[6] * (xx - yy) * (7.f * zz - 1.f) * c[66 + ch] +
-                    SH_C4[7] * xz * (xx - 3.f * yy) * c[69 + ch] +
-                    SH_C4[8] * (xx * (xx - 3.f * yy) - yy * (3.f * xx - yy)) * c[72 + ch]);
+      for (int ch = 0; ch < 3; ++ch) {
+        float acc = SH_C0 * d0[ch];
+        acc += SH_C1 * (-y * c[3 + ch] + z * c[6 + ch] - x * c[9 + ch]);
+        if constexpr (DEG >= 2) {
+          acc += (SH_C2[0] * xy * c[12 + ch] + SH_C2[1] * yz * c[15 + ch] + SH_C2[2] * (2.f * zz - xx - yy) * c[18 + ch] +
+                  SH_C2[3] * xz * c[21 + ch] + SH_C2[4] * (xx - yy) * c[24 + ch]);
+          if constexpr (DEG >= 3) {
+            acc += (SH_C3[0] * y * (3.f * xx - yy) * c[27 + ch] + SH_C3[1] * xy * z * c[30 + ch] +
+                    SH_C3[2] * y * (4.f * zz - xx - yy) * c[33 + ch] +
+                    SH_C3[3] * z * (2.f * zz - 3.f * xx - 3.f * yy) * c[36 + ch] +
+                    SH_C3[4] * x * (4.f * zz - xx - yy) * c[39 + ch] + SH_C3[5] * z * (xx - yy) * c[42 + ch] +
+                    SH_C3[6] * x * (xx - 3.f * yy) * c[45 + ch]);
+            if constexpr (DEG >= 4) {
+              acc += (SH_C4[0] * xy * (xx - yy) * c[48 + ch] + SH_C4[1] * yz * (3.f * xx - yy) * c[51 + ch] +
+                      SH_C4[2] * xy * (7.f * zz - 1.f) * c[54 + ch] + SH_C4[3] * yz * (7.f * zz - 3.f) * c[57 + ch] +
+                      SH_C4[4] * (zz * (35.f * zz - 30.f) + 3.f) * c[60 + ch] +
+                      SH_C4[5] * xz * (7.f * zz - 3.f) * c[63 + ch] +
+                      SH_C4[6] * (xx - yy) * (7.f * zz - 1.f) * c[66 + ch] +
+                      SH_C4[7] * xz * (xx - 3.f * yy) * c[69 + ch] +
+                      SH_C4[8] * (xx * (xx - 3.f * yy) - yy * (3.f * xx - yy)) * c[72 + ch]);
+            }
           }
         }
+        rgbs[3 * (o + i) + ch] = fmaxf(acc + 0.5f, 0.f);
       }
-      rgbs[3 * i + ch] = fmaxf(acc + 0.5f, 0.f);
     }
+    project_point(i, px, py, pz, sc0, sc1, sc2, q0, q1, q2, q3, 1.f, vm, fx, fy, cx, cy, img_h, img_w, bw, 0.01f,
+                  xys + 2 * o, depths + o, radii + o, conics + 3 * o, nullptr, num_tiles_hit + o, nullptr);
   }
-  project_point(i, px, py, pz, sc0, sc1, sc2, q0, q1, q2, q3, 1.f, vm, fx, fy, cx, cy, img_h, img_w, bw, 0.01f, xys,
-                depths, radii, conics, nullptr, num_tiles_hit, nullptr);
+}
+
+// launch over n Gaussians x nviews cameras (c2ws [nviews][4][4]; per-view outputs at view * n records)
+int launch_prep(int n, int nviews, int num_bases, const float* means, const float* log_scales, const float* quats_raw,
+                const float* opac_logit, const float* dc, const float* rest, PrepStrides ld, const float* c2ws,
+                float fx, float fy, float cx, float cy, int img_h, int img_w, int bw, float* viewmat_out, float* rgbs,
+                float* opac, float* xys, float* depths, int* radii, float* conics, int* num_tiles_hit,
+                hipStream_t st) {
+  const unsigned blocks = sfx::ceil_div(n > 0 ? n : 1, 256);
+#define SFX_PREP(DG)                                                                                              \
+  render_prep_project_kernel<DG><<<blocks, 256, 0, st>>>(n, nviews, means, log_scales, quats_raw, opac_logit, dc,  \
+                                                         rest, ld, c2ws, fx, fy, cx, cy, img_h, img_w, bw,           \
+                                                         viewmat_out, rgbs, opac, xys, depths, radii, conics,         \
+                                                         num_tiles_hit)
+  switch (num_bases) {
+    case 1: SFX_PREP(0); break;
+    case 4: SFX_PREP(1); break;
+    case 9: SFX_PREP(2); break;
+    case 16: SFX_PREP(3); break;
+    default: SFX_PREP(4); break;
+  }
+#undef SFX_PREP
+  return SFX_OK;
 }
 
 // backward of project (gsplat project_gaussians_backward_kernel semantics: the
@@ -1478,10 +1516,10 @@ int sfx_render_prep_project(int n, int num_bases, const float* means, long long 
     SFX_REQUIRE(means && log_scales && quats_raw && opac_logit && features_dc && (num_bases == 1 || features_rest) &&
                     rgbs && opacities && xys && depths && radii && conics && num_tiles_hit,
                 "sfx_render_prep_project: null buffer");
-  render_prep_project_kernel<<<sfx::ceil_div(n > 0 ? n : 1, 256), 256, 0, sfx::as_stream(stream)>>>(
-      n, num_bases, means, log_scales, quats_raw, opac_logit, features_dc, features_rest,
-      PrepStrides{ld_means, ld_scales, ld_quats, ld_opac, ld_dc, ld_rest}, camera_to_world, fx, fy, cx,
-      cy, img_h, img_w, block_width, viewmat_out, rgbs, opacities, xys, depths, radii, conics, num_tiles_hit);
+  launch_prep(n, 1, num_bases, means, log_scales, quats_raw, opac_logit, features_dc, features_rest,
+              PrepStrides{ld_means, ld_scales, ld_quats, ld_opac, ld_dc, ld_rest}, camera_to_world, fx, fy, cx, cy,
+              img_h, img_w, block_width, viewmat_out, rgbs, opacities, xys, depths, radii, conics, num_tiles_hit,
+              sfx::as_stream(stream));
   return sfx::check_launch("sfx_render_prep_project");
 }
 
@@ -1581,11 +1619,10 @@ int sfx_render_prep_project_views(int n, int views, int num_bases, const float* 
   SFX_REQUIRE(means && log_scales && quats_raw && opac_logit && features_dc && (num_bases == 1 || features_rest) &&
                   rgbs && opacities && xys && depths && radii && conics && num_tiles_hit,
               "sfx_render_prep_project_views: null buffer");
-  dim3 grid(sfx::ceil_div(n, 256), views);
-  render_prep_project_kernel<<<grid, 256, 0, sfx::as_stream(stream)>>>(
-      n, num_bases, means, log_scales, quats_raw, opac_logit, features_dc, features_rest,
-      PrepStrides{ld_means, ld_scales, ld_quats, ld_opac, ld_dc, ld_rest}, camera_to_worlds, fx, fy, cx, cy, img_h,
-      img_w, block_width, nullptr, rgbs, opacities, xys, depths, radii, conics, num_tiles_hit);
+  launch_prep(n, views, num_bases, means, log_scales, quats_raw, opac_logit, features_dc, features_rest,
+              PrepStrides{ld_means, ld_scales, ld_quats, ld_opac, ld_dc, ld_rest}, camera_to_worlds, fx, fy, cx, cy,
+              img_h, img_w, block_width, nullptr, rgbs, opacities, xys, depths, radii, conics, num_tiles_hit,
+              sfx::as_stream(stream));
   return sfx::check_launch("sfx_render_prep_project_views");
 }
 

@@ -39,6 +39,29 @@ def main():
         step()
     torch.cuda.synchronize()
     print(f"wall {1e3 * (time.perf_counter() - t0) / steps:.3f} ms/step (no profiler)")
+    # host-only cost without the profiler's per-call overhead: wall time minus the time spent blocked in event
+    # waits (the library's host reads: HostRead.get -> Event.synchronize) -- what the Python side itself costs
+    waited = [0.0]
+    orig_sync = torch.cuda.Event.synchronize
+
+    def timed_sync(ev):
+        a = time.perf_counter()
+        orig_sync(ev)
+        waited[0] += time.perf_counter() - a
+    torch.cuda.Event.synchronize = timed_sync
+    try:
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        t_enq = time.perf_counter()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+    finally:
+        torch.cuda.Event.synchronize = orig_sync
+    print(f"host python {1e3 * (t_enq - t0 - waited[0]) / steps:.3f} ms/step (wall to last enqueue "
+          f"{1e3 * (t_enq - t0) / steps:.3f} ms, blocked in host reads {1e3 * waited[0] / steps:.3f} ms, "
+          f"GPU tail after the last enqueue {1e3 * (t1 - t_enq):.3f} ms)")
     pr = cProfile.Profile()
     pr.enable()
     for _ in range(steps):
