@@ -118,10 +118,10 @@ int sfx_rasterize_bwd(int tiles_x, int tiles_y, int block_width, int img_h, int 
                       const float* v_out, const float* v_out_alpha, float* v_xy, float* v_xy_abs, float* v_conic,
                       float* v_rgb, float* v_opacity, void* stream);
 
-/* Eval-path rasterizer over packed records (round 2): sfx_pack_raster_records writes one 48-byte record per
- * projected Gaussian, r0 = (x, y, opacity, conic.a), r1 = (conic.b, conic.c, r, g), r2 = (b, 0, 0, 0)
- * (records 16-byte aligned, 12 floats each); sfx_rasterize_fwd_views_packed is sfx_rasterize_fwd_views over
- * them (same outputs, bit for bit). */
+/* Eval-path rasterizer over packed records (round 2): sfx_pack_raster_records writes one record per projected
+ * Gaussian, r0 = (x, y, opacity, conic.a), r1 = (conic.b, conic.c, r, g), r2 = (b, 0, 0, 0) -- (ABI v13) 16 floats
+ * per record (64-byte stride; the fourth float4 is not written), records [n][16]; sfx_rasterize_fwd_views_packed is
+ * sfx_rasterize_fwd_views over them (same outputs, bit for bit). */
 int sfx_pack_raster_records(int n, const float* xys, const float* conics, const float* colors, const float* opacity,
                             float* records, void* stream);
 int sfx_rasterize_fwd_views_packed(int views, int tiles_x, int tiles_y, int block_width, int img_h, int img_w,
@@ -411,7 +411,13 @@ int sfx_isect_count_cull_views(int n_total, int n_per_view, const float* xys, co
 int sfx_isect_emit_cull_views(int n_total, int n_per_view, const float* xys, const float* conics,
                               const float* opacities, const float* depths, const int* radii, const int* cum_tiles_hit,
                               int tiles_x, int tiles_y, int block_width, int img_h, int img_w, int64_t* isect_ids,
-                              int32_t* gaussian_ids, void* stream);
+                              int32_t* gaussian_ids, const int* order, void* stream);
+/* (ABI v13) two-level intersection sort: keys[i] = the depth bits of depths[i] (u64).  Argsorting them (stable,
+ * sfx_sort_pairs_u64 bits [0, 32)) gives `order`; sfx_isect_emit_cull_views with that order (cum_tiles_hit = the
+ * inclusive scan of num_tiles_kept[order]) emits the pairs depth-sorted, and a stable sort of bits [32, 32 + tile
+ * bits) alone then yields gsplat's (tile, depth) order with its emission-order ties: the same list as a full 64-bit
+ * sort, with the depth passes run over Gaussian-views instead of pairs.  order = NULL: emission in index order. */
+int sfx_depth_keys(long long n, const float* depths, uint64_t* keys, void* stream);
 int sfx_rasterize_fwd_views_quad(int views, int tiles_x, int tiles_y, int block_width, int img_h, int img_w,
                                  const int32_t* gids_sorted, const int* tile_bins, const float* records,
                                  const float* background, int clamp_max1, float* final_Ts, int* final_idx,

@@ -732,7 +732,8 @@ rasterize_fwd_kernel(int tiles_x, int tiles_y, int bw, int img_h, int img_w,
 
 // ---- packed records (eval path) ------------------------------------------------
 // One 48-byte record per projected Gaussian, written once per view batch: r0 = (x, y, opacity, conic.a),
-// r1 = (conic.b, conic.c, r, g), r2 = (b, 0, 0, 0).  The rasterizer's per-batch fetch is one gather of a
+// r1 = (conic.b, conic.c, r, g), r2 = (b, 0, 0, 0), at a 64-byte stride (one 64-byte sector per record gather; at
+// 48 bytes two of every four records straddle a sector boundary: 1.5 sectors fetched per 36 bytes used).  The rasterizer's per-batch fetch is one gather of a
 // 16-byte-aligned record instead of four gathers from four arrays (xys 8 B, opacity 4 B, conics 12 B,
 // colours 12 B).  Measured: the same kernel time as the four-array form (config E 2285 vs 2278 us for 9
 // 1920x1080 views) -- the rasterizer is not bound by its gathers.  A wave-uniform skip of Gaussians whose
@@ -743,9 +744,9 @@ __global__ void pack_raster_records_kernel(int n, const float* __restrict__ xys,
                                            float4* __restrict__ rec) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  rec[3 * i + 0] = make_float4(xys[2 * i], xys[2 * i + 1], opacity[i], conics[3 * i]);
-  rec[3 * i + 1] = make_float4(conics[3 * i + 1], conics[3 * i + 2], colors[3 * i], colors[3 * i + 1]);
-  rec[3 * i + 2] = make_float4(colors[3 * i + 2], 0.f, 0.f, 0.f);
+  rec[4 * i + 0] = make_float4(xys[2 * i], xys[2 * i + 1], opacity[i], conics[3 * i]);
+  rec[4 * i + 1] = make_float4(conics[3 * i + 1], conics[3 * i + 2], colors[3 * i], colors[3 * i + 1]);
+  rec[4 * i + 2] = make_float4(colors[3 * i + 2], 0.f, 0.f, 0.f);
 }
 
 // rasterize_fwd_kernel over packed records: the same per-pixel arithmetic in the same order (bit-identical
@@ -787,9 +788,9 @@ rasterize_fwd_packed_kernel(int tiles_x, int tiles_y, int bw, int img_h, int img
     const int idx = batch_start + tr;
     if (idx < range_y) {
       const long long g = gids_sorted[idx];
-      r0_batch[tr] = rec[3 * g];
-      r1_batch[tr] = rec[3 * g + 1];
-      r2_batch[tr] = reinterpret_cast<const float*>(rec + 3 * g + 2)[0];
+      r0_batch[tr] = rec[4 * g];
+      r1_batch[tr] = rec[4 * g + 1];
+      r2_batch[tr] = reinterpret_cast<const float*>(rec + 4 * g + 2)[0];
     }
     __syncthreads();
     const int batch_size = min(block_size, range_y - batch_start);
@@ -964,26 +965,29 @@ isect_count_cull_kernel(int n, int n_per_view, const float* __restrict__ xys, co
   if (i < n) num_tiles_kept[i] = cnt;
 }
 
-// isect_emit_kernel over the surviving tiles only (same walk order: the list is a subsequence of gsplat's)
+// isect_emit_kernel over the surviving tiles only (same walk order: the list is a subsequence of gsplat's).
+// order (optional): emit the Gaussian-views in this order (thread j emits order[j], cum_tiles_hit is over j) -- the
+// depth order of the two-level sort (sfx_depth_keys): the pairs then only need a stable sort by tile.
 __global__ void __launch_bounds__(256)
 isect_emit_cull_kernel(int n, int n_per_view, const float* __restrict__ xys, const float* __restrict__ conics,
                        const float* __restrict__ opac, const float* __restrict__ depths,
                        const int* __restrict__ radii, const int* __restrict__ cum_tiles_hit, int tiles_x,
                        int tiles_y, int bw, int img_h, int img_w, int64_t* __restrict__ isect_ids,
-                       int32_t* __restrict__ gaussian_ids) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+                       int32_t* __restrict__ gaussian_ids, const int* __restrict__ order) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  const int i = (order && j < n) ? order[j] : j;
   const int lane = threadIdx.x & 63;
   CullWalk w;
   w.x0 = w.y0 = w.x1 = w.y1 = 0;  // empty walk for lanes without a Gaussian (or without surviving tiles)
   w.area = 0;
   w.g = cull_setup(0.f, 0.f, 0.f, 0.f, 0.f, 0.f);
   int cur = 0, end = 0;
-  if (i < n) {
-    cur = (i == 0) ? 0 : cum_tiles_hit[i - 1];
-    end = cum_tiles_hit[i];
+  if (j < n) {
+    cur = (j == 0) ? 0 : cum_tiles_hit[j - 1];
+    end = cum_tiles_hit[j];
     if (end > cur) w = cull_walk_setup(i, xys, conics, opac, radii, tiles_x, tiles_y, bw);
   }
-  const int64_t depth_id = i < n ? (int64_t)__float_as_int(depths[i]) & 0xffffffffll : 0;
+  const int64_t depth_id = j < n ? (int64_t)__float_as_int(depths[i]) & 0xffffffffll : 0;
   const int64_t tile_base = (int64_t)(i / n_per_view) * tiles_x * tiles_y;
   if (w.area <= CULL_SMALL_AREA) {
     for (int ty = w.y0; ty < w.y1; ++ty)
@@ -1022,6 +1026,13 @@ isect_emit_cull_kernel(int n, int n_per_view, const float* __restrict__ xys, con
       pos += __popcll(bal);
     }
   }
+}
+
+// keys[i] = the bit pattern of depths[i] (u64, upper half 0): the depth half of gsplat's (tile << 32 | depth) key
+__global__ void __launch_bounds__(256) depth_keys_kernel(long long n, const float* __restrict__ depths,
+                                                         uint64_t* __restrict__ keys) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) keys[i] = (uint64_t)(unsigned)__float_as_int(depths[i]);
 }
 
 // rasterize_fwd_packed_kernel with per-wave Gaussian lists: the 16x16 tile is split into four 8x8 quadrants, one
@@ -1077,11 +1088,11 @@ rasterize_fwd_quad_kernel(int tiles_x, int tiles_y, int img_h, int img_w, const 
     unsigned m = 0;
     if (idx < range_y) {
       const long long g = gids_sorted[idx];
-      const float4 a = rec[3 * g];
-      const float4 q = rec[3 * g + 1];
+      const float4 a = rec[4 * g];
+      const float4 q = rec[4 * g + 1];
       r0_batch[tr] = a;
       r1_batch[tr] = q;
-      r2_batch[tr] = reinterpret_cast<const float*>(rec + 3 * g + 2)[0];
+      r2_batch[tr] = reinterpret_cast<const float*>(rec + 4 * g + 2)[0];
       const CullG cg = cull_setup(a.x, a.y, a.w, q.x, q.y, a.z);
 #pragma unroll
       for (int qd = 0; qd < 4; ++qd) {
@@ -1702,7 +1713,7 @@ int sfx_isect_count_cull_views(int n_total, int n_per_view, const float* xys, co
 int sfx_isect_emit_cull_views(int n_total, int n_per_view, const float* xys, const float* conics,
                               const float* opacities, const float* depths, const int* radii, const int* cum_tiles_hit,
                               int tiles_x, int tiles_y, int block_width, int img_h, int img_w, int64_t* isect_ids,
-                              int32_t* gaussian_ids, void* stream) {
+                              int32_t* gaussian_ids, const int* order, void* stream) {
   SFX_REQUIRE(n_total >= 0 && n_per_view > 0 && n_total % n_per_view == 0, "sfx_isect_emit_cull_views: bad sizes");
   SFX_REQUIRE(block_width > 1 && block_width <= 16, "sfx_isect_emit_cull_views: block_width must be in (1,16]");
   SFX_REQUIRE(tiles_x == (img_w + block_width - 1) / block_width && tiles_y == (img_h + block_width - 1) / block_width,
@@ -1712,8 +1723,16 @@ int sfx_isect_emit_cull_views(int n_total, int n_per_view, const float* xys, con
               "sfx_isect_emit_cull_views: null buffer");
   isect_emit_cull_kernel<<<sfx::ceil_div(n_total, 256), 256, 0, sfx::as_stream(stream)>>>(
       n_total, n_per_view, xys, conics, opacities, depths, radii, cum_tiles_hit, tiles_x, tiles_y, block_width, img_h,
-      img_w, isect_ids, gaussian_ids);
+      img_w, isect_ids, gaussian_ids, order);
   return sfx::check_launch("sfx_isect_emit_cull_views");
+}
+
+int sfx_depth_keys(long long n, const float* depths, uint64_t* keys, void* stream) {
+  SFX_REQUIRE(n >= 0, "sfx_depth_keys: n < 0");
+  if (n == 0) return SFX_OK;
+  SFX_REQUIRE(depths && keys, "sfx_depth_keys: null buffer");
+  depth_keys_kernel<<<sfx::ceil_div(n, 256), 256, 0, sfx::as_stream(stream)>>>(n, depths, keys);
+  return sfx::check_launch("sfx_depth_keys");
 }
 
 int sfx_rasterize_fwd_views_quad(int views, int tiles_x, int tiles_y, int block_width, int img_h, int img_w,

@@ -20,6 +20,7 @@ import torch
 from torch import Tensor
 
 from . import _lib
+from . import ptv3_ops as ops
 from ._lib import F, I, L, P, call, ptr, stream
 from .gsplat_compat import (_RasterizeGaussians, bin_and_sort_gaussians, compute_cumulative_intersects,
                             project_gaussians, rasterize_gaussians, spherical_harmonics)
@@ -30,6 +31,9 @@ BLOCK_WIDTH = 16
 # intersection-level parity tests compare key for key).
 import os as _os
 RENDER_CULL = _os.environ.get("SFX_RENDER_CULL", "1") != "0"
+# culled eval path: two-level intersection sort (depth argsort of the Gaussian-views, then the tile bits of the
+# depth-ordered pairs); SFX_SORT_TWO_LEVEL=0: one radix sort of all 32 + tile bits of every pair
+SORT_TWO_LEVEL = _os.environ.get("SFX_SORT_TWO_LEVEL", "1") != "0"
 C0 = 0.28209479177387814
 
 
@@ -52,7 +56,8 @@ _lib.register("sfx_rasterize_fwd_views", [I, I, I, I, I, I, P, P, P, P, P, P, P,
 _lib.register("sfx_pack_raster_records", [I, P, P, P, P, P, P])
 _lib.register("sfx_rasterize_fwd_views_packed", [I, I, I, I, I, I, P, P, P, P, I, P, P, P, P, P])
 _lib.register("sfx_isect_count_cull_views", [I, I, P, P, P, P, I, I, I, I, I, P, P])
-_lib.register("sfx_isect_emit_cull_views", [I, I, P, P, P, P, P, P, I, I, I, I, I, P, P, P])
+_lib.register("sfx_isect_emit_cull_views", [I, I, P, P, P, P, P, P, I, I, I, I, I, P, P, P, P])
+_lib.register("sfx_depth_keys", [L, P, P, P])
 _lib.register("sfx_rasterize_fwd_views_quad", [I, I, I, I, I, I, P, P, P, P, I, P, P, P, P, P])
 
 
@@ -179,7 +184,7 @@ def _render_fused_views(gs, c2ws, cameras, meta=None):
     # inclusive scan of the tiles hit; the per-view ends (and the total = the last of them) reach the host in ONE
     # asynchronous read, with the count-independent record packing enqueued in front of the wait
     cum = torch.empty(V * n, device=dev, dtype=torch.int32)
-    rec = f(V * n, 12)  # packed 48-byte records: one gather per Gaussian in the rasterizer's batch fetch
+    rec = f(V * n, 16)  # packed 64-byte records: one gather per Gaussian in the rasterizer's batch fetch
     bw = BLOCK_WIDTH
     tiles_x, tiles_y = (W + bw - 1) // bw, (H + bw - 1) // bw
     T = tiles_x * tiles_y
@@ -195,6 +200,16 @@ def _render_fused_views(gs, c2ws, cameras, meta=None):
         call("sfx_scan_i32", V * n, ptr(kept), ptr(cum), 1, ptr(ws), ws.numel(), ptr(tot_dev), stream())
         ends_rd = _lib.HostRead(cum.view(V, n)[:, -1])
         call("sfx_pack_raster_records", V * n, ptr(xys), ptr(conics), ptr(rgbs), ptr(opac), ptr(rec), stream())
+        if cull and SORT_TWO_LEVEL:
+            # two-level sort (include/sfx.h sfx_depth_keys): the Gaussian-views argsorted by depth (4 passes over
+            # V n keys), their surviving tile counts scanned in that order -- queued while the host waits for `ends`
+            dkeys = torch.empty(V * n, device=dev, dtype=torch.int64)
+            call("sfx_depth_keys", V * n, ptr(depths), ptr(dkeys), stream())
+            _, dorder = ops._sort(dkeys, None, 0, 32)
+            del dkeys
+            cum_o = torch.empty(V * n, device=dev, dtype=torch.int32)
+            call("sfx_scan_i32", V * n, ptr(kept.index_select(0, dorder)), ptr(cum_o), 1, ptr(ws), ws.numel(),
+                 ptr(tot_dev), stream())
         ends = ends_rd.get()
     else:
         ends = [0] * V
@@ -209,17 +224,20 @@ def _render_fused_views(gs, c2ws, cameras, meta=None):
     if total > 0:
         isect = f(total, dt=torch.int64)
         gids = f(total, dt=torch.int32)
+        two_level = cull and SORT_TWO_LEVEL
         if cull:
             call("sfx_isect_emit_cull_views", V * n, n, ptr(xys), ptr(conics), ptr(opac), ptr(depths), ptr(radii),
-                 ptr(cum), tiles_x, tiles_y, bw, H, W, ptr(isect), ptr(gids), stream())
+                 ptr(cum_o if two_level else cum), tiles_x, tiles_y, bw, H, W, ptr(isect), ptr(gids),
+                 ptr(dorder) if two_level else None, stream())
         else:
             call("sfx_isect_emit_views", V * n, n, ptr(xys), ptr(depths), ptr(radii), ptr(cum), tiles_x, tiles_y, bw,
                  ptr(isect), ptr(gids), stream())
         isect_s, gids_s = torch.empty_like(isect), torch.empty_like(gids)
         key_bits = 32 + max(1, int(V * T - 1).bit_length())
         ws = _lib.workspace(_lib.fn("sfx_sort_workspace_bytes")(total), dev)
-        call("sfx_sort_pairs_u64", total, ptr(isect), ptr(gids), ptr(isect_s), ptr(gids_s), 0, key_bits, ptr(ws),
-             ws.numel(), stream())
+        # two-level: the pairs arrive depth-sorted, so a stable sort of the tile bits alone finishes gsplat's order
+        call("sfx_sort_pairs_u64", total, ptr(isect), ptr(gids), ptr(isect_s), ptr(gids_s), 32 if two_level else 0,
+             key_bits, ptr(ws), ws.numel(), stream())
         del isect, gids
         bins = f(V * T, 2, dt=torch.int32)
         call("sfx_tile_bins", total, ptr(isect_s), V * T, ptr(bins), stream())
