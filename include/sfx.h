@@ -411,13 +411,15 @@ int sfx_isect_count_cull_views(int n_total, int n_per_view, const float* xys, co
 int sfx_isect_emit_cull_views(int n_total, int n_per_view, const float* xys, const float* conics,
                               const float* opacities, const float* depths, const int* radii, const int* cum_tiles_hit,
                               int tiles_x, int tiles_y, int block_width, int img_h, int img_w, int64_t* isect_ids,
-                              int32_t* gaussian_ids, const int* order, void* stream);
+                              int32_t* gaussian_ids, const int* rank, void* stream);
 /* (ABI v13) two-level intersection sort: keys[i] = the depth bits of depths[i] (u64).  Argsorting them (stable,
- * sfx_sort_pairs_u64 bits [0, 32)) gives `order`; sfx_isect_emit_cull_views with that order (cum_tiles_hit = the
- * inclusive scan of num_tiles_kept[order]) emits the pairs depth-sorted, and a stable sort of bits [32, 32 + tile
- * bits) alone then yields gsplat's (tile, depth) order with its emission-order ties: the same list as a full 64-bit
- * sort, with the depth passes run over Gaussian-views instead of pairs.  order = NULL: emission in index order. */
+ * sfx_sort_pairs_u64 bits [0, 32)) gives `order`, sfx_invert_permutation its inverse `rank`;
+ * sfx_isect_emit_cull_views with that rank (cum_tiles_hit = the inclusive scan of num_tiles_kept[order]) emits the
+ * pairs depth-sorted, and a stable sort of bits [32, 32 + tile bits) alone then yields gsplat's (tile, depth) order
+ * with its emission-order ties: the same list as a full 64-bit sort, with the depth passes run over Gaussian-views
+ * instead of pairs.  rank = NULL: emission in index order. */
 int sfx_depth_keys(long long n, const float* depths, uint64_t* keys, void* stream);
+int sfx_invert_permutation(long long n, const int* perm, int* inv, void* stream);
 int sfx_rasterize_fwd_views_quad(int views, int tiles_x, int tiles_y, int block_width, int img_h, int img_w,
                                  const int32_t* gids_sorted, const int* tile_bins, const float* records,
                                  const float* background, int clamp_max1, float* final_Ts, int* final_idx,

@@ -56,45 +56,44 @@ __global__ void __launch_bounds__(256) point_embed_kernel(int n, int K, const fl
                                                           const float* __restrict__ scale,
                                                           const float* __restrict__ shift, float* __restrict__ y,
                                                           long long ldy) {
-  constexpr int NO = N / 4;  // outputs per thread
+  // one point per thread, all N outputs in registers: W^T is staged once per 256 points and read as wave-uniform
+  // (broadcast) LDS float4s, each input row is read once (was: 64 points per block, 4 threads per point each
+  // re-reading the row, and a K x N staging with a division per element per 64 points -- 182 us at 500k x 59)
   __shared__ __attribute__((aligned(16))) float wt[64 * N];  // [k][o]
   __shared__ __attribute__((aligned(16))) float cst[3][N];
-  for (int e = threadIdx.x; e < K * N; e += 256) {
-    const int o = e / K, k = e - o * K;
-    wt[k * N + o] = w[(long long)o * K + k];
-  }
+  for (int o = 0; o < N; ++o)
+    if (threadIdx.x < K) wt[threadIdx.x * N + o] = w[(long long)o * K + threadIdx.x];
   for (int o = threadIdx.x; o < N; o += 256) {
     cst[0][o] = b ? b[o] : 0.f;
     cst[1][o] = scale ? scale[o] : 1.f;
     cst[2][o] = shift ? shift[o] : 0.f;
   }
   __syncthreads();
-  const int i = blockIdx.x * 64 + (threadIdx.x >> 2);
-  const int q = threadIdx.x & 3;
+  const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
-  float acc[NO];
+  float acc[N];
 #pragma unroll
-  for (int j = 0; j < NO; ++j) acc[j] = cst[0][q * NO + j];
+  for (int j = 0; j < N; ++j) acc[j] = cst[0][j];
   const float* xr = x + (long long)i * ldx;
   for (int k = 0; k < K; ++k) {
     const float xv = xr[k];
 #pragma unroll
-    for (int j = 0; j < NO; j += 4) {
-      const float4 wv = *reinterpret_cast<const float4*>(&wt[k * N + q * NO + j]);
+    for (int j = 0; j < N; j += 4) {
+      const float4 wv = *reinterpret_cast<const float4*>(&wt[k * N + j]);
       acc[j] = fmaf(xv, wv.x, acc[j]);
       acc[j + 1] = fmaf(xv, wv.y, acc[j + 1]);
       acc[j + 2] = fmaf(xv, wv.z, acc[j + 2]);
       acc[j + 3] = fmaf(xv, wv.w, acc[j + 3]);
     }
   }
-  float* yr = y + (long long)i * ldy + q * NO;
+  float* yr = y + (long long)i * ldy;
 #pragma unroll
-  for (int j = 0; j < NO; j += 4) {
+  for (int j = 0; j < N; j += 4) {
     float4 o4;
     float* ov = reinterpret_cast<float*>(&o4);
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      const float v = acc[j + t] * cst[1][q * NO + j + t] + cst[2][q * NO + j + t];
+      const float v = acc[j + t] * cst[1][j + t] + cst[2][j + t];
       ov[t] = 0.5f * v * (1.f + erff(v * 0.70710678118654752f));
     }
     *reinterpret_cast<float4*>(yr + j) = o4;
@@ -158,9 +157,9 @@ int sfx_point_embed(int n, int K, int N, const float* x, long long ldx, const fl
               "sfx_point_embed: bad buffers");
   hipStream_t st = sfx::as_stream(stream);
   if (N == 64)
-    point_embed_kernel<64><<<sfx::ceil_div(n, 64), 256, 0, st>>>(n, K, x, ldx, w, b, scale, shift, y, ldy);
+    point_embed_kernel<64><<<sfx::ceil_div(n, 256), 256, 0, st>>>(n, K, x, ldx, w, b, scale, shift, y, ldy);
   else
-    point_embed_kernel<32><<<sfx::ceil_div(n, 64), 256, 0, st>>>(n, K, x, ldx, w, b, scale, shift, y, ldy);
+    point_embed_kernel<32><<<sfx::ceil_div(n, 256), 256, 0, st>>>(n, K, x, ldx, w, b, scale, shift, y, ldy);
   return sfx::check_launch("sfx_point_embed");
 }
 

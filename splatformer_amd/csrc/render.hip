@@ -966,28 +966,29 @@ isect_count_cull_kernel(int n, int n_per_view, const float* __restrict__ xys, co
 }
 
 // isect_emit_kernel over the surviving tiles only (same walk order: the list is a subsequence of gsplat's).
-// order (optional): emit the Gaussian-views in this order (thread j emits order[j], cum_tiles_hit is over j) -- the
-// depth order of the two-level sort (sfx_depth_keys): the pairs then only need a stable sort by tile.
+// rank (optional): Gaussian-view i is the rank[i]-th in emission order and cum_tiles_hit is over that order -- the
+// depth order of the two-level sort (sfx_depth_keys), so the pairs only need a stable sort by tile.  Threads stay
+// in index order (coalesced reads of the per-Gaussian inputs); only the output offsets follow the rank.
 __global__ void __launch_bounds__(256)
 isect_emit_cull_kernel(int n, int n_per_view, const float* __restrict__ xys, const float* __restrict__ conics,
                        const float* __restrict__ opac, const float* __restrict__ depths,
                        const int* __restrict__ radii, const int* __restrict__ cum_tiles_hit, int tiles_x,
                        int tiles_y, int bw, int img_h, int img_w, int64_t* __restrict__ isect_ids,
-                       int32_t* __restrict__ gaussian_ids, const int* __restrict__ order) {
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  const int i = (order && j < n) ? order[j] : j;
+                       int32_t* __restrict__ gaussian_ids, const int* __restrict__ rank) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int j = (rank && i < n) ? rank[i] : i;
   const int lane = threadIdx.x & 63;
   CullWalk w;
   w.x0 = w.y0 = w.x1 = w.y1 = 0;  // empty walk for lanes without a Gaussian (or without surviving tiles)
   w.area = 0;
   w.g = cull_setup(0.f, 0.f, 0.f, 0.f, 0.f, 0.f);
   int cur = 0, end = 0;
-  if (j < n) {
+  if (i < n) {
     cur = (j == 0) ? 0 : cum_tiles_hit[j - 1];
     end = cum_tiles_hit[j];
     if (end > cur) w = cull_walk_setup(i, xys, conics, opac, radii, tiles_x, tiles_y, bw);
   }
-  const int64_t depth_id = j < n ? (int64_t)__float_as_int(depths[i]) & 0xffffffffll : 0;
+  const int64_t depth_id = i < n ? (int64_t)__float_as_int(depths[i]) & 0xffffffffll : 0;
   const int64_t tile_base = (int64_t)(i / n_per_view) * tiles_x * tiles_y;
   if (w.area <= CULL_SMALL_AREA) {
     for (int ty = w.y0; ty < w.y1; ++ty)
@@ -1026,6 +1027,13 @@ isect_emit_cull_kernel(int n, int n_per_view, const float* __restrict__ xys, con
       pos += __popcll(bal);
     }
   }
+}
+
+// inv[perm[j]] = j
+__global__ void __launch_bounds__(256) invert_perm_kernel(long long n, const int* __restrict__ perm,
+                                                          int* __restrict__ inv) {
+  const long long j = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (j < n) inv[perm[j]] = (int)j;
 }
 
 // keys[i] = the bit pattern of depths[i] (u64, upper half 0): the depth half of gsplat's (tile << 32 | depth) key
@@ -1713,7 +1721,7 @@ int sfx_isect_count_cull_views(int n_total, int n_per_view, const float* xys, co
 int sfx_isect_emit_cull_views(int n_total, int n_per_view, const float* xys, const float* conics,
                               const float* opacities, const float* depths, const int* radii, const int* cum_tiles_hit,
                               int tiles_x, int tiles_y, int block_width, int img_h, int img_w, int64_t* isect_ids,
-                              int32_t* gaussian_ids, const int* order, void* stream) {
+                              int32_t* gaussian_ids, const int* rank, void* stream) {
   SFX_REQUIRE(n_total >= 0 && n_per_view > 0 && n_total % n_per_view == 0, "sfx_isect_emit_cull_views: bad sizes");
   SFX_REQUIRE(block_width > 1 && block_width <= 16, "sfx_isect_emit_cull_views: block_width must be in (1,16]");
   SFX_REQUIRE(tiles_x == (img_w + block_width - 1) / block_width && tiles_y == (img_h + block_width - 1) / block_width,
@@ -1723,8 +1731,16 @@ int sfx_isect_emit_cull_views(int n_total, int n_per_view, const float* xys, con
               "sfx_isect_emit_cull_views: null buffer");
   isect_emit_cull_kernel<<<sfx::ceil_div(n_total, 256), 256, 0, sfx::as_stream(stream)>>>(
       n_total, n_per_view, xys, conics, opacities, depths, radii, cum_tiles_hit, tiles_x, tiles_y, block_width, img_h,
-      img_w, isect_ids, gaussian_ids, order);
+      img_w, isect_ids, gaussian_ids, rank);
   return sfx::check_launch("sfx_isect_emit_cull_views");
+}
+
+int sfx_invert_permutation(long long n, const int* perm, int* inv, void* stream) {
+  SFX_REQUIRE(n >= 0 && n < (1ll << 31), "sfx_invert_permutation: n out of range");
+  if (n == 0) return SFX_OK;
+  SFX_REQUIRE(perm && inv && perm != inv, "sfx_invert_permutation: null or aliased buffer");
+  invert_perm_kernel<<<sfx::ceil_div(n, 256), 256, 0, sfx::as_stream(stream)>>>(n, perm, inv);
+  return sfx::check_launch("sfx_invert_permutation");
 }
 
 int sfx_depth_keys(long long n, const float* depths, uint64_t* keys, void* stream) {

@@ -58,6 +58,7 @@ _lib.register("sfx_rasterize_fwd_views_packed", [I, I, I, I, I, I, P, P, P, P, I
 _lib.register("sfx_isect_count_cull_views", [I, I, P, P, P, P, I, I, I, I, I, P, P])
 _lib.register("sfx_isect_emit_cull_views", [I, I, P, P, P, P, P, P, I, I, I, I, I, P, P, P, P])
 _lib.register("sfx_depth_keys", [L, P, P, P])
+_lib.register("sfx_invert_permutation", [L, P, P, P])
 _lib.register("sfx_rasterize_fwd_views_quad", [I, I, I, I, I, I, P, P, P, P, I, P, P, P, P, P])
 
 
@@ -207,6 +208,8 @@ def _render_fused_views(gs, c2ws, cameras, meta=None):
             call("sfx_depth_keys", V * n, ptr(depths), ptr(dkeys), stream())
             _, dorder = ops._sort(dkeys, None, 0, 32)
             del dkeys
+            drank = torch.empty_like(dorder)
+            call("sfx_invert_permutation", V * n, ptr(dorder), ptr(drank), stream())
             cum_o = torch.empty(V * n, device=dev, dtype=torch.int32)
             call("sfx_scan_i32", V * n, ptr(kept.index_select(0, dorder)), ptr(cum_o), 1, ptr(ws), ws.numel(),
                  ptr(tot_dev), stream())
@@ -228,7 +231,7 @@ def _render_fused_views(gs, c2ws, cameras, meta=None):
         if cull:
             call("sfx_isect_emit_cull_views", V * n, n, ptr(xys), ptr(conics), ptr(opac), ptr(depths), ptr(radii),
                  ptr(cum_o if two_level else cum), tiles_x, tiles_y, bw, H, W, ptr(isect), ptr(gids),
-                 ptr(dorder) if two_level else None, stream())
+                 ptr(drank) if two_level else None, stream())
         else:
             call("sfx_isect_emit_views", V * n, n, ptr(xys), ptr(depths), ptr(radii), ptr(cum), tiles_x, tiles_y, bw,
                  ptr(isect), ptr(gids), stream())
