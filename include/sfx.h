@@ -387,7 +387,9 @@ int sfx_render_prep_project_views(int n, int views, int num_bases, const float* 
                                   long long ld_rest, const float* camera_to_worlds, float fx, float fy, float cx,
                                   float cy, int img_h, int img_w, int block_width, float* rgbs, float* opacities,
                                   float* xys, float* depths, int* radii, float* conics, int* num_tiles_hit,
-                                  void* stream);
+                                  float* records, void* stream);
+/* (ABI v13) records (optional, [views * n][16]): also writes sfx_pack_raster_records' record of every
+ * Gaussian-view (no separate packing pass) */
 int sfx_isect_emit_views(int n_total, int n_per_view, const float* xys, const float* depths, const int* radii,
                          const int* cum_tiles_hit, int tiles_x, int tiles_y, int block_width, int64_t* isect_ids,
                          int32_t* gaussian_ids, void* stream);
@@ -477,7 +479,9 @@ size_t sfx_mlp_params_floats(int C);
 int sfx_mlp_pack(int C, const float* w1, const float* b1, const float* w2, const float* b2, const float* gamma,
                  const float* beta, float* stream, float* params, int* workspace, void* stream_);
 int sfx_block_mlp(int M, int C, const float* x, long long ldx, const float* stream, const float* params, float eps,
-                  float* y, long long ldy, void* stream_);
+                  float* y, long long ldy, int* rowexp, void* stream_);
+/* (ABI v13) rowexp (optional, [M] int32): also writes sfx_subm_rowexp(y) -- the next Block's fused SubM conv input
+ * exponents -- from the output rows it just computed */
 /* (ABI v13) training forward of the same tail (train.py:240-289, model.train()): also stores z [M][4C] (contiguous)
  * = fc1(LN2(x)), the pre-activation the backward needs, and applies the DropPath keep factor rowscale [M] (NULL:
  * none) to the branch: y = x + rowscale * (fc2(GELU(z)) + b2). */

@@ -381,6 +381,7 @@ __global__ void __launch_bounds__(WAVES * 64, (WAVES == 4 && C > 128) ? 1 : 2)
   // ---- epilogue: Y = X2 + acc2 / (t s_c) + b2, 16-byte stores of 4 consecutive channels ----
   const __amdgpu_buffer_rsrc_t rY = rsrc_ext(Y, (unsigned)M * (unsigned)ldy * 4u);
   const unsigned yr = (unsigned)prow * (unsigned)ldy;
+  float ymax = 0.f;  // MLP_EVAL with Z: this point's max |Y| -> the next fused SubM conv's row exponent
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
     const float4* pp = reinterpret_cast<const float4*>(s_par + 10 * C + 2 * fc2_par_index(b, h, 0));
@@ -402,6 +403,24 @@ __global__ void __launch_bounds__(WAVES * 64, (WAVES == 4 && C > 128) ? 1 : 2)
         y.w = xres.w + rsp * (acc2[b][4 * g4 + 3] * (tinv * w23.z) + w23.w);
       }
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, y), rY, pok ? (yr + c0) * 4u : OOB, 0, 0);
+      if constexpr (KIND == MLP_EVAL) ymax = fmaxf(ymax, fmaxf(fmaxf(fabsf(y.x), fabsf(y.y)), fmaxf(fabsf(y.z), fabsf(y.w))));
+    }
+  }
+  if constexpr (KIND == MLP_EVAL) {
+    // sfx_subm_rowexp of the output row (csrc/subm_fused.hip, same rule): max in [2^14, 2^15), 127 for a zero row,
+    // 0 for inf / nan -- the next Block's fused conv reads it instead of re-reading the row
+    if (Z) {
+      ymax = fmaxf(ymax, __shfl_xor(ymax, 32, 64));
+      if (h == 0 && pok) {
+        int e = 127;
+        if (ymax > 0.f && ymax <= 3.4028235e38f) {
+          e = 15 - __builtin_amdgcn_frexp_expf(ymax);
+          e = e > 126 ? 126 : (e < -126 ? -126 : e);
+        } else if (!(ymax <= 3.4028235e38f)) {
+          e = 0;
+        }
+        reinterpret_cast<int*>(Z)[prow] = e;
+      }
     }
   }
 }
@@ -579,7 +598,7 @@ int sfx_mlp_pack(int C, const float* w1, const float* b1, const float* w2, const
 }
 
 int sfx_block_mlp(int M, int C, const float* x, long long ldx, const float* stream, const float* params, float eps,
-                  float* y, long long ldy, void* stream_) {
+                  float* y, long long ldy, int* rowexp, void* stream_) {
   SFX_REQUIRE(M >= 0 && mlp_channels_ok(C), "sfx_block_mlp: C must be one of 64, 96, 128, 256 (got %d)", C);
   if (M == 0) return SFX_OK;
   SFX_REQUIRE(x && stream && params && y, "sfx_block_mlp: null buffer");
@@ -602,17 +621,17 @@ int sfx_block_mlp(int M, int C, const float* x, long long ldx, const float* stre
   switch (C) {
     // (waves, ring phases): 4 waves = 128 points per workgroup, 2 workgroups per CU for C <= 128 (64 KB ring);
     // C = 256 runs 4 waves as 2 hidden-split pairs (its LN2 fragments + output accumulators fill 512 registers)
-    case 64: return waves == 4 ? (hs == 2 ? run_impl<64, 4, 4, true>(M, x, ldx, stream, params, eps, y, ldy, st)
-                                          : run_impl<64, 4, 4>(M, x, ldx, stream, params, eps, y, ldy, st))
-                               : run_impl<64, 8, 4>(M, x, ldx, stream, params, eps, y, ldy, st);
-    case 96: return waves == 4 ? (hs == 2 ? run_impl<96, 4, 4, true>(M, x, ldx, stream, params, eps, y, ldy, st)
-                                          : run_impl<96, 4, 4>(M, x, ldx, stream, params, eps, y, ldy, st))
-                               : run_impl<96, 8, 4>(M, x, ldx, stream, params, eps, y, ldy, st);
-    case 128: return waves == 4 ? (hs >= 1 ? run_impl<128, 4, 4, true>(M, x, ldx, stream, params, eps, y, ldy, st)
-                                          : run_impl<128, 4, 4>(M, x, ldx, stream, params, eps, y, ldy, st))
-                                : run_impl<128, 8, 4>(M, x, ldx, stream, params, eps, y, ldy, st);
-    default: return hs ? run_impl<256, 4, SFX_MLP_RING256, true>(M, x, ldx, stream, params, eps, y, ldy, st)
-                       : run_impl<256, 4, SFX_MLP_RING256>(M, x, ldx, stream, params, eps, y, ldy, st);
+    case 64: return waves == 4 ? (hs == 2 ? run_impl<64, 4, 4, true>(M, x, ldx, stream, params, eps, y, ldy, st, nullptr, reinterpret_cast<float*>(rowexp))
+                                          : run_impl<64, 4, 4>(M, x, ldx, stream, params, eps, y, ldy, st, nullptr, reinterpret_cast<float*>(rowexp)))
+                               : run_impl<64, 8, 4>(M, x, ldx, stream, params, eps, y, ldy, st, nullptr, reinterpret_cast<float*>(rowexp));
+    case 96: return waves == 4 ? (hs == 2 ? run_impl<96, 4, 4, true>(M, x, ldx, stream, params, eps, y, ldy, st, nullptr, reinterpret_cast<float*>(rowexp))
+                                          : run_impl<96, 4, 4>(M, x, ldx, stream, params, eps, y, ldy, st, nullptr, reinterpret_cast<float*>(rowexp)))
+                               : run_impl<96, 8, 4>(M, x, ldx, stream, params, eps, y, ldy, st, nullptr, reinterpret_cast<float*>(rowexp));
+    case 128: return waves == 4 ? (hs >= 1 ? run_impl<128, 4, 4, true>(M, x, ldx, stream, params, eps, y, ldy, st, nullptr, reinterpret_cast<float*>(rowexp))
+                                          : run_impl<128, 4, 4>(M, x, ldx, stream, params, eps, y, ldy, st, nullptr, reinterpret_cast<float*>(rowexp)))
+                                : run_impl<128, 8, 4>(M, x, ldx, stream, params, eps, y, ldy, st, nullptr, reinterpret_cast<float*>(rowexp));
+    default: return hs ? run_impl<256, 4, SFX_MLP_RING256, true>(M, x, ldx, stream, params, eps, y, ldy, st, nullptr, reinterpret_cast<float*>(rowexp))
+                       : run_impl<256, 4, SFX_MLP_RING256>(M, x, ldx, stream, params, eps, y, ldy, st, nullptr, reinterpret_cast<float*>(rowexp));
   }
 }
 

@@ -308,7 +308,7 @@ __global__ void __launch_bounds__(256) render_prep_project_kernel(
     const float* __restrict__ rest, PrepStrides ld, const float* __restrict__ c2ws, float fx, float fy, float cx,
     float cy, int img_h, int img_w, int bw, float* __restrict__ viewmat_out, float* __restrict__ rgbs,
     float* __restrict__ opac, float* __restrict__ xys, float* __restrict__ depths, int* __restrict__ radii,
-    float* __restrict__ conics, int* __restrict__ num_tiles_hit) {
+    float* __restrict__ conics, int* __restrict__ num_tiles_hit, float4* __restrict__ rec) {
   // canonical glue arithmetic (oracle/render_ref.py glue_args(canonical=True)): exp / sigmoid in double rounded
   // once, norms as left-to-right sums with a correctly rounded sqrt, no contraction
 #pragma clang fp contract(off)
@@ -411,6 +411,15 @@ __global__ void __launch_bounds__(256) render_prep_project_kernel(
     }
     project_point(i, px, py, pz, sc0, sc1, sc2, q0, q1, q2, q3, 1.f, vm, fx, fy, cx, cy, img_h, img_w, bw, 0.01f,
                   xys + 2 * o, depths + o, radii + o, conics + 3 * o, nullptr, num_tiles_hit + o, nullptr);
+    if (rec) {  // the rasterizer's packed record (pack_raster_records_kernel's layout), from this thread's own stores
+      const long long r = o + i;
+      const float* xy = xys + 2 * r;
+      const float* cn = conics + 3 * r;
+      const float* cl = rgbs + 3 * r;
+      rec[4 * r + 0] = make_float4(xy[0], xy[1], op, cn[0]);
+      rec[4 * r + 1] = make_float4(cn[1], cn[2], cl[0], cl[1]);
+      rec[4 * r + 2] = make_float4(cl[2], 0.f, 0.f, 0.f);
+    }
   }
 }
 
@@ -419,13 +428,13 @@ int launch_prep(int n, int nviews, int num_bases, const float* means, const floa
                 const float* opac_logit, const float* dc, const float* rest, PrepStrides ld, const float* c2ws,
                 float fx, float fy, float cx, float cy, int img_h, int img_w, int bw, float* viewmat_out, float* rgbs,
                 float* opac, float* xys, float* depths, int* radii, float* conics, int* num_tiles_hit,
-                hipStream_t st) {
+                hipStream_t st, float* rec = nullptr) {
   const unsigned blocks = sfx::ceil_div(n > 0 ? n : 1, 256);
 #define SFX_PREP(DG)                                                                                              \
   render_prep_project_kernel<DG><<<blocks, 256, 0, st>>>(n, nviews, means, log_scales, quats_raw, opac_logit, dc,  \
                                                          rest, ld, c2ws, fx, fy, cx, cy, img_h, img_w, bw,           \
                                                          viewmat_out, rgbs, opac, xys, depths, radii, conics,         \
-                                                         num_tiles_hit)
+                                                         num_tiles_hit, reinterpret_cast<float4*>(rec))
   switch (num_bases) {
     case 1: SFX_PREP(0); break;
     case 4: SFX_PREP(1); break;
@@ -1626,7 +1635,7 @@ int sfx_render_prep_project_views(int n, int views, int num_bases, const float* 
                                   long long ld_rest, const float* camera_to_worlds, float fx, float fy, float cx,
                                   float cy, int img_h, int img_w, int block_width, float* rgbs, float* opacities,
                                   float* xys, float* depths, int* radii, float* conics, int* num_tiles_hit,
-                                  void* stream) {
+                                  float* records, void* stream) {
   SFX_REQUIRE(n >= 0 && views >= 1 && views <= 65535, "sfx_render_prep_project_views: bad sizes");
   SFX_REQUIRE((long long)n * views < (1ll << 31), "sfx_render_prep_project_views: views * n must fit int32");
   SFX_REQUIRE(num_bases == 1 || num_bases == 4 || num_bases == 9 || num_bases == 16 || num_bases == 25,
@@ -1641,7 +1650,7 @@ int sfx_render_prep_project_views(int n, int views, int num_bases, const float* 
   launch_prep(n, views, num_bases, means, log_scales, quats_raw, opac_logit, features_dc, features_rest,
               PrepStrides{ld_means, ld_scales, ld_quats, ld_opac, ld_dc, ld_rest}, camera_to_worlds, fx, fy, cx, cy,
               img_h, img_w, block_width, nullptr, rgbs, opacities, xys, depths, radii, conics, num_tiles_hit,
-              sfx::as_stream(stream));
+              sfx::as_stream(stream), records);
   return sfx::check_launch("sfx_render_prep_project_views");
 }
 

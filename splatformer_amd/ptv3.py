@@ -149,11 +149,14 @@ class Block(nn.Module):
         ln_c = self.cpe[2]
         ln1 = self.norm1[0]
         xc = x if conv_in is None else conv_in
-        if ops.subm_fused_ok(C, x.shape[0]):
-            # conv + LN_cpe + shortcut + norm1 in one launch, pair products summed on chip (csrc/subm_fused.hip)
+        fused = ops.subm_fused_ok(C, x.shape[0])
+        if fused:
+            # conv + LN_cpe + shortcut + norm1 in one launch, pair products summed on chip (csrc/subm_fused.hip);
+            # the conv input's row exponents come from the previous Block's MLP epilogue when it wrote xc
             wpk, winv, bf = self.cpe_packed()
+            re = point.get("feat_rowexp")
             x1, h = ops.subm_cpe_ln(xc, x, point.nbr, wpk, winv, bf, ln_c.weight, ln_c.bias, ln1.weight, ln1.bias,
-                                    ln1.eps)
+                                    ln1.eps, rowexp=re[1] if re is not None and re[0] is xc else None)
         else:
             wf, bf = self.cpe_fused()
             # the conv's pair products go to per-pair rows that the LN kernel sums in a fixed order (no float
@@ -172,14 +175,19 @@ class Block(nn.Module):
             K, win, nw = point_windows(point, self.attn.patch_size_max)
             a = ops.window_attention(qkv, point.order_phys[oi], win, nw, K, self.attn.num_heads, C, qkv_amax=q_amax)
         x2 = ops.linear(a, self.attn.proj.weight, self.attn.proj.bias, residual=x1)
-        return self._mlp_tail(point, x2, out)
+        return self._mlp_tail(point, x2, out, rowexp=fused)
 
-    def _mlp_tail(self, point: Point, x2: Tensor, out: Optional[Tensor]) -> Point:
-        """x += MLP(LN2 x) (calflops.py:72-82)."""
+    def _mlp_tail(self, point: Point, x2: Tensor, out: Optional[Tensor], rowexp: bool = False) -> Point:
+        """x += MLP(LN2 x) (calflops.py:72-82).  rowexp: also emit the output rows' fused-conv exponents (this map
+        runs the fused SubM conv, so the next Block on it reads them instead of re-reading its input)."""
         ln2 = self.norm2[0]
         mlp = self.mlp[0]
+        point.pop("feat_rowexp", None)
         if ops.block_mlp_ok(x2, self.channels):  # norm2 -> fc1 -> GELU -> fc2 -> + shortcut in one launch (mlp.hip)
-            point.feat = ops.block_mlp(x2, ln2, mlp.fc1, mlp.fc2, out=out)
+            e = torch.empty(x2.shape[0], device=x2.device, dtype=torch.int32) if rowexp else None
+            point.feat = ops.block_mlp(x2, ln2, mlp.fc1, mlp.fc2, out=out, rowexp=e)
+            if e is not None:
+                point.feat_rowexp = (point.feat, e)
             return point
         h2 = ops.layernorm(x2, ln2.weight, ln2.bias, ln2.eps)
         m = ops.linear(h2, mlp.fc1.weight, mlp.fc1.bias, act=ops.ACT_GELU)

@@ -62,7 +62,7 @@ _lib.register("sfx_gemm_force_config", [I, I])
 _lib.register("sfx_mlp_stream_floats", [I], Z)
 _lib.register("sfx_mlp_params_floats", [I], Z)
 _lib.register("sfx_mlp_pack", [I, P, P, P, P, P, P, P, P, P, P])
-_lib.register("sfx_block_mlp", [I, I, P, L, P, P, F, P, L, P])
+_lib.register("sfx_block_mlp", [I, I, P, L, P, P, F, P, L, P, P])
 _lib.register("sfx_block_mlp_train", [I, I, P, L, P, P, F, P, P, P, L, P])
 _lib.register("sfx_block_mlp_bwd", [I, I, P, L, P, P, P, P, P, L, P])
 
@@ -325,7 +325,7 @@ def block_mlp_ok(x: Tensor, C: int) -> bool:
         and x.stride(0) % 4 == 0
 
 
-def block_mlp(x2: Tensor, ln2, fc1, fc2, out: Optional[Tensor] = None) -> Tensor:
+def block_mlp(x2: Tensor, ln2, fc1, fc2, out: Optional[Tensor] = None, rowexp: Optional[Tensor] = None) -> Tensor:
     """Y = x2 + fc2(GELU(fc1(LN2(x2)))) in one launch (Block.forward's norm2 / mlp / shortcut, calflops.py:72-82;
     csrc/mlp.hip): the LayerNorm output and the [M, 4C] hidden stay on chip.  C in MLP_CHANNELS."""
     M, C = x2.shape
@@ -334,7 +334,7 @@ def block_mlp(x2: Tensor, ln2, fc1, fc2, out: Optional[Tensor] = None) -> Tensor
         out = torch.empty(M, C, device=x2.device, dtype=torch.float32)
     px, ldx = _rows(x2)
     py, ldy = _rows(out)
-    call("sfx_block_mlp", M, C, px, ldx, ptr(st), ptr(pr), float(ln2.eps), py, ldy, stream())
+    call("sfx_block_mlp", M, C, px, ldx, ptr(st), ptr(pr), float(ln2.eps), py, ldy, ptr(rowexp, torch.int32), stream())
     return out
 
 
@@ -806,14 +806,16 @@ def subm_rowexp(x: Tensor) -> Tensor:
 
 
 def subm_cpe_ln(xc: Tensor, x: Tensor, smap: "SubmMap", wpk: Tensor, winv: Tensor, bias: Tensor, g_cpe: Tensor,
-                b_cpe: Tensor, g1: Tensor, b1: Tensor, eps: float) -> Tuple[Tensor, Tensor]:
+                b_cpe: Tensor, g1: Tensor, b1: Tensor, eps: float,
+                rowexp: Optional[Tensor] = None) -> Tuple[Tensor, Tensor]:
     """x1 = x + LN_cpe(SubMConv'(xc)), h = LN1(x1) in one launch (csrc/subm_fused.hip; C in SUBM_FUSED_KERNELS)."""
     n, C = x.shape
     if xc.shape != x.shape or not (xc.is_contiguous() and x.is_contiguous()):
         raise RuntimeError("subm_cpe_ln: contiguous [n, C] inputs expected")
     x1 = torch.empty_like(x)
     h = torch.empty_like(x)
-    call("sfx_subm_cpe_ln", n, C, ptr(xc), ptr(x), ptr(smap.nbr), ptr(smap.order), ptr(subm_rowexp(xc)), ptr(wpk),
+    call("sfx_subm_cpe_ln", n, C, ptr(xc), ptr(x), ptr(smap.nbr), ptr(smap.order),
+         ptr(subm_rowexp(xc) if rowexp is None else rowexp), ptr(wpk),
          ptr(winv), ptr(bias), ptr(g_cpe), ptr(b_cpe), ptr(g1), ptr(b1), float(eps), ptr(x1), ptr(h), stream())
     return x1, h
 

@@ -109,3 +109,27 @@ def test_block_mlp_launch_variants(device, monkeypatch, C, waves, hs):
     e_row = (bh - br).norm(dim=1) / br.norm(dim=1).clamp_min(1e-30)
     e32 = (b32 - br).norm(dim=1) / br.norm(dim=1).clamp_min(1e-30)
     assert bool((e_row <= 4 * e32 + 1e-6).all()), float((e_row - 4 * e32).max())
+
+
+@pytest.mark.parametrize("C", ops.MLP_CHANNELS)
+def test_block_mlp_rowexp(device, C):
+    """The MLP epilogue's row exponents of its output (for the next fused SubM conv) equal sfx_subm_rowexp of the
+    output, bit for bit, incl. zero rows (127)."""
+    M = 3001
+    ln, fc1, fc2 = _mods(C, 7 * C)
+    g = torch.Generator().manual_seed(C)
+    x = torch.randn(M, C, generator=g) * 2.0
+    x[::7] *= 1e4
+    x[3::11] *= 1e-4
+    mods = [m.to(device) for m in (ln, fc1, fc2)]
+    e = torch.full((M,), -999, device=device, dtype=torch.int32)
+    y = ops.block_mlp(x.to(device), *mods, rowexp=e)
+    assert torch.equal(e.cpu(), ops.subm_rowexp(y).cpu())
+    # zero output rows (x = 0 and a zero fc2): exponent 127
+    with torch.no_grad():
+        mods[2].weight.zero_()
+        mods[2].bias.zero_()
+    xz = torch.zeros(64, C, device=device)
+    ez = torch.empty(64, device=device, dtype=torch.int32)
+    yz = ops.block_mlp(xz, *mods, rowexp=ez)
+    assert float(yz.abs().max()) == 0.0 and bool((ez == 127).all())

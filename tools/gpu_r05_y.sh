@@ -3,7 +3,7 @@
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
-timeout -k 10 1000 python -u -m pytest -x -q --timeout 400 --timeout-method thread tests/test_gpu_render.py tests/test_gpu_full.py tests/test_gpu_downsample.py tests/test_gpu_train.py \
+timeout -k 10 1000 python -u -m pytest -x -q --timeout 400 --timeout-method thread tests/test_gpu_render.py tests/test_gpu_mlp.py tests/test_gpu_ptv3.py tests/test_gpu_full.py \
   > gpurun_out/r05y_tests.log 2>&1 || { echo "tests failed"; tail -30 gpurun_out/r05y_tests.log; exit 1; }
 tail -1 gpurun_out/r05y_tests.log
 timeout -k 10 300 python bench.py --config E --steps 10 --warmup 2 --no-cpu-baseline --no-traffic --no-psnr > gpurun_out/r05y_E.log 2>&1 || { tail -5 gpurun_out/r05y_E.log; exit 1; }
