@@ -81,6 +81,8 @@ def parse(argv=None):
     ap.add_argument("--n", type=int, default=None)
     ap.add_argument("--res", type=str, default=None, help="W or WxH")
     ap.add_argument("--views", type=int, default=None)
+    ap.add_argument("--train-prec", choices=["fp32", "amp"], default="fp32",
+                    help="configs C/D: refiner precision; amp = the reference's enable_amp (train.py:240) class")
     ap.add_argument("--sh", type=int, default=None)
     ap.add_argument("--batch", type=int, default=None, help="scenes per step (C) / micro-steps (D)")
     ap.add_argument("--flash", action="store_true",
@@ -337,7 +339,7 @@ def measure_traffic(args):
     (2*FETCH_SIZE + WRITE_SIZE: gfx950 FETCH_SIZE counts half the bytes of wide reads), or (None, reason)."""
     argv = ["--config", args.config, "--n", str(args.n), "--res", f"{args.width}x{args.height}",
             "--views", str(args.views), "--sh", str(args.sh), "--batch", str(args.batch), "--steps", "2",
-            "--warmup", "1", "--profile-only", "--markers"]
+            "--warmup", "1", "--profile-only", "--markers", "--train-prec", args.train_prec]
     tmp = tempfile.mkdtemp(prefix="sfx_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
     try:
         got = {}
@@ -553,7 +555,7 @@ def main(argv=None):
             gts = [rasterize_gaussians_to_multiimgs(sc, cams)[0] for sc in scenes]
         group = torch.distributed.group.WORLD if multi else None
         tr = Trainer(model, accumulate_step=(n_sc if args.config == "D" else 1), group=group,
-                     generator=torch.Generator(device=dev).manual_seed(rank))
+                     generator=torch.Generator(device=dev).manual_seed(rank), precision=args.train_prec)
 
         if args.config == "C":
             def step():
@@ -642,7 +644,8 @@ def main(argv=None):
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "fp32",
+            "dtype": ("fp16-autocast-class (refiner GEMMs: leading fp16 term product, fp32 accumulation; "
+                      "--train-prec amp)") if train and args.train_prec == "amp" else "fp32",
             "data": f"synthetic (seeded {args.n}-Gaussian scene(s) per rank, random-init ptv3_base weights)",
             "config": {"workload": workload, "scenes_per_step": (args.batch if train else 1) * world,
                        "views_per_scene": args.views, "parallelism": par,

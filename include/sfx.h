@@ -175,6 +175,17 @@ int sfx_ln_amax_bound(int C, const float* gamma, const float* beta, unsigned lon
  * process.  Eight-wave configurations apply only to split (K >= 64) launches. */
 int sfx_gemm_force_config(int cfg, int stream_k);
 
+/* Library operand-precision mode for every later GEMM launch of the process (ABI 14):
+ *   0 (default) fp32-accurate: fp16x2 / bf16x3 split operands, three resp. six term products per block;
+ *   1 reference precision, the class of the reference's fp16 autocast training (train.py:240,
+ *     configs/train/default.gin:11): sfx_linear / sfx_subm_conv / sfx_linear_bwd_data and the SubM conv
+ *     backward form only the leading fp16 product of each block (operands rounded to fp16 after the per-row
+ *     power-of-two scaling, fp32 accumulation, fp32 outputs); sfx_linear_wgrad forms three bf16 products
+ *     (16-bit significands).  The fused MLP, attention and head kernels keep their fp32-accurate forms.
+ * Returns SFX_OK or an error for a mode other than 0 / 1; sfx_get_precision returns the current mode. */
+int sfx_set_precision(int mode);
+int sfx_get_precision(void);
+
 /* ---- training (configs C/D): backward of the nn.Linear layers -------------------------------------
  * dX[M,K] (=|+=) rowscale[m] * (dY[M,N] W[N,K]) * act'(dact_pre[m,k]) for k < dact_ncols (-1 = all);
  * Wt = W^T stored [K, N] (ldwt); dact: 0 none, 1 GELU(erf) on the pre-activation, 2 ReLU, 3 tanh given

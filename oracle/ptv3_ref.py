@@ -15,6 +15,7 @@ fp32 torch ops on the CPU; integer serialization via oracle.serialize_ref.
 """
 from __future__ import annotations
 
+import contextlib
 import math
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence
@@ -50,19 +51,48 @@ class PTv3Config:
         return len(self.enc_depths)
 
 
+# ---- autocast precision (reference train.py:240 `torch.cuda.amp.autocast(enabled=enable_amp)`,
+# configs/train/default.gin:11) ------------------------------------------------------------------------------
+# Under CUDA autocast the matmul-class ops (F.linear, the spconv SubM conv, the attention matmuls) take fp16
+# operands, accumulate in fp32 and return fp16; LayerNorm / softmax run in fp32 on the (fp16) values they get;
+# BatchNorm and GELU keep their fp16 input type.  The restatement stays an fp32 computation and rounds every
+# value autocast would hold in fp16 to fp16 (`_h`); autograd through the roundings gives the fp16 gradients of
+# those ops.  fp64 tensors pass through unchanged (the fp64 oracle is exact by construction).
+AUTOCAST = False
+
+
+def _h(t):
+    return t.half().float() if (AUTOCAST and t is not None and t.dtype == torch.float32) else t
+
+
+@contextlib.contextmanager
+def autocast(enabled: bool = True):
+    """Run the enclosed oracle calls in the reference's autocast precision."""
+    global AUTOCAST
+    prev, AUTOCAST = AUTOCAST, enabled
+    try:
+        yield
+    finally:
+        AUTOCAST = prev
+
+
+def _lin(x, w, b):
+    return _h(F.linear(_h(x), _h(w), _h(b)))
+
+
 # ---- primitives -------------------------------------------------------------
 def linear(x, sd, p):
-    return F.linear(x, sd[p + ".weight"], sd.get(p + ".bias"))
+    return _lin(x, sd[p + ".weight"], sd.get(p + ".bias"))
 
 
 def bn(x, sd, p, eps, train=False):
     """Eval: running statistics.  Train (model.train(), train.py:236): batch statistics; the running
     statistics are updated on the state dict in place (momentum 0.01, pointtransformer_v3.py:252)."""
     if not train:
-        return F.batch_norm(x, sd[p + ".running_mean"], sd[p + ".running_var"], sd[p + ".weight"], sd[p + ".bias"],
-                            False, 0.0, eps)
-    return F.batch_norm(x, sd[p + ".running_mean"], sd[p + ".running_var"], sd[p + ".weight"], sd[p + ".bias"],
-                        True, 0.01, eps)
+        return _h(F.batch_norm(x, sd[p + ".running_mean"], sd[p + ".running_var"], sd[p + ".weight"],
+                               sd[p + ".bias"], False, 0.0, eps))
+    return _h(F.batch_norm(x, sd[p + ".running_mean"], sd[p + ".running_var"], sd[p + ".weight"], sd[p + ".bias"],
+                           True, 0.01, eps))
 
 
 def ln(x, sd, p, eps):
@@ -70,7 +100,7 @@ def ln(x, sd, p, eps):
 
 
 def gelu(x):
-    return F.gelu(x)
+    return _h(F.gelu(x))
 
 
 def subm_neighbors(grid: torch.Tensor, batch: torch.Tensor) -> torch.Tensor:
@@ -97,11 +127,12 @@ def subm_conv(x, nbr, weight, bias):
     cout = weight.shape[0]
     W = weight.reshape(cout, 27, -1)
     out = torch.zeros(x.shape[0], cout, dtype=x.dtype)
-    xz = torch.cat([x, torch.zeros(1, x.shape[1], dtype=x.dtype)], 0)
+    xz = torch.cat([_h(x), torch.zeros(1, x.shape[1], dtype=x.dtype)], 0)
     idx = torch.where(nbr < 0, torch.full_like(nbr, x.shape[0]), nbr)
+    W = _h(W)
     for k in range(27):
         out = out + xz[idx[:, k]] @ W[:, k, :].T
-    return out + bias
+    return _h(out + _h(bias))
 
 
 # ---- Point ------------------------------------------------------------------
@@ -195,9 +226,9 @@ def serialized_attention_heads(sd, p, point: Point, C, H, patch_size_max, order_
     qkv = linear(feat, sd, p + ".qkv")[order]
     q, k, v = qkv.reshape(-1, K, 3, H, C // H).permute(2, 0, 3, 1, 4).unbind(dim=0)
     scale = (C // H) ** -0.5
-    attn = (q * scale) @ k.transpose(-2, -1)
+    attn = _h(_h(q * scale) @ k.transpose(-2, -1))
     attn = torch.softmax(attn, dim=-1)
-    out = (attn @ v).transpose(1, 2).reshape(-1, C)
+    out = _h(_h(attn) @ v).transpose(1, 2).reshape(-1, C)
     return out[inverse]
 
 
@@ -274,7 +305,7 @@ def serialized_unpooling(sd, p, point: Point, cfg: PTv3Config, train=False):
     inverse = point.pooling_inverse
     coarse = gelu(bn(linear(point.feat, sd, p + ".proj.0"), sd, p + ".proj.1", cfg.bn_eps, train))
     skip = gelu(bn(linear(parent.feat, sd, p + ".proj_skip.0"), sd, p + ".proj_skip.1", cfg.bn_eps, train))
-    parent.feat = skip + coarse[inverse]
+    parent.feat = _h(skip + coarse[inverse])  # (two fp16 tensors under autocast)
     parent.stale_conv_feat = skip  # sparse_conv_feat is not refreshed by SerializedUnpooling
     return parent
 
@@ -339,11 +370,11 @@ def heads_forward(sd, y: torch.Tensor, feat: torch.Tensor, in_gs: Dict[str, torc
             continue
         h = h0
         for li in range(nlayer - 1):
-            z = F.linear(h, sd[f"{prefix}{f}.{2 * li}.weight"], sd[f"{prefix}{f}.{2 * li}.bias"])
+            z = _lin(h, sd[f"{prefix}{f}.{2 * li}.weight"], sd[f"{prefix}{f}.{2 * li}.bias"])
             h = torch.relu(z) if relu_masks is None else z * relu_masks[f][li].to(z.dtype)
-        o = F.linear(h, sd[f"{prefix}{f}.{2 * (nlayer - 1)}.weight"], sd[f"{prefix}{f}.{2 * (nlayer - 1)}.bias"])
+        o = _lin(h, sd[f"{prefix}{f}.{2 * (nlayer - 1)}.weight"], sd[f"{prefix}{f}.{2 * (nlayer - 1)}.bias"])
         if f == "means":
-            o = torch.tanh(o)
+            o = _h(torch.tanh(o))
         if f == "features_rest":
             o = o.view(o.shape[0], -1, 3)
         out[f] = in_gs[f] + o

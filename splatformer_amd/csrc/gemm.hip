@@ -65,9 +65,9 @@ using namespace sfxg;
 template <int BM, int BN, int WGM, int NW, bool VEC, int MODE, int SPL>
 __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs p, int tiles_n, int total_tiles) {
   constexpr bool SPLIT = SPL != 0;
-  constexpr bool F16 = SPL == 2;               // fp16x2 terms
-  constexpr int NTERM = F16 ? 2 : 3;          // LDS term images per operand
-  static_assert(SPL == 0 || SPL == 2 || SPL == 3, "operand precision");
+  constexpr bool F16 = SPL == 2 || SPL == 1;   // fp16 terms (SPL 1: the leading term only)
+  constexpr int NTERM = SPL == 1 ? 1 : (F16 ? 2 : 3);  // LDS term images per operand
+  static_assert(SPL == 0 || SPL == 1 || SPL == 2 || SPL == 3, "operand precision");
   constexpr int NT = NW * 64;                  // threads
   constexpr int WGN = NW / WGM;                // waves along N
   constexpr int WM = BM / WGM, WN = BN / WGN;  // wave sub-tile
@@ -112,7 +112,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs
   const int h = lane >> 5, l32 = lane & 31;
   const int K = p.K;
   const int nk = (K + BK - 1) / BK;
-  if constexpr (SPL == 2) {
+  if constexpr (F16) {
     if (tid < NBUF) s_flag[tid] = 0;  // (published by the first barrier)
   }
   // byte offsets fit 31 bits (host checks every operand against the 2 GiB buffer range)
@@ -234,7 +234,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs
   auto store_tiles = [&](int buf, bool first, int par) {
     if constexpr (SPLIT) {
       const int b = NBUF == 2 ? buf : 0;
-      if constexpr (SPL == 2) {
+      if constexpr (F16) {
         ++sq;
         float m[A_ITERS];
         bool over = false;
@@ -288,15 +288,15 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs
           uint2 t[2];
           split2h(ra[i], srow[i], t);
           const int o = swz(lrow + RPP * i, lcol >> 2);
-          *reinterpret_cast<uint2*>(sAs + ((b * 2 + 0) * BM) * 64 + o) = t[0];
-          *reinterpret_cast<uint2*>(sAs + ((b * 2 + 1) * BM) * 64 + o) = t[1];
+          *reinterpret_cast<uint2*>(sAs + ((b * NTERM + 0) * BM) * 64 + o) = t[0];
+          if constexpr (NTERM == 2) *reinterpret_cast<uint2*>(sAs + ((b * NTERM + 1) * BM) * 64 + o) = t[1];
         }
 #pragma unroll
         for (int i = 0; i < W_ITERS; ++i) {  // pre-split: h terms in .x/.y, l terms in .z/.w
           const uint4 w = __builtin_bit_cast(uint4, rw[i]);
           const int o = swz(lrow + RPP * i, lcol >> 2);
-          *reinterpret_cast<uint2*>(sWs + ((b * 2 + 0) * BN) * 64 + o) = make_uint2(w.x, w.y);
-          *reinterpret_cast<uint2*>(sWs + ((b * 2 + 1) * BN) * 64 + o) = make_uint2(w.z, w.w);
+          *reinterpret_cast<uint2*>(sWs + ((b * NTERM + 0) * BN) * 64 + o) = make_uint2(w.x, w.y);
+          if constexpr (NTERM == 2) *reinterpret_cast<uint2*>(sWs + ((b * NTERM + 1) * BN) * 64 + o) = make_uint2(w.z, w.w);
         }
         return;
       } else {
@@ -671,7 +671,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs
       if constexpr (F16) {
         constexpr int QA[3] = {1, 0, 0}, QW[3] = {0, 1, 0};
 #pragma unroll
-        for (int j = 0; j < 3; ++j)
+        for (int j = SPL == 1 ? 2 : 0; j < 3; ++j)  // SPL 1: h*h only
 #pragma unroll
           for (int a = 0; a < MB; ++a)
 #pragma unroll
@@ -690,7 +690,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs
     }
   };
   auto compute = [&](int buf) {
-    if constexpr (SPL == 2) {  // a later slab lowered some rows' scales: rescale their accumulators first
+    if constexpr (F16) {  // a later slab lowered some rows' scales: rescale their accumulators first
       ++cq;
       const int b = NBUF == 2 ? buf : 0;
       if (__builtin_amdgcn_readfirstlane(s_flag[b]) == cq) {
@@ -872,11 +872,15 @@ void launch(GemmArgs a, int groups, bool vec, hipStream_t st) {
   if constexpr (NW == 8) {  // split-only tiles (vec operands)
     if (a.split == 2)
       gemm_kernel<BM, BN, WGM, 8, true, MODE, 2><<<grid, 512, 0, st>>>(a, tiles_n, total);
+    else if (a.split == 1)
+      gemm_kernel<BM, BN, WGM, 8, true, MODE, 1><<<grid, 512, 0, st>>>(a, tiles_n, total);
     else
       gemm_kernel<BM, BN, WGM, 8, true, MODE, 3><<<grid, 512, 0, st>>>(a, tiles_n, total);
   } else {
     if (vec && a.split == 2)
       gemm_kernel<BM, BN, WGM, 4, true, MODE, 2><<<grid, 256, 0, st>>>(a, tiles_n, total);
+    else if (vec && a.split == 1)
+      gemm_kernel<BM, BN, WGM, 4, true, MODE, 1><<<grid, 256, 0, st>>>(a, tiles_n, total);
     else if (vec && split)
       gemm_kernel<BM, BN, WGM, 4, true, MODE, 3><<<grid, 256, 0, st>>>(a, tiles_n, total);
     else if (vec)
@@ -903,6 +907,9 @@ constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
 // Operand precision of a launch (GemmArgs::split): exact fp32 MFMA below K = 64 (SFX_GEMM_SPLIT_MINK) or with
 // SFX_GEMM_PREC=fp32; otherwise split operands, fp16x2 (default) or bf16x3 (SFX_GEMM_PREC=bf16x3).  Both split
 // forms are as accurate as fp32 arithmetic; fp16x2 needs half the MFMAs and LDS images of bf16x3.
+// library precision mode (sfx_set_precision): 0 fp32-accurate (default), 1 reference precision (autocast class)
+int g_prec = 0;
+
 int split_mode(int K) {
   static int min_k = -2, mode = 2;
   if (min_k == -2) {
@@ -1190,6 +1197,7 @@ void dispatch(const GemmArgs& a0, int groups, bool vec, hipStream_t st) {
   // fp16x2 needs the pre-split W (per-row scales of A' are chosen in the kernel); without one the launch runs the
   // range-safe bf16x3 form.
   if (a.split == 2 && !a.Wsp) a.split = 3;
+  if (a.split == 2 && g_prec == 1) a.split = 1;  // reference-precision mode: single fp16 term
   if (a.pair_mode)
     dispatch_mode<MODE_PAIR>(a, groups, vec, st);
   else if (!a.gidx)
@@ -1324,6 +1332,9 @@ __global__ void __launch_bounds__(THREADS) wgrad_kernel(int M, int N, int K, con
 constexpr int WG2_T = 128;  // output tile rows (n) and columns (k)
 constexpr int WG2_PLANE = WG2_T * 64;  // bytes of one term image
 
+// NQ = 2 (reference-precision mode): the two leading terms and three products t0t0, t0t1, t1t0 (16-bit
+// significands, still finer than the reference autocast's fp16 operands).
+template <int NQ>
 __global__ void __launch_bounds__(256, 2) wgrad2_kernel(int M, int N, int K, const float* __restrict__ dY,
                                                         long long ldy, const float* __restrict__ X, long long ldx,
                                                         float* __restrict__ dW, long long ldw, int chunk,
@@ -1377,7 +1388,7 @@ __global__ void __launch_bounds__(256, 2) wgrad2_kernel(int M, int N, int K, con
       sfx::split3(hi, t1);
       const int row = 4 * c4 + j;
 #pragma unroll
-      for (int q = 0; q < 3; ++q)
+      for (int q = 0; q < NQ; ++q)
         *reinterpret_cast<uint4*>(img + (op * 3 + q) * WG2_PLANE + chunk_off(row, mg)) =
             make_uint4(t0[q].x, t0[q].y, t1[q].x, t1[q].y);
     }
@@ -1389,7 +1400,7 @@ __global__ void __launch_bounds__(256, 2) wgrad2_kernel(int M, int N, int K, con
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int q = 0; q < 3; ++q) {
+        for (int q = 0; q < NQ; ++q) {
           af[i][q] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(
                                                     img + q * WG2_PLANE + chunk_off(wn * 64 + i * 32 + l32, 2 * s + h)));
           bf[i][q] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(
@@ -1401,7 +1412,7 @@ __global__ void __launch_bounds__(256, 2) wgrad2_kernel(int M, int N, int K, con
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
-          for (int p = 0; p < 6; ++p)
+          for (int p = NQ == 3 ? 0 : 3; p < 6; ++p)
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][QA[p]], bf[j][QB[p]], acc[i][j], 0, 0, 0);
     }
   }
@@ -1700,6 +1711,14 @@ int sfx_linear_bwd_data(int M, int N, int K, const float* dY, long long ldy, con
   return sfx::check_launch("sfx_linear_bwd_data");
 }
 
+int sfx_set_precision(int mode) {
+  SFX_REQUIRE(mode == 0 || mode == 1, "sfx_set_precision: mode %d (0 fp32-accurate, 1 reference precision)", mode);
+  g_prec = mode;
+  return SFX_OK;
+}
+
+int sfx_get_precision(void) { return g_prec; }
+
 int sfx_linear_wgrad(int M, int N, int K, const float* dY, long long ldy, const float* X, long long ldx, float* dW,
                      long long ldw, float* db, void* stream) {
   SFX_REQUIRE(M >= 0 && N > 0 && K > 0, "sfx_linear_wgrad: bad sizes M=%d N=%d K=%d", M, N, K);
@@ -1718,7 +1737,10 @@ int sfx_linear_wgrad(int M, int N, int K, const float* dY, long long ldy, const 
     if (splits2 < 1) splits2 = 1;
     const int chunk2 = (int)sfx::ceil_div(slabs, splits2) * BK;
     splits2 = (int)sfx::ceil_div(M, chunk2);
-    wgrad2_kernel<<<dim3(tiles2, splits2), 256, 0, st>>>(M, N, K, dY, ldy, X, ldx, dW, ldw, chunk2, db);
+    if (g_prec == 1)
+      wgrad2_kernel<2><<<dim3(tiles2, splits2), 256, 0, st>>>(M, N, K, dY, ldy, X, ldx, dW, ldw, chunk2, db);
+    else
+      wgrad2_kernel<3><<<dim3(tiles2, splits2), 256, 0, st>>>(M, N, K, dY, ldy, X, ldx, dW, ldw, chunk2, db);
     return sfx::check_launch("sfx_linear_wgrad");
   }
   const int tiles = (int)(sfx::ceil_div(N, WG_TILE) * sfx::ceil_div(K, WG_TILE));

@@ -73,7 +73,11 @@ struct GemmArgs {
   // boundary gets partial sums (atomic add into a zero-filled output; the k-slab-0 owner adds the linear
   // epilogue terms).  Only for linear epilogues (no activation, no pre-residual copy, no in-place residual).
   int sk;
-  int split;  // operand precision (see gemm_kernel): 0 exact fp32 MFMA, 2 fp16x2, 3 bf16x3; chosen in pick_cfg
+  // operand precision (see gemm_kernel): 0 exact fp32 MFMA, 2 fp16x2, 3 bf16x3; 1 = the reference-precision mode
+  // (sfx_set_precision(1), the class of the reference's fp16 autocast training, train.py:240): the leading fp16
+  // term only -- operands rounded to fp16 after the per-row power-of-two scaling, one product per block, fp32
+  // accumulation and outputs.  Chosen in dispatch.
+  int split;
   // fp16x2 operand maxima, as "amax slots": 64 sub-slots of (tag << 32 | float bits) written with atomicMax
   // by the producer of the tensor (one sub-slot per producing workgroup); a reader takes the max over the
   // sub-slots carrying the expected tag, so slots are reused without clearing.  Upper bounds are enough

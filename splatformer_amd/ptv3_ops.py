@@ -6,6 +6,7 @@ fallback: a missing library or a CPU tensor raises.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 from typing import List, Optional, Sequence, Tuple
@@ -59,6 +60,8 @@ _lib.register("sfx_heads_params_floats", [I], Z)
 _lib.register("sfx_heads_pack", [I, I, I, P, I, P, P, P, P, P, P, P, P, P])
 _lib.register("sfx_heads", [I, I, I, I, P, L, I, I, P, P, P, P, P])
 _lib.register("sfx_gemm_force_config", [I, I])
+_lib.register("sfx_set_precision", [I])
+_lib.register("sfx_get_precision", [])
 _lib.register("sfx_mlp_stream_floats", [I], Z)
 _lib.register("sfx_mlp_params_floats", [I], Z)
 _lib.register("sfx_mlp_pack", [I, P, P, P, P, P, P, P, P, P, P])
@@ -74,6 +77,30 @@ GEMM_NUM_CONFIGS = 7
 def gemm_force_config(cfg: int = -1, stream_k: int = -1) -> None:
     """Tuning / test hook: force the GEMM tile configuration and Stream-K choice (-1 = cost model)."""
     call("sfx_gemm_force_config", cfg, stream_k)
+
+
+# Library operand-precision modes (include/sfx.h sfx_set_precision): "fp32" = fp32-accurate split operands (the
+# default), "amp" = reference precision, the class of the reference's fp16 autocast training (train.py:240,
+# configs/train/default.gin:11 enable_amp): leading fp16 term product only in the GEMM family.
+PRECISIONS = {"fp32": 0, "amp": 1}
+
+
+def get_precision() -> str:
+    m = _lib.fn("sfx_get_precision")()
+    return {v: k for k, v in PRECISIONS.items()}[m]
+
+
+@contextlib.contextmanager
+def precision(mode: str):
+    """Run the enclosed launches in precision `mode` ("fp32" | "amp"); restores the previous mode."""
+    if mode not in PRECISIONS:
+        raise ValueError(f"precision {mode!r}: expected one of {sorted(PRECISIONS)}")
+    prev = _lib.fn("sfx_get_precision")()
+    call("sfx_set_precision", PRECISIONS[mode])
+    try:
+        yield
+    finally:
+        call("sfx_set_precision", prev)
 ORDER_TYPES = {"z": 0, "z-trans": 1, "hilbert": 2, "hilbert-trans": 3}
 
 

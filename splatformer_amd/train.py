@@ -11,6 +11,7 @@ configs/train/default.gin).
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, List, Optional, Sequence
 
 import torch
@@ -98,8 +99,18 @@ class Trainer:
     all-reduce per optimiser step under DDP), clip_grad_norm_ + Adam on device."""
 
     def __init__(self, model: FeaturePredictor, lr: float = 3e-5, eps: float = 1e-15, betas=(0.9, 0.999),
-                 grad_clip_norm: float = 2.0, accumulate_step: int = 1, group=None, generator=None):
+                 grad_clip_norm: float = 2.0, accumulate_step: int = 1, group=None, generator=None,
+                 precision: Optional[str] = None):
+        """precision: "fp32" (default; fp32-accurate refiner forward + backward) or "amp", the reference's
+        `training.enable_amp` (train.py:214-299, configs/train/default.gin:11): refiner forward and backward in
+        the autocast precision class (ptv3_ops.precision); the renderer, loss and optimiser stay fp32 as in the
+        reference (its rasterisation runs outside the autocast region).  No GradScaler: the GEMMs scale every
+        operand row by its own power of two, so fp16 range limits never flush or overflow a gradient.
+        Default from SFX_TRAIN_PREC."""
         self.model = model
+        self.precision = precision or os.environ.get("SFX_TRAIN_PREC", "fp32")
+        if self.precision not in ops.PRECISIONS:
+            raise ValueError(f"precision {self.precision!r}: expected one of {sorted(ops.PRECISIONS)}")
         for name, p in model.named_parameters():       # utils/optimizers.py:4-16, :48-52
             p.requires_grad_("attn.qkv" in name)
         pt.check_trainable(model.backbone.backbone)
@@ -130,13 +141,15 @@ class Trainer:
         total = 0.0
         num_images = sum(len(im) for im in images)  # counted over the whole batch (train.py:273-281)
         for gs, cams, imgs in zip(scenes, cameras, images):
-            packed, tape = refine_train(self.model, gs, masks, perms=perms, group=self.group)
+            with ops.precision(self.precision):
+                packed, tape = refine_train(self.model, gs, masks, perms=perms, group=self.group)
             leaf, out_gs = unpack_leaf(self.model, packed, gs)
             with torch.enable_grad():
                 preds, _ = rasterize_gaussians_to_multiimgs(out_gs, cams)
                 loss = image_l1(preds, imgs) / num_images / len(scenes) / self.accumulate_step
                 loss.backward()
-            refine_backward(self.model, tape, leaf.grad)
+            with ops.precision(self.precision):
+                refine_backward(self.model, tape, leaf.grad)
             total = total + loss.detach()  # summed on the device: one host read per micro-step, not per scene
             del tape, packed, leaf, out_gs, preds
         self.micro += 1

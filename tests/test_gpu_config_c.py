@@ -16,12 +16,20 @@ parameters (utils/optimizers.py:48-52).  Checked against the oracle:
   magnitude and relative L2 <= 2e-4;
 * refiner backward: the qkv gradients for HIP's d(loss)/d(refined record), as close to the fp64 oracle as the
   fp32 oracle is (2x + 1e-5; the bar of tests/test_gpu_train.py, with the heads' ReLU active sets replayed).
+
+Reference-precision mode (Trainer(precision="amp") = the reference's `training.enable_amp`, train.py:240,
+configs/train/default.gin:11; ops.precision / include/sfx.h sfx_set_precision): the same train-mode refine and
+refiner backward (same weights, order shuffles, DropPath masks and upstream gradient) in that mode, against the
+oracle in its autocast mode (oracle/ptv3_ref.autocast: every value CUDA autocast holds in fp16 rounded to fp16):
+the refined residual's and the qkv gradients' distances to the fp32 resp. fp64 oracle are at most 1.5x the
+autocast oracle's own (and the residual measurably differs from the fp32 mode's, > 1e-5: the mode is on).
 """
 import pytest
 import torch
 
 from oracle import gsplat_ref, ptv3_ref
 from splatformer_amd import gs_render
+from splatformer_amd import ptv3_ops as ops
 from splatformer_amd import train as strain
 from splatformer_amd.scenes import make_cameras, make_scene, to_device
 from test_gpu_ptv3 import rel_l2
@@ -110,23 +118,36 @@ def hip_c(device):
                 grads={k: cpu(mpar[k].grad) for k in names}, names=names, loss=float(loss.detach()))
 
 
-def _oracle(hip, dtype):
-    """Oracle train-mode refine + autograd to the qkv parameters for HIP's upstream gradient, in `dtype`."""
+def _oracle(hip, dtype, autocast=False):
+    """Oracle train-mode refine + autograd to the qkv parameters for HIP's upstream gradient, in `dtype` (in the
+    reference's autocast precision with autocast=True)."""
     sd = {k: (v.to(dtype) if v.is_floating_point() else v).clone() for k, v in hip["sd"].items()}
     for k in hip["names"]:
         sd[k].requires_grad_()
     sc = {k: v.to(dtype) for k, v in hip["scene"].items()}
     mk = {k: m.to(dtype) for k, m in hip["masks"].items()}
-    ref, _ = ptv3_ref.feature_predictor_forward(sd, ptv3_ref.PTv3Config(), sc, hip["perms"], train=True, masks=mk,
-                                                relu_masks=hip["relu"])
-    rp = torch.cat([ref[f].reshape(N, -1) for f in FEATS], 1)
-    (rp * hip["d_packed"].to(dtype)).sum().backward()
+    with ptv3_ref.autocast(autocast):
+        ref, _ = ptv3_ref.feature_predictor_forward(sd, ptv3_ref.PTv3Config(), sc, hip["perms"], train=True,
+                                                    masks=mk, relu_masks=hip["relu"])
+        rp = torch.cat([ref[f].reshape(N, -1) for f in FEATS], 1)
+        (rp * hip["d_packed"].to(dtype)).sum().backward()
     return {k: sd[k].grad.double() for k in hip["names"]}, rp.detach()
 
 
 @pytest.fixture(scope="module")
 def oracle32(hip_c):
     return _oracle(hip_c, torch.float32)
+
+
+@pytest.fixture(scope="module")
+def oracle64(hip_c):
+    prev = torch.get_default_dtype()
+    torch.set_default_dtype(torch.float64)
+    try:
+        g64, _ = _oracle(hip_c, torch.float64)
+    finally:
+        torch.set_default_dtype(prev)
+    return g64
 
 
 def test_config_c_train_forward(hip_c, oracle32):
@@ -169,14 +190,9 @@ def test_config_c_render_backward(hip_c, v):
     print(f"\n[config C view {v}] raster/project backward max-rel errors {['%.1e' % e for e in errs]}")
 
 
-def test_config_c_qkv_grads(hip_c, oracle32):
+def test_config_c_qkv_grads(hip_c, oracle32, oracle64):
     g32, _ = oracle32
-    prev = torch.get_default_dtype()
-    torch.set_default_dtype(torch.float64)
-    try:
-        g64, _ = _oracle(hip_c, torch.float64)
-    finally:
-        torch.set_default_dtype(prev)
+    g64 = oracle64
     names = hip_c["names"]
     hip = torch.cat([hip_c["grads"][k].double().reshape(-1) for k in names])
     r32 = torch.cat([g32[k].reshape(-1) for k in names])
@@ -184,3 +200,55 @@ def test_config_c_qkv_grads(hip_c, oracle32):
     e_hip, e_ref = rel_l2(hip, r64), rel_l2(r32, r64)
     print(f"\n[config C] qkv grads to fp64: HIP {e_hip:.2e}, fp32 oracle {e_ref:.2e}")
     assert e_hip <= 2.0 * e_ref + 1e-5
+
+
+# ---- reference-precision mode ---------------------------------------------------------------------------------
+@pytest.fixture(scope="module")
+def hip_amp(device, hip_c):
+    """The train-mode refine + refiner backward of hip_c in precision "amp", for hip_c's upstream gradient."""
+    from splatformer_amd.feature_predictor import FeaturePredictor
+    torch.manual_seed(0)
+    model = FeaturePredictor(sh_degree=1, zeroinit=False).to(device)
+    for name, p in model.named_parameters():
+        p.requires_grad_("attn.qkv" in name)
+        p.grad = torch.zeros_like(p) if p.requires_grad else None
+    gs = to_device(hip_c["scene"], device)
+    masks = RecordingMasks(77)
+    torch.manual_seed(1)
+    with ops.precision("amp"):
+        packed, tape = strain.refine_train(model, gs, masks)
+        strain.refine_backward(model, tape, hip_c["d_packed"].to(device))
+    torch.cuda.synchronize()
+    # the same order shuffles and DropPath masks as the fp32 run (so the oracle runs of hip_c apply)
+    assert model.backbone.backbone.last_perms == hip_c["perms"]
+    assert all(torch.equal(masks.masks[k], hip_c["masks"][k]) for k in hip_c["masks"])
+    mpar = dict(model.named_parameters())
+    return dict(packed=packed.detach().cpu(), grads={k: mpar[k].grad.detach().cpu() for k in hip_c["names"]})
+
+
+@pytest.fixture(scope="module")
+def oracle_amp(hip_c):
+    return _oracle(hip_c, torch.float32, autocast=True)
+
+
+def test_config_c_amp_train_forward(hip_c, hip_amp, oracle32, oracle_amp):
+    _, ref32 = oracle32
+    _, ref16 = oracle_amp
+    s = hip_c["scene"]
+    inp = torch.cat([s[f].reshape(N, -1) for f in FEATS], 1)
+    e_hip = rel_l2(hip_amp["packed"] - inp, ref32 - inp)
+    e_orc = rel_l2(ref16 - inp, ref32 - inp)
+    print(f"\n[config C amp] train-forward residual rel L2 to the fp32 oracle: HIP amp {e_hip:.2e}, "
+          f"autocast oracle {e_orc:.2e}")
+    assert 1e-5 < e_hip <= 1.5 * e_orc
+
+
+def test_config_c_amp_qkv_grads(hip_c, hip_amp, oracle64, oracle_amp):
+    g16, _ = oracle_amp
+    names = hip_c["names"]
+    hip = torch.cat([hip_amp["grads"][k].double().reshape(-1) for k in names])
+    r16 = torch.cat([g16[k].reshape(-1) for k in names])
+    r64 = torch.cat([oracle64[k].reshape(-1) for k in names])
+    e_hip, e_orc = rel_l2(hip, r64), rel_l2(r16, r64)
+    print(f"\n[config C amp] qkv grads to fp64: HIP amp {e_hip:.2e}, autocast oracle {e_orc:.2e}")
+    assert e_hip <= 1.5 * e_orc

@@ -123,6 +123,29 @@ def test_linear_split_precision_is_fp32(device, scale):
     assert e_hip <= 1.5 * e_f32, (e_hip, e_f32)
 
 
+@pytest.mark.parametrize("M,N,K", [(3000, 384, 128), (2000, 1024, 256), (777, 96, 96)])
+def test_linear_reference_precision_mode(device, M, N, K):
+    """ops.precision("amp") (include/sfx.h sfx_set_precision(1): the class of the reference's fp16 autocast
+    training, train.py:240) forms one fp16 product per block -- operands rounded to fp16 (round-to-nearest; the
+    kernel's power-of-two row scales change no rounding of a normal value), exact products, fp32 accumulation:
+    within 2x (+1e-7) of torch's fp32 error on the fp16-rounded operands, as far from the exact product as fp16
+    operand rounding puts it, and the mode is restored on exit."""
+    g = torch.Generator().manual_seed(M + K)
+    x = torch.randn(M, K, generator=g) * 3
+    w = torch.randn(N, K, generator=g) / K ** 0.5
+    x16, w16 = x.half().float(), w.half().float()
+    ref16 = x16.double() @ w16.double().T
+    with ops.precision("amp"):
+        assert ops.get_precision() == "amp"
+        y = ops.linear(x.to(device), w.to(device), None).cpu()
+    assert ops.get_precision() == "fp32"
+    assert rel_l2(y, ref16) <= 2 * rel_l2(x16 @ w16.T, ref16) + 1e-7
+    e = rel_l2(y, x.double() @ w.double().T)
+    assert 5e-5 < e < 1e-3, e
+    y32 = ops.linear(x.to(device), w.to(device), None).cpu()  # default mode again: fp32-accurate
+    assert rel_l2(y32, x.double() @ w.double().T) <= 1.5 * rel_l2(x @ w.T, x.double() @ w.double().T) + 1e-7
+
+
 @pytest.mark.parametrize("span", [10, 20])
 def test_linear_split_rows_wide_dynamic_range(device, span):
     """Rows whose magnitudes span 2^-span .. 2^span (of each other) keep fp32 accuracy row by row: every row's

@@ -59,6 +59,25 @@ def test_linear_wgrad(device, M, N, K):
     assert rel_l2(db, db0 + dy.double().sum(0)) < 1e-5
 
 
+@pytest.mark.parametrize("M,N,K", [(37759, 768, 256), (5003, 128, 64)])
+def test_linear_wgrad_reference_precision(device, M, N, K):
+    """Weight gradient under ops.precision("amp") (three bf16 term products, 16-bit significands): finer than the
+    reference autocast's fp16-operand product, coarser than the fp32-accurate default."""
+    g = torch.Generator().manual_seed(K)
+    dy = torch.randn(M, N, generator=g)
+    x = torch.randn(M, K, generator=g)
+    exact = dy.double().T @ x.double()
+    e16 = rel_l2(dy.half().double().T @ x.half().double(), exact)
+    dw = torch.zeros(N, K, device=device)
+    with ops.precision("amp"):
+        tops.linear_wgrad(dy.to(device), x.to(device), dw, None)
+    e_amp = rel_l2(dw, exact)
+    dw.zero_()
+    tops.linear_wgrad(dy.to(device), x.to(device), dw, None)
+    e_32 = rel_l2(dw, exact)
+    assert e_32 < e_amp <= e16, (e_32, e_amp, e16)
+
+
 @pytest.mark.parametrize("n,cin,cout,dup", [(3000, 64, 64, False), (2000, 96, 128, True), (500, 256, 256, False)])
 def test_subm_conv_bwd_data(device, n, cin, cout, dup):
     g = torch.Generator().manual_seed(n)
