@@ -180,8 +180,10 @@ int sfx_gemm_force_config(int cfg, int stream_k);
  *   1 reference precision, the class of the reference's fp16 autocast training (train.py:240,
  *     configs/train/default.gin:11): sfx_linear / sfx_subm_conv / sfx_linear_bwd_data and the SubM conv
  *     backward form only the leading fp16 product of each block (operands rounded to fp16 after the per-row
- *     power-of-two scaling, fp32 accumulation, fp32 outputs); sfx_linear_wgrad forms three bf16 products
- *     (16-bit significands).  The fused MLP, attention and head kernels keep their fp32-accurate forms.
+ *     power-of-two scaling, fp32 accumulation, fp32 outputs); so do the training MLP tail
+ *     (sfx_block_mlp_train / sfx_block_mlp_bwd), sfx_window_attention_bwd and sfx_window_attention's fp16x2 form
+ *     (its bf16x3 form, no qkv bound given: three bf16 products); sfx_linear_wgrad forms three bf16 products
+ *     (16-bit significands).  The eval-only fused kernels (sfx_block_mlp, sfx_subm_cpe_ln, sfx_heads) ignore it.
  * Returns SFX_OK or an error for a mode other than 0 / 1; sfx_get_precision returns the current mode. */
 int sfx_set_precision(int mode);
 int sfx_get_precision(void);

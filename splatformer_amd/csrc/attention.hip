@@ -26,6 +26,8 @@
 
 #include "common.h"
 
+extern "C" int sfx_get_precision(void);  // gemm.hip (include/sfx.h)
+
 #ifndef SFX_ATTN_OCC16
 #define SFX_ATTN_OCC16 4  // workgroups per CU the d = 16 split kernel is compiled for
 #endif
@@ -497,7 +499,9 @@ flash_bwd_key_kernel(const float* __restrict__ qkv, const int* __restrict__ orde
 // power of two that puts the bound in [2^14, 2^15), the unnormalised probabilities (0, 1] by 2^14, two fp16
 // terms each (sfx::split2h), three term products per block on v_mfma_f32_32x32x16_f16; S and O are unscaled
 // in registers.  Same fp32-level accuracy, half the MFMAs and two-thirds of the LDS images.
-template <int D, bool F16>
+// ONE (sfx_set_precision(1), the reference's autocast class): F16 the leading product h*h only, bf16x3 the three
+// leading term products (16-bit significands)
+template <int D, bool F16, bool ONE = false>
 __global__ void __launch_bounds__(256, D == 16 ? SFX_ATTN_OCC16 : 3)
 window_attn_split_kernel(const float* __restrict__ qkv, const int* __restrict__ order, const int* __restrict__ win,
                          int Kwin, int C, float scale, float* __restrict__ out,
@@ -620,6 +624,7 @@ window_attn_split_kernel(const float* __restrict__ qkv, const int* __restrict__ 
   // term products, smallest first
   constexpr int NP = F16 ? 3 : 6;
   constexpr int QA[6] = {F16 ? 1 : 2, F16 ? 0 : 1, 0, 1, 0, 0}, QB[6] = {0, 1, F16 ? 0 : 2, 0, 1, 0};
+  constexpr int JS = ONE ? (F16 ? 2 : 3) : 0;  // first term product formed
   auto mfma = [](const bf16x8& a, const bf16x8& b, floatx16 c) -> floatx16 {
     if constexpr (F16) return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
     else return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
@@ -640,7 +645,7 @@ window_attn_split_kernel(const float* __restrict__ qkv, const int* __restrict__ 
         kf[q] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(
                                                Ks + q * KMAX * QROW + qk_off(kb * 32 + l32, 2 * ks + h)));
 #pragma unroll
-      for (int j = 0; j < NP; ++j) s[kb] = mfma(kf[QA[j]], qf[ks][QB[j]], s[kb]);
+      for (int j = JS; j < NP; ++j) s[kb] = mfma(kf[QA[j]], qf[ks][QB[j]], s[kb]);
     }
   }
   if constexpr (F16) {  // S was formed from sq-scaled q and k
@@ -698,7 +703,7 @@ window_attn_split_kernel(const float* __restrict__ qkv, const int* __restrict__ 
         vf[q] = __builtin_bit_cast(bf16x8, vv);
       }
 #pragma unroll
-      for (int j = 0; j < NP; ++j) o = mfma(vf[QA[j]], pf[QB[j]], o);
+      for (int j = JS; j < NP; ++j) o = mfma(vf[QA[j]], pf[QB[j]], o);
     }
 
   const float oscale = F16 ? rinv * iq * (1.f / 16384.f) : rinv;
@@ -1521,7 +1526,10 @@ __device__ __forceinline__ void bwd_frag(float4 a, float4 b, float s, f16x8 (&f)
 #pragma unroll
   for (int t = 0; t < 2; ++t) f[t] = __builtin_bit_cast(f16x8, make_uint4(ta[t].x, ta[t].y, tb[t].x, tb[t].y));
 }
+// ONE (sfx_set_precision(1), the reference's autocast class): the leading product only
+template <bool ONE = false>
 __device__ __forceinline__ floatx16 mfma3(const f16x8 (&a)[2], const f16x8 (&b)[2], floatx16 c) {
+  if constexpr (ONE) return __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], b[0], c, 0, 0, 0);
   c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[1], b[0], c, 0, 0, 0);  // smallest first
   c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], b[1], c, 0, 0, 0);
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], b[0], c, 0, 0, 0);
@@ -1587,7 +1595,7 @@ __device__ __forceinline__ void bwd_tr_frag(const unsigned short* timg, int l32,
   }
 }
 
-template <int D>
+template <int D, bool ONE = false>
 __global__ void __launch_bounds__(256, 3)
 window_attn_bwd_q_kernel(const float* __restrict__ qkv, const int* __restrict__ order, const int* __restrict__ win,
                          int Kwin, int C, float scale, const float* __restrict__ attn_out,
@@ -1700,7 +1708,7 @@ window_attn_bwd_q_kernel(const float* __restrict__ qkv, const int* __restrict__ 
     for (int ks = 0; ks < NKS; ++ks) {
       f16x8 kf[2];
       bwd_row_frag<KD>(Kr, kb * 32 + l32, 2 * ks + h, kf);
-      s[kb] = mfma3(kf, qf[ks], s[kb]);
+      s[kb] = mfma3<ONE>(kf, qf[ks], s[kb]);
     }
   }
   const float cS = scale * 1.4426950408889634f * iQ * iK;
@@ -1741,7 +1749,7 @@ window_attn_bwd_q_kernel(const float* __restrict__ qkv, const int* __restrict__ 
     for (int ks = 0; ks < NKS; ++ks) {
       f16x8 vf[2];
       bwd_row_frag<KD>(Vr, kb * 32 + l32, 2 * ks + h, vf);
-      dp = mfma3(vf, gf[ks], dp);
+      dp = mfma3<ONE>(vf, gf[ks], dp);
     }
     float m = 0.f;
 #pragma unroll
@@ -1761,7 +1769,7 @@ window_attn_bwd_q_kernel(const float* __restrict__ qkv, const int* __restrict__ 
       bwd_frag(make_float4(dp[8 * st + 0], dp[8 * st + 1], dp[8 * st + 2], dp[8 * st + 3]),
                make_float4(dp[8 * st + 4], dp[8 * st + 5], dp[8 * st + 6], dp[8 * st + 7]), sd, bf);
       bwd_tr_frag<D>(Kt, l32, 2 * kb + st, h, kt);
-      t = mfma3(kt, bf, t);
+      t = mfma3<ONE>(kt, bf, t);
     }
 #pragma unroll
     for (int r = 0; r < 16; ++r) dq[r] += t[r] * isd;
@@ -1779,7 +1787,7 @@ window_attn_bwd_q_kernel(const float* __restrict__ qkv, const int* __restrict__ 
   }
 }
 
-template <int D>
+template <int D, bool ONE = false>
 __global__ void __launch_bounds__(256, 3)
 window_attn_bwd_kv_kernel(const float* __restrict__ qkv, const int* __restrict__ order, const int* __restrict__ win,
                           int Kwin, int C, float scale, const float* __restrict__ dout, float* __restrict__ dqkv,
@@ -1891,9 +1899,9 @@ window_attn_bwd_kv_kernel(const float* __restrict__ qkv, const int* __restrict__
     for (int ks = 0; ks < NKS; ++ks) {
       f16x8 a[2];
       bwd_row_frag<KD>(Qr, qb * 32 + l32, 2 * ks + h, a);
-      sb = mfma3(a, kf[ks], sb);
+      sb = mfma3<ONE>(a, kf[ks], sb);
       bwd_row_frag<KD>(Gr, qb * 32 + l32, 2 * ks + h, a);
-      pb = mfma3(a, vf[ks], pb);
+      pb = mfma3<ONE>(a, vf[ks], pb);
     }
     // rows r: query qb*32 + (r&3) + 8(r>>2) + 4h ; P (<= 1) into sb, dS into pb
     float m = 0.f;
@@ -1917,11 +1925,11 @@ window_attn_bwd_kv_kernel(const float* __restrict__ qkv, const int* __restrict__
       bwd_frag(make_float4(sb[8 * st + 0], sb[8 * st + 1], sb[8 * st + 2], sb[8 * st + 3]),
                make_float4(sb[8 * st + 4], sb[8 * st + 5], sb[8 * st + 6], sb[8 * st + 7]), 16384.f, bp);
       bwd_tr_frag<D>(Gt, l32, 2 * qb + st, h, at);
-      dv = mfma3(at, bp, dv);
+      dv = mfma3<ONE>(at, bp, dv);
       bwd_frag(make_float4(pb[8 * st + 0], pb[8 * st + 1], pb[8 * st + 2], pb[8 * st + 3]),
                make_float4(pb[8 * st + 4], pb[8 * st + 5], pb[8 * st + 6], pb[8 * st + 7]), sd, bd);
       bwd_tr_frag<D>(Qt, l32, 2 * qb + st, h, at);
-      t = mfma3(at, bd, t);
+      t = mfma3<ONE>(at, bd, t);
     }
 #pragma unroll
     for (int r = 0; r < 16; ++r) dk[r] += t[r] * isd;
@@ -2013,16 +2021,24 @@ int sfx_window_attention(int num_windows, int window, int heads, int head_dim, i
     else SFX_ATTN_SEQ(32);
 #undef SFX_ATTN_SEQ
   } else if (qkv_amax) {  // fp16x2 terms (the caller bounds |qkv|)
-#define SFX_ATTN(DD, F)                                                                                  \
-  window_attn_split_kernel<DD, F><<<dim3((unsigned)nblk), 256, 0, st>>>(qkv, order, win, window, channels, scale, \
-                                                                        out, qkv_amax, qkv_tag, num_windows)
-    if (head_dim == 16) SFX_ATTN(16, true);
-    else if (head_dim == 24) SFX_ATTN(24, true);
-    else SFX_ATTN(32, true);
+#define SFX_ATTN(DD, F, O)                                                                                  \
+  window_attn_split_kernel<DD, F, O><<<dim3((unsigned)nblk), 256, 0, st>>>(qkv, order, win, window, channels, scale, \
+                                                                           out, qkv_amax, qkv_tag, num_windows)
+    if (sfx_get_precision() == 1) {  // reference-precision mode: single fp16 products
+      if (head_dim == 16) SFX_ATTN(16, true, true);
+      else if (head_dim == 24) SFX_ATTN(24, true, true);
+      else SFX_ATTN(32, true, true);
+    } else if (head_dim == 16) SFX_ATTN(16, true, false);
+    else if (head_dim == 24) SFX_ATTN(24, true, false);
+    else SFX_ATTN(32, true, false);
   } else {
-    if (head_dim == 16) SFX_ATTN(16, false);
-    else if (head_dim == 24) SFX_ATTN(24, false);
-    else SFX_ATTN(32, false);
+    if (sfx_get_precision() == 1) {
+      if (head_dim == 16) SFX_ATTN(16, false, true);
+      else if (head_dim == 24) SFX_ATTN(24, false, true);
+      else SFX_ATTN(32, false, true);
+    } else if (head_dim == 16) SFX_ATTN(16, false, false);
+    else if (head_dim == 24) SFX_ATTN(24, false, false);
+    else SFX_ATTN(32, false, false);
 #undef SFX_ATTN
   }
   return sfx::check_launch("sfx_window_attention");
@@ -2130,16 +2146,18 @@ int sfx_window_attention_bwd(int num_windows, int window, int heads, int head_di
     const long long nblk = ((long long)num_windows * heads + 7) / 8 * 8;
     SFX_REQUIRE(nblk < (1ll << 31), "sfx_window_attention_bwd: too many windows");
     float4* st4 = reinterpret_cast<float4*>(stats);
-#define SFX_ABWD(DD)                                                                                              \
+#define SFX_ABWD(DD, ONE)                                                                                         \
   do {                                                                                                            \
-    window_attn_bwd_q_kernel<DD><<<dim3((unsigned)nblk), 256, 0, st>>>(qkv, order, win, window, channels, scale,  \
-                                                                       attn_out, dout, dqkv, st4, num_windows);  \
-    window_attn_bwd_kv_kernel<DD><<<dim3((unsigned)nblk), 256, 0, st>>>(qkv, order, win, window, channels, scale, \
-                                                                        dout, dqkv, st4, num_windows);          \
+    window_attn_bwd_q_kernel<DD, ONE><<<dim3((unsigned)nblk), 256, 0, st>>>(qkv, order, win, window, channels,    \
+                                                                            scale, attn_out, dout, dqkv, st4,    \
+                                                                            num_windows);                         \
+    window_attn_bwd_kv_kernel<DD, ONE><<<dim3((unsigned)nblk), 256, 0, st>>>(qkv, order, win, window, channels,   \
+                                                                             scale, dout, dqkv, st4, num_windows); \
   } while (0)
-    if (head_dim == 16) SFX_ABWD(16);
-    else if (head_dim == 24) SFX_ABWD(24);
-    else SFX_ABWD(32);
+    const bool one = sfx_get_precision() == 1;  // reference-precision mode: single fp16 products
+    if (head_dim == 16) { if (one) SFX_ABWD(16, true); else SFX_ABWD(16, false); }
+    else if (head_dim == 24) { if (one) SFX_ABWD(24, true); else SFX_ABWD(24, false); }
+    else { if (one) SFX_ABWD(32, true); else SFX_ABWD(32, false); }
 #undef SFX_ABWD
     return sfx::check_launch("sfx_window_attention_bwd");
   }

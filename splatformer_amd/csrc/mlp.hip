@@ -35,6 +35,8 @@
 
 #include "gemm_common.h"
 
+extern "C" int sfx_get_precision(void);  // gemm.hip (include/sfx.h)
+
 #ifndef SFX_MLP_RING256
 #define SFX_MLP_RING256 8  // LDS ring phases of the C = 256 kernel
 #endif
@@ -117,7 +119,9 @@ __device__ __forceinline__ float gelu_grad_fit(float x) {
   return phi_cdf + x * (0.39894228040143268f * __builtin_amdgcn_exp2f(-0.72134752044448170f * x * x));
 }
 
-template <int C, int WAVES, int RING, bool HS = false, int KIND = MLP_EVAL>
+// ONE (training kinds under sfx_set_precision(1), the reference's autocast class): the leading product h*h of each
+// block only (the l terms are never read: fp16-rounded operands, fp32 accumulation).
+template <int C, int WAVES, int RING, bool HS = false, int KIND = MLP_EVAL, bool ONE = false>
 __global__ void __launch_bounds__(WAVES * 64, (WAVES == 4 && C > 128) ? 1 : 2)
     mlp_kernel(int M, const float* __restrict__ X, long long ldx, const float* __restrict__ stream,
                const float* __restrict__ par, float eps, float* __restrict__ Y, long long ldy, int rot,
@@ -238,6 +242,7 @@ __global__ void __launch_bounds__(WAVES * 64, (WAVES == 4 && C > 128) ? 1 : 2)
   f16x8 hf[2][2][2];  // hidden fragments: [unit block][k-step][term]
 
   auto mfma3 = [](const f16x8& ah, const f16x8& al, const f16x8& bh, const f16x8& bl, floatx16 c) {
+    if constexpr (ONE) return __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, c, 0, 0, 0);
     c = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, c, 0, 0, 0);  // smallest terms first
     c = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, c, 0, 0, 0);
     return __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, c, 0, 0, 0);
@@ -532,7 +537,7 @@ int pack_impl(const float* w1, const float* b1, const float* w2, const float* b2
   return sfx::check_launch("sfx_mlp_pack");
 }
 
-template <int C, int WAVES, int RING, bool HS = false, int KIND = MLP_EVAL>
+template <int C, int WAVES, int RING, bool HS = false, int KIND = MLP_EVAL, bool ONE = false>
 int run_impl(int M, const float* x, long long ldx, const float* stream, const float* par, float eps, float* y,
              long long ldy, hipStream_t st, const float* rowscale = nullptr, float* z = nullptr) {
   static int rot = -1;
@@ -540,7 +545,7 @@ int run_impl(int M, const float* x, long long ldx, const float* stream, const fl
     const char* e = getenv("SFX_MLP_ROT");
     rot = (e && *e) ? (atoi(e) != 0) : 1;
   }
-  mlp_kernel<C, WAVES, RING, HS, KIND><<<sfx::ceil_div(M, HS ? WAVES * 16 : WAVES * 32), WAVES * 64, 0, st>>>(
+  mlp_kernel<C, WAVES, RING, HS, KIND, ONE><<<sfx::ceil_div(M, HS ? WAVES * 16 : WAVES * 32), WAVES * 64, 0, st>>>(
       M, x, ldx, stream, par, eps, y, ldy, rot, rowscale, z);
   return sfx::check_launch(KIND == MLP_EVAL ? "sfx_block_mlp" : KIND == MLP_TRAIN ? "sfx_block_mlp_train"
                                                                                   : "sfx_block_mlp_bwd");
@@ -548,15 +553,25 @@ int run_impl(int M, const float* x, long long ldx, const float* stream, const fl
 
 // the training kinds run the default eval geometry of each C (4 waves; hidden split at C = 128, 256, and for the
 // C = 96 backward, whose whole-chunk tile spills)
+template <int KIND, bool ONE>
+int run_train_p(int M, int C, const float* x, long long ldx, const float* stream, const float* par, float eps, float* y,
+                long long ldy, hipStream_t st, const float* rowscale, float* z) {
+  switch (C) {
+    case 64: return run_impl<64, 4, 4, false, KIND, ONE>(M, x, ldx, stream, par, eps, y, ldy, st, rowscale, z);
+    case 96:
+      return run_impl<96, 4, 4, KIND == MLP_BWD, KIND, ONE>(M, x, ldx, stream, par, eps, y, ldy, st, rowscale, z);
+    case 128: return run_impl<128, 4, 4, true, KIND, ONE>(M, x, ldx, stream, par, eps, y, ldy, st, rowscale, z);
+    default:
+      return run_impl<256, 4, SFX_MLP_RING256, true, KIND, ONE>(M, x, ldx, stream, par, eps, y, ldy, st, rowscale, z);
+  }
+}
+
 template <int KIND>
 int run_train(int M, int C, const float* x, long long ldx, const float* stream, const float* par, float eps, float* y,
               long long ldy, hipStream_t st, const float* rowscale, float* z) {
-  switch (C) {
-    case 64: return run_impl<64, 4, 4, false, KIND>(M, x, ldx, stream, par, eps, y, ldy, st, rowscale, z);
-    case 96: return run_impl<96, 4, 4, KIND == MLP_BWD, KIND>(M, x, ldx, stream, par, eps, y, ldy, st, rowscale, z);
-    case 128: return run_impl<128, 4, 4, true, KIND>(M, x, ldx, stream, par, eps, y, ldy, st, rowscale, z);
-    default: return run_impl<256, 4, SFX_MLP_RING256, true, KIND>(M, x, ldx, stream, par, eps, y, ldy, st, rowscale, z);
-  }
+  return sfx_get_precision() == 1
+             ? run_train_p<KIND, true>(M, C, x, ldx, stream, par, eps, y, ldy, st, rowscale, z)
+             : run_train_p<KIND, false>(M, C, x, ldx, stream, par, eps, y, ldy, st, rowscale, z);
 }
 
 inline bool mlp_channels_ok(int C) { return C == 64 || C == 96 || C == 128 || C == 256; }

@@ -20,7 +20,8 @@ parameters (utils/optimizers.py:48-52).  Checked against the oracle:
 Reference-precision mode (Trainer(precision="amp") = the reference's `training.enable_amp`, train.py:240,
 configs/train/default.gin:11; ops.precision / include/sfx.h sfx_set_precision): the same train-mode refine and
 refiner backward (same weights, order shuffles, DropPath masks and upstream gradient) in that mode, against the
-oracle in its autocast mode (oracle/ptv3_ref.autocast: every value CUDA autocast holds in fp16 rounded to fp16):
+oracle in its autocast mode (oracle/ptv3_ref.autocast: every value CUDA autocast holds in fp16 rounded to fp16;
+the reference's GradScaler loss scaling emulated):
 the refined residual's and the qkv gradients' distances to the fp32 resp. fp64 oracle are at most 1.5x the
 autocast oracle's own (and the residual measurably differs from the fp32 mode's, > 1e-5: the mode is on).
 """
@@ -119,19 +120,26 @@ def hip_c(device):
 
 
 def _oracle(hip, dtype, autocast=False):
-    """Oracle train-mode refine + autograd to the qkv parameters for HIP's upstream gradient, in `dtype` (in the
-    reference's autocast precision with autocast=True)."""
-    sd = {k: (v.to(dtype) if v.is_floating_point() else v).clone() for k, v in hip["sd"].items()}
-    for k in hip["names"]:
-        sd[k].requires_grad_()
-    sc = {k: v.to(dtype) for k, v in hip["scene"].items()}
-    mk = {k: m.to(dtype) for k, m in hip["masks"].items()}
-    with ptv3_ref.autocast(autocast):
-        ref, _ = ptv3_ref.feature_predictor_forward(sd, ptv3_ref.PTv3Config(), sc, hip["perms"], train=True,
-                                                    masks=mk, relu_masks=hip["relu"])
-        rp = torch.cat([ref[f].reshape(N, -1) for f in FEATS], 1)
-        (rp * hip["d_packed"].to(dtype)).sum().backward()
-    return {k: sd[k].grad.double() for k in hip["names"]}, rp.detach()
+    """Oracle train-mode refine + autograd to the qkv parameters for HIP's upstream gradient, in `dtype`.
+    autocast=True: in the reference's autocast precision with its GradScaler (train.py:215, :289-299: the loss
+    scaled by 2^16, halved after a step whose gradients overflow, gradients unscaled before use) -- without the
+    scaling the fp16 gradients underflow and the oracle's qkv gradients are noise."""
+    scale = 65536.0 if autocast else 1.0
+    while True:
+        sd = {k: (v.to(dtype) if v.is_floating_point() else v).clone() for k, v in hip["sd"].items()}
+        for k in hip["names"]:
+            sd[k].requires_grad_()
+        sc = {k: v.to(dtype) for k, v in hip["scene"].items()}
+        mk = {k: m.to(dtype) for k, m in hip["masks"].items()}
+        with ptv3_ref.autocast(autocast):
+            ref, _ = ptv3_ref.feature_predictor_forward(sd, ptv3_ref.PTv3Config(), sc, hip["perms"], train=True,
+                                                        masks=mk, relu_masks=hip["relu"])
+            rp = torch.cat([ref[f].reshape(N, -1) for f in FEATS], 1)
+            (rp * (hip["d_packed"].to(dtype) * scale)).sum().backward()
+        grads = {k: sd[k].grad.double() / scale for k in hip["names"]}
+        if all(torch.isfinite(g).all() for g in grads.values()) or scale <= 1.0:
+            return grads, rp.detach()
+        scale /= 2.0
 
 
 @pytest.fixture(scope="module")

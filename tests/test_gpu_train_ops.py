@@ -124,6 +124,11 @@ def test_window_attention_bwd(device, n, heads, C, mag, gmag):
     dqkv = tops.window_attention_bwd(qkv.detach().to(device), order.int().to(device), win, len(tab), K, heads, C,
                                      dout.to(device))
     assert rel_l2(dqkv, qkv.grad) < 1e-5
+    if mag == 1.0 and gmag == 1.0:  # reference-precision mode: single fp16 products (fp16-operand error)
+        with ops.precision("amp"):
+            dqa = tops.window_attention_bwd(qkv.detach().to(device), order.int().to(device), win, len(tab), K, heads,
+                                            C, dout.to(device))
+        assert 2e-5 < rel_l2(dqa, qkv.grad) < 5e-3, rel_l2(dqa, qkv.grad)
 
 
 @pytest.mark.parametrize("K", [1024, 256])
@@ -317,3 +322,12 @@ def test_block_mlp_train_fwd_bwd(device, C, M):
     y1 = ops.block_mlp_train(x2.to(device), *dev_mods, z)
     assert rel_l2(y1, y1_ref) < 1e-6
     assert rel_l2((y1 - x2.to(device))[keep.to(device)], (y1_ref - xd)[keep]) < 2e-6
+    # reference-precision mode (ops.precision("amp")): one fp16 product per block -- fp16-operand error (~1e-3
+    # relative), far above the default's and bounded by it
+    with ops.precision("amp"):
+        za = torch.empty(M, 4 * C, device=device)
+        ya = ops.block_mlp_train(x2.to(device), *dev_mods, za, rowscale=rs.to(device))
+        dha = ops.block_mlp_bwd(dy.to(device), *dev_mods, za, rowscale=rs.to(device))
+    e_z, e_y = rel_l2(za, z_ref), rel_l2((ya - x2.to(device))[keep.to(device)], (y_ref - xd)[keep])
+    e_d = rel_l2(dha, h2.grad)
+    assert all(2e-5 < e < 5e-3 for e in (e_z, e_y, e_d)), (e_z, e_y, e_d)
