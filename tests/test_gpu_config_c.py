@@ -22,8 +22,8 @@ configs/train/default.gin:11; ops.precision / include/sfx.h sfx_set_precision): 
 refiner backward (same weights, order shuffles, DropPath masks and upstream gradient) in that mode, against the
 oracle in its autocast mode (oracle/ptv3_ref.autocast: every value CUDA autocast holds in fp16 rounded to fp16;
 the reference's GradScaler loss scaling emulated):
-the refined residual's and the qkv gradients' distances to the fp32 resp. fp64 oracle are at most 1.5x the
-autocast oracle's own (and the residual measurably differs from the fp32 mode's, > 1e-5: the mode is on).
+the refined residual's and the qkv gradients' distances to the fp32 oracle are at most 1.5x the autocast oracle's
+own (head ReLU active sets of the amp run replayed for the gradients) (and the residual measurably differs from the fp32 mode's, > 1e-5: the mode is on).
 """
 import pytest
 import torch
@@ -119,7 +119,7 @@ def hip_c(device):
                 grads={k: cpu(mpar[k].grad) for k in names}, names=names, loss=float(loss.detach()))
 
 
-def _oracle(hip, dtype, autocast=False):
+def _oracle(hip, dtype, autocast=False, relu=None):
     """Oracle train-mode refine + autograd to the qkv parameters for HIP's upstream gradient, in `dtype`.
     autocast=True: in the reference's autocast precision with its GradScaler (train.py:215, :289-299: the loss
     scaled by 2^16, halved after a step whose gradients overflow, gradients unscaled before use) -- without the
@@ -133,7 +133,7 @@ def _oracle(hip, dtype, autocast=False):
         mk = {k: m.to(dtype) for k, m in hip["masks"].items()}
         with ptv3_ref.autocast(autocast):
             ref, _ = ptv3_ref.feature_predictor_forward(sd, ptv3_ref.PTv3Config(), sc, hip["perms"], train=True,
-                                                        masks=mk, relu_masks=hip["relu"])
+                                                        masks=mk, relu_masks=relu or hip["relu"])
             rp = torch.cat([ref[f].reshape(N, -1) for f in FEATS], 1)
             (rp * (hip["d_packed"].to(dtype) * scale)).sum().backward()
         grads = {k: sd[k].grad.double() / scale for k in hip["names"]}
@@ -225,18 +225,29 @@ def hip_amp(device, hip_c):
     torch.manual_seed(1)
     with ops.precision("amp"):
         packed, tape = strain.refine_train(model, gs, masks)
+        W = model.width
+        relu = {f: [(h[:, g * W:(g + 1) * W] > 0).cpu() for h in tape["hs"]]
+                for g, f in enumerate(model.output_features)}
         strain.refine_backward(model, tape, hip_c["d_packed"].to(device))
     torch.cuda.synchronize()
     # the same order shuffles and DropPath masks as the fp32 run (so the oracle runs of hip_c apply)
     assert model.backbone.backbone.last_perms == hip_c["perms"]
     assert all(torch.equal(masks.masks[k], hip_c["masks"][k]) for k in hip_c["masks"])
     mpar = dict(model.named_parameters())
-    return dict(packed=packed.detach().cpu(), grads={k: mpar[k].grad.detach().cpu() for k in hip_c["names"]})
+    return dict(packed=packed.detach().cpu(), grads={k: mpar[k].grad.detach().cpu() for k in hip_c["names"]},
+                relu=relu)
+
+
+# Both amp-side oracle runs replay the HIP amp run's head ReLU active sets: a unit whose pre-activation lies within
+# the amp rounding of 0 flips between the two precisions and would otherwise count as an O(1) gradient error.
+@pytest.fixture(scope="module")
+def oracle_amp(hip_c, hip_amp):
+    return _oracle(hip_c, torch.float32, autocast=True, relu=hip_amp["relu"])
 
 
 @pytest.fixture(scope="module")
-def oracle_amp(hip_c):
-    return _oracle(hip_c, torch.float32, autocast=True)
+def oracle32_amp_relu(hip_c, hip_amp):
+    return _oracle(hip_c, torch.float32, relu=hip_amp["relu"])[0]
 
 
 def test_config_c_amp_train_forward(hip_c, hip_amp, oracle32, oracle_amp):
@@ -251,12 +262,13 @@ def test_config_c_amp_train_forward(hip_c, hip_amp, oracle32, oracle_amp):
     assert 1e-5 < e_hip <= 1.5 * e_orc
 
 
-def test_config_c_amp_qkv_grads(hip_c, hip_amp, oracle64, oracle_amp):
+def test_config_c_amp_qkv_grads(hip_c, hip_amp, oracle32_amp_relu, oracle_amp):
+    """(the fp32 oracle is the reference here: its own error, 4e-5, is far below the amp errors)"""
     g16, _ = oracle_amp
     names = hip_c["names"]
     hip = torch.cat([hip_amp["grads"][k].double().reshape(-1) for k in names])
     r16 = torch.cat([g16[k].reshape(-1) for k in names])
-    r64 = torch.cat([oracle64[k].reshape(-1) for k in names])
-    e_hip, e_orc = rel_l2(hip, r64), rel_l2(r16, r64)
-    print(f"\n[config C amp] qkv grads to fp64: HIP amp {e_hip:.2e}, autocast oracle {e_orc:.2e}")
+    r32 = torch.cat([oracle32_amp_relu[k].reshape(-1) for k in names])
+    e_hip, e_orc = rel_l2(hip, r32), rel_l2(r16, r32)
+    print(f"\n[config C amp] qkv grads to the fp32 oracle: HIP amp {e_hip:.2e}, autocast oracle {e_orc:.2e}")
     assert e_hip <= 1.5 * e_orc
