@@ -121,14 +121,20 @@ __device__ __forceinline__ float gelu_grad_fit(float x) {
 
 // ONE (training kinds under sfx_set_precision(1), the reference's autocast class): the leading product h*h of each
 // block only (the l terms are never read: fp16-rounded operands, fp32 accumulation).
-template <int C, int WAVES, int RING, bool HS = false, int KIND = MLP_EVAL, bool ONE = false>
+// SPLIT > 1 (eval; the last, partial round of a launch -- sfx_block_mlp's tail): workgroup (x, s) computes the
+// hidden chunks [s NCH / SPLIT, (s + 1) NCH / SPLIT) of its points only and stores its fc2 partial sum (+ b2 for
+// s = 0) as row x of P [SPLIT][M][C]; mlp_combine_kernel adds X and the SPLIT partials in a fixed order.  The tail
+// then takes 1 / SPLIT of a round instead of a whole one.
+template <int C, int WAVES, int RING, bool HS = false, int KIND = MLP_EVAL, bool ONE = false, int SPLIT = 1>
 __global__ void __launch_bounds__(WAVES * 64, (WAVES == 4 && C > 128) ? 1 : 2)
     mlp_kernel(int M, const float* __restrict__ X, long long ldx, const float* __restrict__ stream,
                const float* __restrict__ par, float eps, float* __restrict__ Y, long long ldy, int rot,
-               const float* __restrict__ rowscale, float* __restrict__ Z) {
+               const float* __restrict__ rowscale, float* __restrict__ Z, float* __restrict__ P = nullptr) {
   using G = MlpGeom<C>;
   constexpr int PTS = HS ? WAVES * 16 : WAVES * 32;  // points per workgroup
-  constexpr int NB = G::NB, NP = G::NP, PPC = G::PPC, NT = C / 16;  // NT: fc1 k-steps
+  static_assert(SPLIT == 1 || (KIND == MLP_EVAL && G::NCH % SPLIT == 0), "hidden-chunk split: eval, whole chunks");
+  constexpr int NCHS = G::NCH / SPLIT;                // hidden chunks of this workgroup
+  constexpr int NB = G::NB, NP = NCHS * G::PPC, PPC = G::PPC, NT = C / 16;  // NT: fc1 k-steps
   constexpr int NTH = WAVES * 64;
   constexpr int PIECES = 16 / WAVES;  // 1 KB LDS-DMA pieces per wave per phase
   constexpr int PAR_OFF = RING * PHASE_BYTES;
@@ -146,7 +152,7 @@ __global__ void __launch_bounds__(WAVES * 64, (WAVES == 4 && C > 128) ? 1 : 2)
 
   // ---- weight stream: logical phase q -> ring slot q % RING; rot: each workgroup starts at its own hidden
   // chunk j0 and wraps, so the workgroups of an XCD read different parts of the stream at any moment
-  const int j0 = rot ? (int)(blockIdx.x % G::NCH) : 0;
+  const int j0 = SPLIT > 1 ? (int)blockIdx.y * NCHS : (rot ? (int)(blockIdx.x % G::NCH) : 0);
   const char* gstream = reinterpret_cast<const char*>(stream);
   auto issue = [&](int q) {
     int jq = q / PPC + j0;
@@ -335,7 +341,7 @@ __global__ void __launch_bounds__(WAVES * 64, (WAVES == 4 && C > 128) ? 1 : 2)
   };
 
   int p = 0;
-  for (int jl = 0; jl < G::NCH; ++jl) {
+  for (int jl = 0; jl < NCHS; ++jl) {
     const int j = jl + j0 - (jl + j0 >= G::NCH ? G::NCH : 0);  // the hidden chunk of this logical chunk
 #pragma unroll
     for (int cb = 0; cb < (HS ? 1 : 2); ++cb)
@@ -395,7 +401,16 @@ __global__ void __launch_bounds__(WAVES * 64, (WAVES == 4 && C > 128) ? 1 : 2)
       const float4 w01 = pp[2 * g4], w23 = pp[2 * g4 + 1];  // (1/s_c, b2_c) of registers 4 g4 .. 4 g4 + 3
       const unsigned c0 = (unsigned)(32 * b + 8 * g4 + 4 * h);
       float4 y;
-      if constexpr (KIND == MLP_BWD) {  // the branch's input gradient: no bias, no residual
+      if constexpr (SPLIT > 1) {  // this split's fc2 partial (b2 carried by split 0) -> P[s][prow]
+        const float bb = blockIdx.y == 0 ? 1.f : 0.f;
+        y.x = acc2[b][4 * g4 + 0] * (tinv * w01.x) + bb * w01.y;
+        y.y = acc2[b][4 * g4 + 1] * (tinv * w01.z) + bb * w01.w;
+        y.z = acc2[b][4 * g4 + 2] * (tinv * w23.x) + bb * w23.y;
+        y.w = acc2[b][4 * g4 + 3] * (tinv * w23.z) + bb * w23.w;
+        if (pok)
+          *reinterpret_cast<float4*>(P + ((size_t)blockIdx.y * M + prow) * C + c0) = y;
+        continue;
+      } else if constexpr (KIND == MLP_BWD) {  // the branch's input gradient: no bias, no residual
         y.x = acc2[b][4 * g4 + 0] * (tinv * w01.x);
         y.y = acc2[b][4 * g4 + 1] * (tinv * w01.z);
         y.z = acc2[b][4 * g4 + 2] * (tinv * w23.x);
@@ -411,7 +426,7 @@ __global__ void __launch_bounds__(WAVES * 64, (WAVES == 4 && C > 128) ? 1 : 2)
       if constexpr (KIND == MLP_EVAL) ymax = fmaxf(ymax, fmaxf(fmaxf(fabsf(y.x), fabsf(y.y)), fmaxf(fabsf(y.z), fabsf(y.w))));
     }
   }
-  if constexpr (KIND == MLP_EVAL) {
+  if constexpr (KIND == MLP_EVAL && SPLIT == 1) {
     // sfx_subm_rowexp of the output row (csrc/subm_fused.hip, same rule): max in [2^14, 2^15), 127 for a zero row,
     // 0 for inf / nan -- the next Block's fused conv reads it instead of re-reading the row
     if (Z) {
@@ -428,6 +443,25 @@ __global__ void __launch_bounds__(WAVES * 64, (WAVES == 4 && C > 128) ? 1 : 2)
       }
     }
   }
+}
+
+// Y = X + (P[0] + P[1] + ... + P[S-1]) (rows of the split tail; fixed order: bitwise reproducible)
+template <int S>
+__global__ void __launch_bounds__(256) mlp_combine_kernel(int M, int C, const float* __restrict__ X, long long ldx,
+                                                          const float* __restrict__ P, float* __restrict__ Y,
+                                                          long long ldy) {
+  const int c4 = C / 4;
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long long)M * c4) return;
+  const int r = (int)(i / c4), c = 4 * (int)(i - (long long)r * c4);
+  float4 a = *reinterpret_cast<const float4*>(P + (size_t)r * C + c);
+#pragma unroll
+  for (int s = 1; s < S; ++s) {
+    const float4 b = *reinterpret_cast<const float4*>(P + ((size_t)s * M + r) * C + c);
+    a = make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+  }
+  const float4 x = *reinterpret_cast<const float4*>(X + (size_t)r * ldx + c);
+  *reinterpret_cast<float4*>(Y + (size_t)r * ldy + c) = make_float4(x.x + a.x, x.y + a.y, x.z + a.z, x.w + a.w);
 }
 
 // ---- weight packing (once per weight version) ----------------------------------------------------------------
@@ -551,6 +585,76 @@ int run_impl(int M, const float* x, long long ldx, const float* stream, const fl
                                                                                   : "sfx_block_mlp_bwd");
 }
 
+// The C = 256 eval tail split: one 4-wave workgroup per CU (512-register waves), so a launch of W workgroups runs
+// ceil(W / CUs) rounds; when the last round is at most half full its workgroups run as SPLIT = 2 or 4 hidden-chunk
+// splits (one round of 1/SPLIT the work) + mlp_combine_kernel.  Scratch: a per-device buffer grown on demand
+// (stream-ordered reuse: the library's launches of one device run on one stream at a time).
+float* mlp_split_scratch(size_t floats) {
+  static float* bufs[64] = {};
+  static size_t caps[64] = {};
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (caps[dev] < floats) {
+    if (bufs[dev]) (void)hipFree(bufs[dev]);
+    bufs[dev] = nullptr;
+    caps[dev] = 0;
+    if (hipMalloc(&bufs[dev], floats * sizeof(float)) != hipSuccess) return nullptr;
+    caps[dev] = floats;
+  }
+  return bufs[dev];
+}
+
+int cu_count() {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+  }
+  return cus;
+}
+
+int run_eval256_split(int M, const float* x, long long ldx, const float* stream, const float* par, float eps, float* y,
+                      long long ldy, hipStream_t st, float* rowexp) {
+  constexpr int PTS = 64;  // 4 waves as 2 hidden-split pairs
+  const int wgs = (M + PTS - 1) / PTS, cus = cu_count();
+  const int full = wgs / cus * cus, r = wgs - full;
+  static int mode = -1;
+  if (mode < 0) {
+    const char* e = getenv("SFX_MLP_SPLIT");
+    mode = (e && *e) ? atoi(e) : 1;
+  }
+  const int S = (mode && full > 0 && r > 0) ? (4 * r <= cus ? 4 : (2 * r <= cus ? 2 : 1)) : 1;
+  if (S == 1 || rowexp)
+    return run_impl<256, 4, SFX_MLP_RING256, true>(M, x, ldx, stream, par, eps, y, ldy, st, nullptr,
+                                                   reinterpret_cast<float*>(rowexp));
+  const int M1 = full * PTS, Mt = M - M1;
+  float* P = mlp_split_scratch((size_t)S * Mt * 256);
+  SFX_REQUIRE(P, "sfx_block_mlp: tail scratch allocation failed");
+  int rc = run_impl<256, 4, SFX_MLP_RING256, true>(M1, x, ldx, stream, par, eps, y, ldy, st, nullptr, nullptr);
+  if (rc) return rc;
+  const float* xt = x + (size_t)M1 * ldx;
+  float* yt = y + (size_t)M1 * ldy;
+  static int rot = -1;
+  if (rot < 0) {
+    const char* e = getenv("SFX_MLP_ROT");
+    rot = (e && *e) ? (atoi(e) != 0) : 1;
+  }
+  const dim3 grid((unsigned)r, (unsigned)S);
+  if (S == 4)
+    mlp_kernel<256, 4, SFX_MLP_RING256, true, MLP_EVAL, false, 4><<<grid, 256, 0, st>>>(
+        Mt, xt, ldx, stream, par, eps, yt, ldy, rot, nullptr, nullptr, P);
+  else
+    mlp_kernel<256, 4, SFX_MLP_RING256, true, MLP_EVAL, false, 2><<<grid, 256, 0, st>>>(
+        Mt, xt, ldx, stream, par, eps, yt, ldy, rot, nullptr, nullptr, P);
+  const long long n4 = (long long)Mt * 64;
+  if (S == 4)
+    mlp_combine_kernel<4><<<(unsigned)((n4 + 255) / 256), 256, 0, st>>>(Mt, 256, xt, ldx, P, yt, ldy);
+  else
+    mlp_combine_kernel<2><<<(unsigned)((n4 + 255) / 256), 256, 0, st>>>(Mt, 256, xt, ldx, P, yt, ldy);
+  return sfx::check_launch("sfx_block_mlp (split tail)");
+}
+
 // the training kinds run the default eval geometry of each C (4 waves; hidden split at C = 128, 256, and for the
 // C = 96 backward, whose whole-chunk tile spills)
 template <int KIND, bool ONE>
@@ -645,7 +749,7 @@ int sfx_block_mlp(int M, int C, const float* x, long long ldx, const float* stre
     case 128: return waves == 4 ? (hs >= 1 ? run_impl<128, 4, 4, true>(M, x, ldx, stream, params, eps, y, ldy, st, nullptr, reinterpret_cast<float*>(rowexp))
                                           : run_impl<128, 4, 4>(M, x, ldx, stream, params, eps, y, ldy, st, nullptr, reinterpret_cast<float*>(rowexp)))
                                 : run_impl<128, 8, 4>(M, x, ldx, stream, params, eps, y, ldy, st, nullptr, reinterpret_cast<float*>(rowexp));
-    default: return hs ? run_impl<256, 4, SFX_MLP_RING256, true>(M, x, ldx, stream, params, eps, y, ldy, st, nullptr, reinterpret_cast<float*>(rowexp))
+    default: return hs ? run_eval256_split(M, x, ldx, stream, params, eps, y, ldy, st, reinterpret_cast<float*>(rowexp))
                        : run_impl<256, 4, SFX_MLP_RING256>(M, x, ldx, stream, params, eps, y, ldy, st, nullptr, reinterpret_cast<float*>(rowexp));
   }
 }

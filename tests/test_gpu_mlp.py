@@ -38,6 +38,17 @@ def _ref(x, ln, fc1, fc2, dtype):
 @pytest.mark.parametrize("C", ops.MLP_CHANNELS)
 @pytest.mark.parametrize("M", [1, 63, 4097])
 def test_block_mlp_matches_fp64(device, C, M):
+    _check_fp64(device, C, M)
+
+
+@pytest.mark.parametrize("M", [256 * 64 + 1000, 256 * 64 + 5000, 2 * 256 * 64 + 777])
+def test_block_mlp_split_tail(device, M):
+    """C = 256 launches whose last round is at most half full (256 CUs, 64 points per workgroup): the tail runs as
+    4- / 2-way hidden-chunk splits + the fixed-order combine (csrc/mlp.hip run_eval256_split) -- same bar."""
+    _check_fp64(device, 256, M)
+
+
+def _check_fp64(device, C, M):
     ln, fc1, fc2 = _mods(C, C + M)
     g = torch.Generator().manual_seed(M)
     x = torch.randn(M, C, generator=g) * 2.0
