@@ -445,23 +445,41 @@ __global__ void __launch_bounds__(WAVES * 64, (WAVES == 4 && C > 128) ? 1 : 2)
   }
 }
 
-// Y = X + (P[0] + P[1] + ... + P[S-1]) (rows of the split tail; fixed order: bitwise reproducible)
+// Y = X + (P[0] + P[1] + ... + P[S-1]) for the rows of a split tail (fixed order: bitwise reproducible); one wave
+// per row, lane i < C / 4 owns channels 4i .. 4i + 3; rowexp (optional): the MLP_EVAL epilogue's row-exponent rule
 template <int S>
 __global__ void __launch_bounds__(256) mlp_combine_kernel(int M, int C, const float* __restrict__ X, long long ldx,
                                                           const float* __restrict__ P, float* __restrict__ Y,
-                                                          long long ldy) {
-  const int c4 = C / 4;
-  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= (long long)M * c4) return;
-  const int r = (int)(i / c4), c = 4 * (int)(i - (long long)r * c4);
-  float4 a = *reinterpret_cast<const float4*>(P + (size_t)r * C + c);
+                                                          long long ldy, int* __restrict__ rowexp) {
+  const int r = (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (r >= M) return;
+  float m = 0.f;
+  if (lane < C / 4) {
+    const int c = 4 * lane;
+    float4 a = *reinterpret_cast<const float4*>(P + (size_t)r * C + c);
 #pragma unroll
-  for (int s = 1; s < S; ++s) {
-    const float4 b = *reinterpret_cast<const float4*>(P + ((size_t)s * M + r) * C + c);
-    a = make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+    for (int q = 1; q < S; ++q) {
+      const float4 b = *reinterpret_cast<const float4*>(P + ((size_t)q * M + r) * C + c);
+      a = make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+    }
+    const float4 x = *reinterpret_cast<const float4*>(X + (size_t)r * ldx + c);
+    const float4 y = make_float4(x.x + a.x, x.y + a.y, x.z + a.z, x.w + a.w);
+    *reinterpret_cast<float4*>(Y + (size_t)r * ldy + c) = y;
+    m = fmaxf(fmaxf(fabsf(y.x), fabsf(y.y)), fmaxf(fabsf(y.z), fabsf(y.w)));
   }
-  const float4 x = *reinterpret_cast<const float4*>(X + (size_t)r * ldx + c);
-  *reinterpret_cast<float4*>(Y + (size_t)r * ldy + c) = make_float4(x.x + a.x, x.y + a.y, x.z + a.z, x.w + a.w);
+  if (rowexp) {
+    m = sfx::wave_max(m);
+    if (lane == 0) {
+      int e = 127;
+      if (m > 0.f && m <= 3.4028235e38f) {
+        e = 15 - __builtin_amdgcn_frexp_expf(m);
+        e = e > 126 ? 126 : (e < -126 ? -126 : e);
+      } else if (!(m <= 3.4028235e38f)) {
+        e = 0;
+      }
+      rowexp[r] = e;
+    }
+  }
 }
 
 // ---- weight packing (once per weight version) ----------------------------------------------------------------
@@ -614,44 +632,47 @@ int cu_count() {
   return cus;
 }
 
-int run_eval256_split(int M, const float* x, long long ldx, const float* stream, const float* par, float eps, float* y,
-                      long long ldy, hipStream_t st, float* rowexp) {
-  constexpr int PTS = 64;  // 4 waves as 2 hidden-split pairs
-  const int wgs = (M + PTS - 1) / PTS, cus = cu_count();
-  const int full = wgs / cus * cus, r = wgs - full;
+template <int C, int WAVES, int RING, bool HS>
+int run_eval_split(int M, const float* x, long long ldx, const float* stream, const float* par, float eps, float* y,
+                   long long ldy, hipStream_t st, int* rowexp) {
+  constexpr int PTS = HS ? WAVES * 16 : WAVES * 32;  // points per workgroup
+  constexpr int NCH = C / 16;                       // hidden chunks
+  const int wgs = (M + PTS - 1) / PTS, slots = ((WAVES == 4 && C > 128) ? 1 : 2) * cu_count();
+  const int full = wgs / slots * slots, r = wgs - full;
   static int mode = -1;
   if (mode < 0) {
     const char* e = getenv("SFX_MLP_SPLIT");
     mode = (e && *e) ? atoi(e) : 1;
   }
-  const int S = (mode && full > 0 && r > 0) ? (4 * r <= cus ? 4 : (2 * r <= cus ? 2 : 1)) : 1;
-  if (S == 1 || rowexp)
-    return run_impl<256, 4, SFX_MLP_RING256, true>(M, x, ldx, stream, par, eps, y, ldy, st, nullptr,
-                                                   reinterpret_cast<float*>(rowexp));
+  int S = 1;
+  // (the 128-point non-HS launches of C <= 96 measured no gain: their rounds are short and the combine is not free)
+  if (HS && mode && full > 0 && r > 0) {
+    for (int cand : {4, 3, 2})
+      if (NCH % cand == 0 && cand * r <= slots) { S = cand; break; }
+  }
+  if (S == 1)
+    return run_impl<C, WAVES, RING, HS>(M, x, ldx, stream, par, eps, y, ldy, st, nullptr,
+                                        reinterpret_cast<float*>(rowexp));
   const int M1 = full * PTS, Mt = M - M1;
-  float* P = mlp_split_scratch((size_t)S * Mt * 256);
+  float* P = mlp_split_scratch((size_t)S * Mt * C);
   SFX_REQUIRE(P, "sfx_block_mlp: tail scratch allocation failed");
-  int rc = run_impl<256, 4, SFX_MLP_RING256, true>(M1, x, ldx, stream, par, eps, y, ldy, st, nullptr, nullptr);
+  int rc = run_impl<C, WAVES, RING, HS>(M1, x, ldx, stream, par, eps, y, ldy, st, nullptr,
+                                        reinterpret_cast<float*>(rowexp));
   if (rc) return rc;
   const float* xt = x + (size_t)M1 * ldx;
   float* yt = y + (size_t)M1 * ldy;
-  static int rot = -1;
-  if (rot < 0) {
-    const char* e = getenv("SFX_MLP_ROT");
-    rot = (e && *e) ? (atoi(e) != 0) : 1;
-  }
+  int* et = rowexp ? rowexp + M1 : nullptr;
   const dim3 grid((unsigned)r, (unsigned)S);
-  if (S == 4)
-    mlp_kernel<256, 4, SFX_MLP_RING256, true, MLP_EVAL, false, 4><<<grid, 256, 0, st>>>(
-        Mt, xt, ldx, stream, par, eps, yt, ldy, rot, nullptr, nullptr, P);
-  else
-    mlp_kernel<256, 4, SFX_MLP_RING256, true, MLP_EVAL, false, 2><<<grid, 256, 0, st>>>(
-        Mt, xt, ldx, stream, par, eps, yt, ldy, rot, nullptr, nullptr, P);
-  const long long n4 = (long long)Mt * 64;
-  if (S == 4)
-    mlp_combine_kernel<4><<<(unsigned)((n4 + 255) / 256), 256, 0, st>>>(Mt, 256, xt, ldx, P, yt, ldy);
-  else
-    mlp_combine_kernel<2><<<(unsigned)((n4 + 255) / 256), 256, 0, st>>>(Mt, 256, xt, ldx, P, yt, ldy);
+#define SFX_MLP_SPLIT_LAUNCH(SS)                                                                                   \
+  do {                                                                                                            \
+    mlp_kernel<C, WAVES, RING, HS, MLP_EVAL, false, SS><<<grid, WAVES * 64, 0, st>>>(Mt, xt, ldx, stream, par, eps, \
+                                                                                     yt, ldy, 1, nullptr, nullptr, P); \
+    mlp_combine_kernel<SS><<<(unsigned)((Mt + 3) / 4), 256, 0, st>>>(Mt, C, xt, ldx, P, yt, ldy, et);           \
+  } while (0)
+  if constexpr (NCH % 4 == 0) { if (S == 4) SFX_MLP_SPLIT_LAUNCH(4); }
+  if constexpr (NCH % 3 == 0) { if (S == 3) SFX_MLP_SPLIT_LAUNCH(3); }
+  if constexpr (NCH % 2 == 0) { if (S == 2) SFX_MLP_SPLIT_LAUNCH(2); }
+#undef SFX_MLP_SPLIT_LAUNCH
   return sfx::check_launch("sfx_block_mlp (split tail)");
 }
 
@@ -741,15 +762,15 @@ int sfx_block_mlp(int M, int C, const float* x, long long ldx, const float* stre
     // (waves, ring phases): 4 waves = 128 points per workgroup, 2 workgroups per CU for C <= 128 (64 KB ring);
     // C = 256 runs 4 waves as 2 hidden-split pairs (its LN2 fragments + output accumulators fill 512 registers)
     case 64: return waves == 4 ? (hs == 2 ? run_impl<64, 4, 4, true>(M, x, ldx, stream, params, eps, y, ldy, st, nullptr, reinterpret_cast<float*>(rowexp))
-                                          : run_impl<64, 4, 4>(M, x, ldx, stream, params, eps, y, ldy, st, nullptr, reinterpret_cast<float*>(rowexp)))
+                                          : run_eval_split<64, 4, 4, false>(M, x, ldx, stream, params, eps, y, ldy, st, rowexp))
                                : run_impl<64, 8, 4>(M, x, ldx, stream, params, eps, y, ldy, st, nullptr, reinterpret_cast<float*>(rowexp));
     case 96: return waves == 4 ? (hs == 2 ? run_impl<96, 4, 4, true>(M, x, ldx, stream, params, eps, y, ldy, st, nullptr, reinterpret_cast<float*>(rowexp))
-                                          : run_impl<96, 4, 4>(M, x, ldx, stream, params, eps, y, ldy, st, nullptr, reinterpret_cast<float*>(rowexp)))
+                                          : run_eval_split<96, 4, 4, false>(M, x, ldx, stream, params, eps, y, ldy, st, rowexp))
                                : run_impl<96, 8, 4>(M, x, ldx, stream, params, eps, y, ldy, st, nullptr, reinterpret_cast<float*>(rowexp));
-    case 128: return waves == 4 ? (hs >= 1 ? run_impl<128, 4, 4, true>(M, x, ldx, stream, params, eps, y, ldy, st, nullptr, reinterpret_cast<float*>(rowexp))
+    case 128: return waves == 4 ? (hs >= 1 ? run_eval_split<128, 4, 4, true>(M, x, ldx, stream, params, eps, y, ldy, st, rowexp)
                                           : run_impl<128, 4, 4>(M, x, ldx, stream, params, eps, y, ldy, st, nullptr, reinterpret_cast<float*>(rowexp)))
                                 : run_impl<128, 8, 4>(M, x, ldx, stream, params, eps, y, ldy, st, nullptr, reinterpret_cast<float*>(rowexp));
-    default: return hs ? run_eval256_split(M, x, ldx, stream, params, eps, y, ldy, st, reinterpret_cast<float*>(rowexp))
+    default: return hs ? run_eval_split<256, 4, SFX_MLP_RING256, true>(M, x, ldx, stream, params, eps, y, ldy, st, rowexp)
                        : run_impl<256, 4, SFX_MLP_RING256>(M, x, ldx, stream, params, eps, y, ldy, st, nullptr, reinterpret_cast<float*>(rowexp));
   }
 }

@@ -41,11 +41,24 @@ def test_block_mlp_matches_fp64(device, C, M):
     _check_fp64(device, C, M)
 
 
-@pytest.mark.parametrize("M", [256 * 64 + 1000, 256 * 64 + 5000, 2 * 256 * 64 + 777])
-def test_block_mlp_split_tail(device, M):
-    """C = 256 launches whose last round is at most half full (256 CUs, 64 points per workgroup): the tail runs as
-    4- / 2-way hidden-chunk splits + the fixed-order combine (csrc/mlp.hip run_eval256_split) -- same bar."""
-    _check_fp64(device, 256, M)
+# (C, M) whose last round of workgroups is at most half full on 256 CUs: C = 256 one 64-point workgroup per CU,
+# C = 128 two 64-point (both split their tail), C <= 96 two 128-point ones (not split: the unsplit path again)
+SPLIT_CASES = [(256, 256 * 64 + 1000), (256, 256 * 64 + 5000), (256, 2 * 256 * 64 + 777), (128, 512 * 64 + 2000),
+               (96, 512 * 128 + 3000), (96, 512 * 128 + 20000), (64, 512 * 128 + 5000)]
+
+
+@pytest.mark.parametrize("C,M", SPLIT_CASES)
+def test_block_mlp_split_tail(device, C, M):
+    """Launches whose last round is at most half full: the tail runs as 4- / 3- / 2-way hidden-chunk splits + the
+    fixed-order combine (csrc/mlp.hip run_eval_split) -- the bar of the unsplit kernel -- and the combine's row
+    exponents equal sfx_subm_rowexp of the output."""
+    _check_fp64(device, C, M)
+    ln, fc1, fc2 = _mods(C, 7 * C)
+    x = torch.randn(M, C, generator=torch.Generator().manual_seed(M)) * 2.0
+    mods = [m.to(device) for m in (ln, fc1, fc2)]
+    e = torch.full((M,), -999, device=device, dtype=torch.int32)
+    y = ops.block_mlp(x.to(device), *mods, rowexp=e)
+    assert torch.equal(e.cpu(), ops.subm_rowexp(y).cpu())
 
 
 def _check_fp64(device, C, M):
