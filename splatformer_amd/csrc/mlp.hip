@@ -132,7 +132,7 @@ __global__ void __launch_bounds__(WAVES * 64, (WAVES == 4 && C > 128) ? 1 : 2)
                const float* __restrict__ rowscale, float* __restrict__ Z, float* __restrict__ P = nullptr) {
   using G = MlpGeom<C>;
   constexpr int PTS = HS ? WAVES * 16 : WAVES * 32;  // points per workgroup
-  static_assert(SPLIT == 1 || (KIND == MLP_EVAL && G::NCH % SPLIT == 0), "hidden-chunk split: eval, whole chunks");
+  static_assert(G::NCH % SPLIT == 0, "hidden-chunk split: whole chunks");
   constexpr int NCHS = G::NCH / SPLIT;                // hidden chunks of this workgroup
   constexpr int NB = G::NB, NP = NCHS * G::PPC, PPC = G::PPC, NT = C / 16;  // NT: fc1 k-steps
   constexpr int NTH = WAVES * 64;
@@ -401,12 +401,13 @@ __global__ void __launch_bounds__(WAVES * 64, (WAVES == 4 && C > 128) ? 1 : 2)
       const float4 w01 = pp[2 * g4], w23 = pp[2 * g4 + 1];  // (1/s_c, b2_c) of registers 4 g4 .. 4 g4 + 3
       const unsigned c0 = (unsigned)(32 * b + 8 * g4 + 4 * h);
       float4 y;
-      if constexpr (SPLIT > 1) {  // this split's fc2 partial (b2 carried by split 0) -> P[s][prow]
-        const float bb = blockIdx.y == 0 ? 1.f : 0.f;
-        y.x = acc2[b][4 * g4 + 0] * (tinv * w01.x) + bb * w01.y;
-        y.y = acc2[b][4 * g4 + 1] * (tinv * w01.z) + bb * w01.w;
-        y.z = acc2[b][4 * g4 + 2] * (tinv * w23.x) + bb * w23.y;
-        y.w = acc2[b][4 * g4 + 3] * (tinv * w23.z) + bb * w23.w;
+      if constexpr (SPLIT > 1) {  // this split's branch partial (b2 carried by split 0) -> P[s][prow]
+        const float bb = (KIND != MLP_BWD && blockIdx.y == 0) ? 1.f : 0.f;
+        const float rr = KIND == MLP_BWD ? 1.f : rsp;  // (BWD: rs is applied to dY in the prologue)
+        y.x = rr * (acc2[b][4 * g4 + 0] * (tinv * w01.x) + bb * w01.y);
+        y.y = rr * (acc2[b][4 * g4 + 1] * (tinv * w01.z) + bb * w01.w);
+        y.z = rr * (acc2[b][4 * g4 + 2] * (tinv * w23.x) + bb * w23.y);
+        y.w = rr * (acc2[b][4 * g4 + 3] * (tinv * w23.z) + bb * w23.w);
         if (pok)
           *reinterpret_cast<float4*>(P + ((size_t)blockIdx.y * M + prow) * C + c0) = y;
         continue;
@@ -462,8 +463,8 @@ __global__ void __launch_bounds__(256) mlp_combine_kernel(int M, int C, const fl
       const float4 b = *reinterpret_cast<const float4*>(P + ((size_t)q * M + r) * C + c);
       a = make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
     }
-    const float4 x = *reinterpret_cast<const float4*>(X + (size_t)r * ldx + c);
-    const float4 y = make_float4(x.x + a.x, x.y + a.y, x.z + a.z, x.w + a.w);
+    const float4 x = X ? *reinterpret_cast<const float4*>(X + (size_t)r * ldx + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 y = X ? make_float4(x.x + a.x, x.y + a.y, x.z + a.z, x.w + a.w) : a;
     *reinterpret_cast<float4*>(Y + (size_t)r * ldy + c) = y;
     m = fmaxf(fmaxf(fabsf(y.x), fabsf(y.y)), fmaxf(fabsf(y.z), fabsf(y.w)));
   }
@@ -632,9 +633,9 @@ int cu_count() {
   return cus;
 }
 
-template <int C, int WAVES, int RING, bool HS>
-int run_eval_split(int M, const float* x, long long ldx, const float* stream, const float* par, float eps, float* y,
-                   long long ldy, hipStream_t st, int* rowexp) {
+template <int C, int WAVES, int RING, bool HS, int KIND = MLP_EVAL, bool ONE = false>
+int run_split(int M, const float* x, long long ldx, const float* stream, const float* par, float eps, float* y,
+              long long ldy, hipStream_t st, const float* rowscale, float* z) {
   constexpr int PTS = HS ? WAVES * 16 : WAVES * 32;  // points per workgroup
   constexpr int NCH = C / 16;                       // hidden chunks
   const int wgs = (M + PTS - 1) / PTS, slots = ((WAVES == 4 && C > 128) ? 1 : 2) * cu_count();
@@ -650,30 +651,38 @@ int run_eval_split(int M, const float* x, long long ldx, const float* stream, co
     for (int cand : {4, 3, 2})
       if (NCH % cand == 0 && cand * r <= slots) { S = cand; break; }
   }
-  if (S == 1)
-    return run_impl<C, WAVES, RING, HS>(M, x, ldx, stream, par, eps, y, ldy, st, nullptr,
-                                        reinterpret_cast<float*>(rowexp));
+  if (S == 1) return run_impl<C, WAVES, RING, HS, KIND, ONE>(M, x, ldx, stream, par, eps, y, ldy, st, rowscale, z);
   const int M1 = full * PTS, Mt = M - M1;
   float* P = mlp_split_scratch((size_t)S * Mt * C);
   SFX_REQUIRE(P, "sfx_block_mlp: tail scratch allocation failed");
-  int rc = run_impl<C, WAVES, RING, HS>(M1, x, ldx, stream, par, eps, y, ldy, st, nullptr,
-                                        reinterpret_cast<float*>(rowexp));
+  int rc = run_impl<C, WAVES, RING, HS, KIND, ONE>(M1, x, ldx, stream, par, eps, y, ldy, st, rowscale, z);
   if (rc) return rc;
   const float* xt = x + (size_t)M1 * ldx;
   float* yt = y + (size_t)M1 * ldy;
-  int* et = rowexp ? rowexp + M1 : nullptr;
+  const float* rst = rowscale ? rowscale + M1 : nullptr;
+  // EVAL: z is the optional row-exponent output (written by the combine); TRAIN / BWD: the [M, 4C] pre-activation
+  int* et = (KIND == MLP_EVAL && z) ? reinterpret_cast<int*>(z) + M1 : nullptr;
+  float* zt = (KIND != MLP_EVAL) ? z + (size_t)M1 * 4 * C : nullptr;
   const dim3 grid((unsigned)r, (unsigned)S);
 #define SFX_MLP_SPLIT_LAUNCH(SS)                                                                                   \
   do {                                                                                                            \
-    mlp_kernel<C, WAVES, RING, HS, MLP_EVAL, false, SS><<<grid, WAVES * 64, 0, st>>>(Mt, xt, ldx, stream, par, eps, \
-                                                                                     yt, ldy, 1, nullptr, nullptr, P); \
-    mlp_combine_kernel<SS><<<(unsigned)((Mt + 3) / 4), 256, 0, st>>>(Mt, C, xt, ldx, P, yt, ldy, et);           \
+    mlp_kernel<C, WAVES, RING, HS, KIND, ONE, SS><<<grid, WAVES * 64, 0, st>>>(Mt, xt, ldx, stream, par, eps, yt, \
+                                                                               ldy, 1, rst, zt, P);             \
+    mlp_combine_kernel<SS><<<(unsigned)((Mt + 3) / 4), 256, 0, st>>>(Mt, C, KIND == MLP_BWD ? nullptr : xt, ldx, P, \
+                                                                     yt, ldy, et);                               \
   } while (0)
   if constexpr (NCH % 4 == 0) { if (S == 4) SFX_MLP_SPLIT_LAUNCH(4); }
   if constexpr (NCH % 3 == 0) { if (S == 3) SFX_MLP_SPLIT_LAUNCH(3); }
   if constexpr (NCH % 2 == 0) { if (S == 2) SFX_MLP_SPLIT_LAUNCH(2); }
 #undef SFX_MLP_SPLIT_LAUNCH
   return sfx::check_launch("sfx_block_mlp (split tail)");
+}
+
+template <int C, int WAVES, int RING, bool HS>
+int run_eval_split(int M, const float* x, long long ldx, const float* stream, const float* par, float eps, float* y,
+                   long long ldy, hipStream_t st, int* rowexp) {
+  return run_split<C, WAVES, RING, HS>(M, x, ldx, stream, par, eps, y, ldy, st, nullptr,
+                                       reinterpret_cast<float*>(rowexp));
 }
 
 // the training kinds run the default eval geometry of each C (4 waves; hidden split at C = 128, 256, and for the
@@ -685,9 +694,9 @@ int run_train_p(int M, int C, const float* x, long long ldx, const float* stream
     case 64: return run_impl<64, 4, 4, false, KIND, ONE>(M, x, ldx, stream, par, eps, y, ldy, st, rowscale, z);
     case 96:
       return run_impl<96, 4, 4, KIND == MLP_BWD, KIND, ONE>(M, x, ldx, stream, par, eps, y, ldy, st, rowscale, z);
-    case 128: return run_impl<128, 4, 4, true, KIND, ONE>(M, x, ldx, stream, par, eps, y, ldy, st, rowscale, z);
+    case 128: return run_split<128, 4, 4, true, KIND, ONE>(M, x, ldx, stream, par, eps, y, ldy, st, rowscale, z);
     default:
-      return run_impl<256, 4, SFX_MLP_RING256, true, KIND, ONE>(M, x, ldx, stream, par, eps, y, ldy, st, rowscale, z);
+      return run_split<256, 4, SFX_MLP_RING256, true, KIND, ONE>(M, x, ldx, stream, par, eps, y, ldy, st, rowscale, z);
   }
 }
 

@@ -283,7 +283,9 @@ def test_drop_mask(device):
     assert abs(both - keep * keep) < 0.01
 
 
-@pytest.mark.parametrize("C,M", [(64, 3001), (96, 2050), (128, 1999), (256, 1037)])
+@pytest.mark.parametrize("C,M", [(64, 3001), (96, 2050), (128, 1999), (256, 1037),
+                                 # last round at most half full: split tails (csrc/mlp.hip run_split)
+                                 (128, 512 * 64 + 2000), (256, 256 * 64 + 1000)])
 def test_block_mlp_train_fwd_bwd(device, C, M):
     """Fused training MLP tail (csrc/mlp.hip MLP_TRAIN / MLP_BWD) vs fp64 autograd of LN2 -> fc1 -> GELU -> fc2 ->
     DropPath row scale -> + shortcut: y, the stored pre-activation z, and the LN2-output gradient dh2."""
