@@ -486,7 +486,10 @@ int sfx_fps(int n, int m, const float* xyz, int start, int* out, float* dist_ws,
  * sfx_mlp_pack (once per weight version): w1 [4C][C], b1 [4C], w2 [C][4C], b2 [C], gamma / beta [C] (torch
  *   Linear / LayerNorm layouts, contiguous) -> `stream` (sfx_mlp_stream_floats(C) floats: the pre-split weights
  *   in the kernel's LDS-DMA slab order) and `params` (sfx_mlp_params_floats(C) floats); workspace: 9C ints.
- * sfx_block_mlp: X [M][ldx], Y [M][ldy] (distinct buffers), 16-byte aligned rows; eps = the LayerNorm eps. */
+ * sfx_block_mlp: X [M][ldx], Y [M][ldy] (distinct buffers), 16-byte aligned rows; eps = the LayerNorm eps.
+ * At C >= 128 (and in the training entries below) a launch whose last round of workgroups is at most half full
+ * runs that round as hidden-chunk partials + a fixed-order combine (bitwise reproducible) in a library-owned
+ * per-device scratch buffer, reused in stream order (SFX_MLP_SPLIT=0: one launch). */
 size_t sfx_mlp_stream_floats(int C);
 size_t sfx_mlp_params_floats(int C);
 int sfx_mlp_pack(int C, const float* w1, const float* b1, const float* w2, const float* b2, const float* gamma,
