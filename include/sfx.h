@@ -175,7 +175,8 @@ int sfx_ln_amax_bound(int C, const float* gamma, const float* beta, unsigned lon
  * process.  Eight-wave configurations apply only to split (K >= 64) launches. */
 int sfx_gemm_force_config(int cfg, int stream_k);
 
-/* Library operand-precision mode for every later GEMM launch of the process (ABI 14):
+/* Library operand-precision mode for every later GEMM launch issued by the calling host thread (ABI 14; per thread
+ * since ABI 15 -- launches from other threads keep their own mode, default 0):
  *   0 (default) fp32-accurate: fp16x2 / bf16x3 split operands, three resp. six term products per block;
  *   1 reference precision, the class of the reference's fp16 autocast training (train.py:240,
  *     configs/train/default.gin:11): sfx_linear / sfx_subm_conv / sfx_linear_bwd_data and the SubM conv
@@ -403,9 +404,12 @@ int sfx_render_prep_project_views(int n, int views, int num_bases, const float* 
                                   float* records, void* stream);
 /* (ABI v13) records (optional, [views * n][16]): also writes sfx_pack_raster_records' record of every
  * Gaussian-view (no separate packing pass) */
+/* (ABI v15) capacity: the length of isect_ids / gaussian_ids; pairs whose prefix offset falls outside [0, capacity)
+ * are dropped, so a wrong prefix (a look-back scan that reached its spin cap, sfx_lookback_timeouts) can give a
+ * wrong list but never an out-of-bounds write (also sfx_isect_emit_cull_views) */
 int sfx_isect_emit_views(int n_total, int n_per_view, const float* xys, const float* depths, const int* radii,
                          const int* cum_tiles_hit, int tiles_x, int tiles_y, int block_width, int64_t* isect_ids,
-                         int32_t* gaussian_ids, void* stream);
+                         int32_t* gaussian_ids, long long capacity, void* stream);
 int sfx_rasterize_fwd_views(int views, int tiles_x, int tiles_y, int block_width, int img_h, int img_w,
                             const int32_t* gids_sorted, const int* tile_bins, const float* xys, const float* conics,
                             const float* colors, const float* opacity, const float* background, int clamp_max1,
@@ -426,7 +430,7 @@ int sfx_isect_count_cull_views(int n_total, int n_per_view, const float* xys, co
 int sfx_isect_emit_cull_views(int n_total, int n_per_view, const float* xys, const float* conics,
                               const float* opacities, const float* depths, const int* radii, const int* cum_tiles_hit,
                               int tiles_x, int tiles_y, int block_width, int img_h, int img_w, int64_t* isect_ids,
-                              int32_t* gaussian_ids, const int* rank, void* stream);
+                              int32_t* gaussian_ids, const int* rank, long long capacity, void* stream);
 /* (ABI v13) two-level intersection sort: keys[i] = the depth bits of depths[i] (u64).  Argsorting them (stable,
  * sfx_sort_pairs_u64 bits [0, 32)) gives `order`, sfx_invert_permutation its inverse `rank`;
  * sfx_isect_emit_cull_views with that rank (cum_tiles_hit = the inclusive scan of num_tiles_kept[order]) emits the
@@ -489,7 +493,9 @@ int sfx_fps(int n, int m, const float* xyz, int start, int* out, float* dist_ws,
  * sfx_block_mlp: X [M][ldx], Y [M][ldy] (distinct buffers), 16-byte aligned rows; eps = the LayerNorm eps.
  * At C >= 128 (and in the training entries below) a launch whose last round of workgroups is at most half full
  * runs that round as hidden-chunk partials + a fixed-order combine (bitwise reproducible) in a library-owned
- * per-device scratch buffer, reused in stream order (SFX_MLP_SPLIT=0: one launch). */
+ * scratch buffer per (device, stream), reused in stream order (SFX_MLP_SPLIT=0: one launch).  The buffer grows
+ * on the first call that needs more (synchronising that stream once): under HIP graph capture, run the entry
+ * once at the captured sizes before capturing. */
 size_t sfx_mlp_stream_floats(int C);
 size_t sfx_mlp_params_floats(int C);
 int sfx_mlp_pack(int C, const float* w1, const float* b1, const float* w2, const float* b2, const float* gamma,

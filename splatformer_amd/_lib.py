@@ -133,6 +133,25 @@ class HostRead:
         return self._v is not None or self._ev.query()
 
 
+_LB_SEEN: dict = {}  # stream -> look-back timeouts already reported (one process per GPU)
+
+
+def check_lookback(where: str, st=None) -> None:
+    """Raise if a decoupled look-back wait (single-pass scan / radix pass, csrc/common.h lb_lookback_wave) on this
+    stream reached its spin cap since the last check: that scan's prefix -- an intersection list, a pooled count --
+    is wrong.  Call where results are consumed on the host (the stream is drained there anyway: the call
+    synchronises it).  Each timeout is reported once; later checks only report new ones."""
+    st = stream() if st is None else st
+    n = int(fn("sfx_lookback_timeouts")(st))
+    if n <= 0:  # 0: every wait exact; -1: nothing scanned on this stream yet
+        return
+    seen = _LB_SEEN.get(st, 0)
+    if n > seen:
+        _LB_SEEN[st] = n
+        raise RuntimeError(f"{where}: {n - seen} decoupled look-back wait(s) on this stream reached the spin cap "
+                           "(a scan or radix pass produced a wrong prefix; its results are invalid)")
+
+
 def require_gpu(t: torch.Tensor | None = None) -> None:
     if not torch.cuda.is_available():
         raise RuntimeError("splatformer_amd requires a ROCm GPU (MI355X); no device is visible")

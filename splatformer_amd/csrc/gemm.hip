@@ -907,8 +907,10 @@ constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
 // Operand precision of a launch (GemmArgs::split): exact fp32 MFMA below K = 64 (SFX_GEMM_SPLIT_MINK) or with
 // SFX_GEMM_PREC=fp32; otherwise split operands, fp16x2 (default) or bf16x3 (SFX_GEMM_PREC=bf16x3).  Both split
 // forms are as accurate as fp32 arithmetic; fp16x2 needs half the MFMAs and LDS images of bf16x3.
-// library precision mode (sfx_set_precision): 0 fp32-accurate (default), 1 reference precision (autocast class)
-int g_prec = 0;
+// library precision mode (sfx_set_precision): 0 fp32-accurate (default), 1 reference precision (autocast class);
+// per host thread, so a launch from another thread (an eval pass beside a Trainer inside its amp region) keeps
+// its own mode
+thread_local int g_prec = 0;
 
 int split_mode(int K) {
   static int min_k = -2, mode = 2;

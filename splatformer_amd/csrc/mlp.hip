@@ -31,6 +31,8 @@
 // ([2 halves][2 terms][32 channels][32 units, permuted]).  A phase = 2 slabs (16 KB) = 12 MFMAs per wave; the ring
 // holds RING phases, RING-1 in flight; one barrier per phase (RAW for the arriving slabs, WAR for the refilled
 // slot), counted vmcnt, raw s_barrier (no __syncthreads: its fence would drain the DMA queue).
+#include <map>
+#include <mutex>
 #include <cstdlib>
 
 #include "gemm_common.h"
@@ -606,21 +608,33 @@ int run_impl(int M, const float* x, long long ldx, const float* stream, const fl
 
 // The C = 256 eval tail split: one 4-wave workgroup per CU (512-register waves), so a launch of W workgroups runs
 // ceil(W / CUs) rounds; when the last round is at most half full its workgroups run as SPLIT = 2 or 4 hidden-chunk
-// splits (one round of 1/SPLIT the work) + mlp_combine_kernel.  Scratch: a per-device buffer grown on demand
-// (stream-ordered reuse: the library's launches of one device run on one stream at a time).
-float* mlp_split_scratch(size_t floats) {
-  static float* bufs[64] = {};
-  static size_t caps[64] = {};
+// splits (one round of 1/SPLIT the work) + mlp_combine_kernel.  Scratch: one buffer per (device, stream) behind a
+// mutex (as sfx::lookback_state), grown on demand -- launches on two streams or host threads never share partials,
+// and a stream's reuse is ordered by the stream itself.  Growing synchronises that stream before freeing the old
+// buffer (work in flight may still read it), so it must not happen inside a graph capture: warm the entry up once
+// at the captured sizes first (include/sfx.h, sfx_block_mlp).
+float* mlp_split_scratch(size_t floats, hipStream_t st) {
+  struct Buf {
+    float* p = nullptr;
+    size_t cap = 0;
+  };
+  static std::mutex mu;
+  static std::map<std::pair<int, hipStream_t>, Buf> bufs;
   int dev = 0;
-  (void)hipGetDevice(&dev);
-  if (caps[dev] < floats) {
-    if (bufs[dev]) (void)hipFree(bufs[dev]);
-    bufs[dev] = nullptr;
-    caps[dev] = 0;
-    if (hipMalloc(&bufs[dev], floats * sizeof(float)) != hipSuccess) return nullptr;
-    caps[dev] = floats;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lock(mu);
+  Buf& b = bufs[{dev, st}];
+  if (b.cap < floats) {
+    if (b.p) {
+      if (hipStreamSynchronize(st) != hipSuccess || hipFree(b.p) != hipSuccess) return nullptr;
+      b = Buf();
+    }
+    void* q = nullptr;
+    if (hipMalloc(&q, floats * sizeof(float)) != hipSuccess) return nullptr;
+    b.p = static_cast<float*>(q);
+    b.cap = floats;
   }
-  return bufs[dev];
+  return b.p;
 }
 
 int cu_count() {
@@ -653,7 +667,7 @@ int run_split(int M, const float* x, long long ldx, const float* stream, const f
   }
   if (S == 1) return run_impl<C, WAVES, RING, HS, KIND, ONE>(M, x, ldx, stream, par, eps, y, ldy, st, rowscale, z);
   const int M1 = full * PTS, Mt = M - M1;
-  float* P = mlp_split_scratch((size_t)S * Mt * C);
+  float* P = mlp_split_scratch((size_t)S * Mt * C, st);
   SFX_REQUIRE(P, "sfx_block_mlp: tail scratch allocation failed");
   int rc = run_impl<C, WAVES, RING, HS, KIND, ONE>(M1, x, ldx, stream, par, eps, y, ldy, st, rowscale, z);
   if (rc) return rc;

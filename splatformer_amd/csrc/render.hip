@@ -8,6 +8,8 @@
 // quats (w,x,y,z), [N,2] xys, [N,3] conics ...), so the drop-in shim can hand
 // torch tensors straight through.  One workgroup of bw*bw lanes (4 waves at
 // bw=16) per 16x16 tile; per-batch Gaussian records staged in LDS.
+#include <climits>
+
 #include "common.h"
 
 namespace {
@@ -619,17 +621,19 @@ __global__ void project_bwd_kernel(int n, const float* __restrict__ means, const
 __global__ void isect_emit_kernel(int n, const float* __restrict__ xys, const float* __restrict__ depths,
                                   const int* __restrict__ radii, const int* __restrict__ cum_tiles_hit,
                                   int tiles_x, int tiles_y, int bw, int64_t* __restrict__ isect_ids,
-                                  int32_t* __restrict__ gaussian_ids, int n_per_view) {
+                                  int32_t* __restrict__ gaussian_ids, int n_per_view, int cap) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   if (radii[i] <= 0) return;
   int x0, y0, x1, y1;
   get_tile_bbox(xys[2 * i], xys[2 * i + 1], (float)radii[i], tiles_x, tiles_y, bw, x0, y0, x1, y1);
-  int cur = (i == 0) ? 0 : cum_tiles_hit[i - 1];
+  // cap: the caller's buffer length -- a wrong prefix (a look-back scan that timed out) cannot write out of bounds
+  int cur = (i == 0) ? 0 : max(cum_tiles_hit[i - 1], 0);
   const int64_t depth_id = (int64_t)__float_as_int(depths[i]);
   const int64_t tile_base = n_per_view > 0 ? (int64_t)(i / n_per_view) * tiles_x * tiles_y : 0;
   for (int ty = y0; ty < y1; ++ty)
     for (int tx = x0; tx < x1; ++tx) {
+      if (cur >= cap) return;
       const int64_t tile_id = tile_base + (int64_t)ty * tiles_x + tx;
       isect_ids[cur] = (tile_id << 32) | (depth_id & 0xffffffffll);
       gaussian_ids[cur] = i;
@@ -983,7 +987,7 @@ isect_emit_cull_kernel(int n, int n_per_view, const float* __restrict__ xys, con
                        const float* __restrict__ opac, const float* __restrict__ depths,
                        const int* __restrict__ radii, const int* __restrict__ cum_tiles_hit, int tiles_x,
                        int tiles_y, int bw, int img_h, int img_w, int64_t* __restrict__ isect_ids,
-                       int32_t* __restrict__ gaussian_ids, const int* __restrict__ rank) {
+                       int32_t* __restrict__ gaussian_ids, const int* __restrict__ rank, int cap) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   const int j = (rank && i < n) ? rank[i] : i;
   const int lane = threadIdx.x & 63;
@@ -993,8 +997,10 @@ isect_emit_cull_kernel(int n, int n_per_view, const float* __restrict__ xys, con
   w.g = cull_setup(0.f, 0.f, 0.f, 0.f, 0.f, 0.f);
   int cur = 0, end = 0;
   if (i < n) {
-    cur = (j == 0) ? 0 : cum_tiles_hit[j - 1];
-    end = cum_tiles_hit[j];
+    // [cur, end) clamped into the caller's buffer [0, cap): a wrong prefix (a look-back scan that timed out, counted
+    // by sfx_lookback_timeouts) yields a wrong list, never an out-of-bounds write
+    cur = (j == 0) ? 0 : max(cum_tiles_hit[j - 1], 0);
+    end = min(cum_tiles_hit[j], cap);
     if (end > cur) w = cull_walk_setup(i, xys, conics, opac, radii, tiles_x, tiles_y, bw);
   }
   const int64_t depth_id = i < n ? (int64_t)__float_as_int(depths[i]) & 0xffffffffll : 0;
@@ -1575,7 +1581,7 @@ int sfx_isect_emit(int n, const float* xys, const float* depths, const int* radi
   if (n == 0) return SFX_OK;
   SFX_REQUIRE(xys && depths && radii && cum_tiles_hit && isect_ids && gaussian_ids, "sfx_isect_emit: null buffer");
   isect_emit_kernel<<<sfx::ceil_div(n, 256), 256, 0, sfx::as_stream(stream)>>>(
-      n, xys, depths, radii, cum_tiles_hit, tiles_x, tiles_y, block_width, isect_ids, gaussian_ids, 0);
+      n, xys, depths, radii, cum_tiles_hit, tiles_x, tiles_y, block_width, isect_ids, gaussian_ids, 0, INT_MAX);
   return sfx::check_launch("sfx_isect_emit");
 }
 
@@ -1656,14 +1662,15 @@ int sfx_render_prep_project_views(int n, int views, int num_bases, const float* 
 
 int sfx_isect_emit_views(int n_total, int n_per_view, const float* xys, const float* depths, const int* radii,
                          const int* cum_tiles_hit, int tiles_x, int tiles_y, int block_width, int64_t* isect_ids,
-                         int32_t* gaussian_ids, void* stream) {
+                         int32_t* gaussian_ids, long long capacity, void* stream) {
   SFX_REQUIRE(n_total >= 0 && n_per_view > 0 && n_total % n_per_view == 0, "sfx_isect_emit_views: bad sizes");
   SFX_REQUIRE(block_width > 1 && block_width <= 16, "sfx_isect_emit_views: block_width must be in (1,16]");
   if (n_total == 0) return SFX_OK;
   SFX_REQUIRE(xys && depths && radii && cum_tiles_hit && isect_ids && gaussian_ids,
               "sfx_isect_emit_views: null buffer");
   isect_emit_kernel<<<sfx::ceil_div(n_total, 256), 256, 0, sfx::as_stream(stream)>>>(
-      n_total, xys, depths, radii, cum_tiles_hit, tiles_x, tiles_y, block_width, isect_ids, gaussian_ids, n_per_view);
+      n_total, xys, depths, radii, cum_tiles_hit, tiles_x, tiles_y, block_width, isect_ids, gaussian_ids, n_per_view,
+      (int)(capacity < INT_MAX ? capacity : INT_MAX));
   return sfx::check_launch("sfx_isect_emit_views");
 }
 
@@ -1730,7 +1737,7 @@ int sfx_isect_count_cull_views(int n_total, int n_per_view, const float* xys, co
 int sfx_isect_emit_cull_views(int n_total, int n_per_view, const float* xys, const float* conics,
                               const float* opacities, const float* depths, const int* radii, const int* cum_tiles_hit,
                               int tiles_x, int tiles_y, int block_width, int img_h, int img_w, int64_t* isect_ids,
-                              int32_t* gaussian_ids, const int* rank, void* stream) {
+                              int32_t* gaussian_ids, const int* rank, long long capacity, void* stream) {
   SFX_REQUIRE(n_total >= 0 && n_per_view > 0 && n_total % n_per_view == 0, "sfx_isect_emit_cull_views: bad sizes");
   SFX_REQUIRE(block_width > 1 && block_width <= 16, "sfx_isect_emit_cull_views: block_width must be in (1,16]");
   SFX_REQUIRE(tiles_x == (img_w + block_width - 1) / block_width && tiles_y == (img_h + block_width - 1) / block_width,
@@ -1740,7 +1747,7 @@ int sfx_isect_emit_cull_views(int n_total, int n_per_view, const float* xys, con
               "sfx_isect_emit_cull_views: null buffer");
   isect_emit_cull_kernel<<<sfx::ceil_div(n_total, 256), 256, 0, sfx::as_stream(stream)>>>(
       n_total, n_per_view, xys, conics, opacities, depths, radii, cum_tiles_hit, tiles_x, tiles_y, block_width, img_h,
-      img_w, isect_ids, gaussian_ids, rank);
+      img_w, isect_ids, gaussian_ids, rank, (int)(capacity < INT_MAX ? capacity : INT_MAX));
   return sfx::check_launch("sfx_isect_emit_cull_views");
 }
 

@@ -12,7 +12,7 @@ from typing import Callable, Dict, Sequence
 
 import torch
 
-from . import dist
+from . import _lib, dist
 from .gs_render import rasterize_gaussians_to_multiimgs
 from .metrics import image_stats_u8, psnr_from_stats, ssim
 
@@ -43,5 +43,7 @@ def evaluate_scenes(model, scenes: Sequence[dict], cameras: Sequence[dict],
         num_images += pred.shape[0]
         if not evaluate_input and hasattr(model, "check_refine"):
             model.check_refine()  # the refine's deferred pooling checks, at the readback that consumes it
+        else:
+            _lib.check_lookback("evaluate_scenes")  # the render's intersection scans / sorts
     return dist.reduce_metrics({"psnr": psnr_sum, "ssim": ssim_sum}, num_images, len(mine),
                                device=device if ws > 1 and device.type == "cuda" else None)

@@ -184,8 +184,11 @@ class FeaturePredictor(nn.Module):
     def check_refine(self, wait: bool = True) -> None:
         """Validate the pooled run counts of the refines issued so far (PointTransformerV3.check_deferred): call
         where a refined result is consumed on the host (evaluate_scenes does, at its metric readback).  Raises once
-        per failing forward, naming it; the model stays usable."""
+        per failing forward, naming it; the model stays usable.  With `wait`, also the stream's look-back scans
+        (serialization / pooling / intersection sorts: _lib.check_lookback; the stream is drained there)."""
         self.backbone.backbone.check_deferred(wait=wait)
+        if wait:
+            _lib.check_lookback("FeaturePredictor.check_refine")
 
     def _fused_heads(self):
         """(slab stream, parameter table, output columns, out_dim) of the fused heads kernel, rebuilt with the

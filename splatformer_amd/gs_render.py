@@ -51,12 +51,12 @@ def _scalar(x) -> float:
 
 _lib.register("sfx_render_prep_project_views", [I, I, I, P, L, P, L, P, L, P, L, P, L, P, L, P, F, F, F, F, I, I, I,
                                                  P, P, P, P, P, P, P, P, P])
-_lib.register("sfx_isect_emit_views", [I, I, P, P, P, P, I, I, I, P, P, P])
+_lib.register("sfx_isect_emit_views", [I, I, P, P, P, P, I, I, I, P, P, L, P])
 _lib.register("sfx_rasterize_fwd_views", [I, I, I, I, I, I, P, P, P, P, P, P, P, I, P, P, P, P, P])
 _lib.register("sfx_pack_raster_records", [I, P, P, P, P, P, P])
 _lib.register("sfx_rasterize_fwd_views_packed", [I, I, I, I, I, I, P, P, P, P, I, P, P, P, P, P])
 _lib.register("sfx_isect_count_cull_views", [I, I, P, P, P, P, I, I, I, I, I, P, P])
-_lib.register("sfx_isect_emit_cull_views", [I, I, P, P, P, P, P, P, I, I, I, I, I, P, P, P, P])
+_lib.register("sfx_isect_emit_cull_views", [I, I, P, P, P, P, P, P, I, I, I, I, I, P, P, P, L, P])
 _lib.register("sfx_depth_keys", [L, P, P, P])
 _lib.register("sfx_invert_permutation", [L, P, P, P])
 _lib.register("sfx_rasterize_fwd_views_quad", [I, I, I, I, I, I, P, P, P, P, I, P, P, P, P, P])
@@ -237,10 +237,10 @@ def _render_fused_views(gs, c2ws, cameras, meta=None):
         if cull:
             call("sfx_isect_emit_cull_views", V * n, n, ptr(xys), ptr(conics), ptr(opac), ptr(depths), ptr(radii),
                  ptr(cum_o if two_level else cum), tiles_x, tiles_y, bw, H, W, ptr(isect), ptr(gids),
-                 ptr(drank) if two_level else None, stream())
+                 ptr(drank) if two_level else None, total, stream())
         else:
             call("sfx_isect_emit_views", V * n, n, ptr(xys), ptr(depths), ptr(radii), ptr(cum), tiles_x, tiles_y, bw,
-                 ptr(isect), ptr(gids), stream())
+                 ptr(isect), ptr(gids), total, stream())
         isect_s, gids_s = torch.empty_like(isect), torch.empty_like(gids)
         key_bits = 32 + max(1, int(V * T - 1).bit_length())
         ws = _lib.workspace(_lib.fn("sfx_sort_workspace_bytes")(total), dev)

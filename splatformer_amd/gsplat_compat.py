@@ -38,7 +38,7 @@ def deg_from_sh(num_bases: int) -> int:
 CULL = os.environ.get("SFX_RENDER_CULL", "1") != "0"
 _I, _P = _lib.I, _lib.P
 _lib.register("sfx_isect_count_cull_views", [_I, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P])
-_lib.register("sfx_isect_emit_cull_views", [_I, _I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P])
+_lib.register("sfx_isect_emit_cull_views", [_I, _I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _lib.L, _P])
 _lib.register("sfx_pack_raster_records", [_I, _P, _P, _P, _P, _P, _P])
 _lib.register("sfx_rasterize_fwd_views_quad", [_I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _I, _P, _P, _P, _P, _P])
 _lib.register("sfx_rasterize_bwd_quad", [_I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
@@ -270,7 +270,7 @@ def _culled_forward(n, xys, depths, radii, conics, colors, opacity, background, 
     isect = torch.empty(total, device=dev, dtype=torch.int64)
     gids = torch.empty(total, device=dev, dtype=torch.int32)
     call("sfx_isect_emit_cull_views", n, n, ptr(xys), ptr(conics), ptr(opacity), ptr(depths), ptr(radii), ptr(cum),
-         tiles_x, tiles_y, 16, H, W, ptr(isect), ptr(gids), None, stream())
+         tiles_x, tiles_y, 16, H, W, ptr(isect), ptr(gids), None, total, stream())
     isect_s, gids_s = torch.empty_like(isect), torch.empty_like(gids)
     ws = _lib.workspace(_lib.fn("sfx_sort_workspace_bytes")(total), dev)
     call("sfx_sort_pairs_u64", total, ptr(isect), ptr(gids), ptr(isect_s), ptr(gids_s), 0,

@@ -46,20 +46,50 @@ def wt(w: Tensor) -> Tensor:
     return t
 
 
-def device_drop_masks(generator: Optional[torch.Generator] = None) -> MaskFn:
-    """timm DropPath per point: keep ~ Bernoulli(1-p), scaled by 1/(1-p); None when p == 0 (Identity).  One
-    sfx_drop_mask launch per mask; the hash seeds come from the generator's seed and a host-side draw counter
-    (reproducible for a seeded generator, no device read)."""
-    base = int(generator.initial_seed()) if generator is not None else int(torch.initial_seed())
-    state = {"k": 0}
+_MASK_STREAMS = [0]  # DropMasks objects created in this process (each gets its own seed stream)
 
-    def fn(name: str, n: int, p: float, device=None) -> Optional[Tensor]:
+
+class DropMasks:
+    """timm DropPath per point: keep ~ Bernoulli(1-p), scaled by 1/(1-p); None when p == 0 (Identity).  One
+    sfx_drop_mask launch per mask, hash-seeded from (base seed, rank, stream id, draw counter): reproducible for a
+    seeded generator with no device read, different on every DDP rank (timm draws each rank's masks from its own
+    device RNG state), and different for every DropMasks of the process (a second Trainer, or one re-created in
+    the same process, does not replay the first one's masks).  state_dict / load_state_dict carry the counter
+    across a checkpoint resume (Trainer.state_dict)."""
+
+    def __init__(self, generator: Optional[torch.Generator] = None, rank: Optional[int] = None):
+        self.base = int(generator.initial_seed()) if generator is not None else int(torch.initial_seed())
+        if rank is None:
+            dist = torch.distributed
+            rank = dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
+        self.rank = int(rank)
+        self.stream_id = _MASK_STREAMS[0]
+        _MASK_STREAMS[0] += 1
+        self.k = 0
+
+    def seed(self) -> int:
+        m = 0xFFFFFFFFFFFFFFFF
+        s = (self.base * 0x9E3779B97F4A7C15) & m
+        s = (s ^ ((self.rank + 1) * 0xBF58476D1CE4E5B9)) & m
+        s = (s ^ (self.stream_id * 0x94D049BB133111EB)) & m
+        return (s + self.k * 0xD1B54A32D192ED03) & m
+
+    def __call__(self, name: str, n: int, p: float, device=None) -> Optional[Tensor]:
         if p <= 0.0:
             return None
-        state["k"] += 1
-        seed = (base * 0x9E3779B97F4A7C15 + state["k"] * 0xD1B54A32D192ED03) & 0xFFFFFFFFFFFFFFFF
-        return tops.drop_mask(n, 1.0 - p, seed, device)
-    return fn
+        self.k += 1
+        return tops.drop_mask(n, 1.0 - p, self.seed(), device)
+
+    def state_dict(self) -> dict:
+        return {"base": self.base, "rank": self.rank, "stream_id": self.stream_id, "k": self.k}
+
+    def load_state_dict(self, sd: dict) -> None:
+        self.base, self.rank, self.stream_id, self.k = (int(sd[k]) for k in ("base", "rank", "stream_id", "k"))
+
+
+def device_drop_masks(generator: Optional[torch.Generator] = None, rank: Optional[int] = None) -> MaskFn:
+    """The default DropPath mask source of the training step (DropMasks)."""
+    return DropMasks(generator, rank)
 
 
 def _grad_buffers(lin: torch.nn.Linear):

@@ -17,6 +17,7 @@ from typing import Dict, List, Optional, Sequence
 import torch
 from torch import Tensor
 
+from . import _lib
 from . import ptv3_ops as ops
 from . import ptv3_train as pt
 from . import train_ops as tops
@@ -104,8 +105,9 @@ class Trainer:
         """precision: "fp32" (default; fp32-accurate refiner forward + backward) or "amp", the reference's
         `training.enable_amp` (train.py:214-299, configs/train/default.gin:11): refiner forward and backward in
         the autocast precision class (ptv3_ops.precision); the renderer, loss and optimiser stay fp32 as in the
-        reference (its rasterisation runs outside the autocast region).  No GradScaler: the GEMMs scale every
-        operand row by its own power of two, so fp16 range limits never flush or overflow a gradient.
+        reference (its rasterisation runs outside the autocast region).  No loss scale: the GEMMs scale every
+        operand row by its own power of two, so fp16 range limits never flush or overflow a gradient; GradScaler's
+        skip of a step with non-finite gradients is kept (optimizer_step).
         Default from SFX_TRAIN_PREC."""
         self.model = model
         self.precision = precision or os.environ.get("SFX_TRAIN_PREC", "fp32")
@@ -130,6 +132,7 @@ class Trainer:
         self.world = torch.distributed.get_world_size(group) if group is not None else 1
         self.masks = pt.device_drop_masks(generator)
         self.step_count = 0
+        self.skipped_steps = 0  # amp: optimiser steps skipped for non-finite gradients (GradScaler semantics)
         self.micro = 0
         self.last_norm: Optional[Tensor] = None
 
@@ -153,7 +156,9 @@ class Trainer:
             total = total + loss.detach()  # summed on the device: one host read per micro-step, not per scene
             del tape, packed, leaf, out_gs, preds
         self.micro += 1
-        return float(total)
+        loss = float(total)  # (drains the stream)
+        _lib.check_lookback("Trainer.micro_step")  # the step's scans / radix passes (pooling, intersection sort)
+        return loss
 
     def optimizer_step(self) -> None:
         if self.group is not None and self.world > 1:
@@ -161,6 +166,16 @@ class Trainer:
         coef = None
         if self.clip > 0:
             coef, self.last_norm = tops.grad_clip_coef([self.flat_grad], self.clip)
+        if self.precision == "amp":
+            # GradScaler.step (train.py:297-298) skips the optimiser step when a gradient is inf / NaN; with no loss
+            # scale to halve (the per-row operand scales need none) the skip is all that remains.  One 8-byte read
+            # per optimiser step: the micro-steps' loss reads have drained the stream already.
+            norm = self.last_norm if self.last_norm is not None else self.flat_grad.square().sum()
+            if not bool(torch.isfinite(norm).all()):
+                self.skipped_steps += 1
+                self.flat_grad.zero_()
+                self.micro = 0
+                return
         self.step_count += 1
         for p, m1, m2 in zip(self.params, self.exp_avg, self.exp_avg_sq):
             tops.adam_step(p.data, p.grad, m1, m2, self.step_count, self.lr, self.betas, self.eps, grad_scale=coef)
@@ -169,6 +184,22 @@ class Trainer:
             torch.autograd.graph.increment_version(p)
         self.flat_grad.zero_()
         self.micro = 0
+
+    def state_dict(self) -> dict:
+        """Optimiser state for a resume: Adam moments, step counts and the DropPath mask counter (so a resumed
+        run draws new masks instead of replaying step 0's)."""
+        return {"exp_avg": [t.detach().cpu() for t in self.exp_avg],
+                "exp_avg_sq": [t.detach().cpu() for t in self.exp_avg_sq],
+                "step_count": self.step_count, "skipped_steps": self.skipped_steps,
+                "masks": self.masks.state_dict() if hasattr(self.masks, "state_dict") else None}
+
+    def load_state_dict(self, sd: dict) -> None:
+        for dst, src in zip(self.exp_avg + self.exp_avg_sq, list(sd["exp_avg"]) + list(sd["exp_avg_sq"])):
+            dst.copy_(src)
+        self.step_count = int(sd["step_count"])
+        self.skipped_steps = int(sd.get("skipped_steps", 0))
+        if sd.get("masks") is not None and hasattr(self.masks, "load_state_dict"):
+            self.masks.load_state_dict(sd["masks"])
 
     def step(self, scenes, cameras, images, masks=None, perms=None) -> float:
         loss = self.micro_step(scenes, cameras, images, masks=masks, perms=perms)

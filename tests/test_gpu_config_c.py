@@ -22,8 +22,10 @@ configs/train/default.gin:11; ops.precision / include/sfx.h sfx_set_precision): 
 refiner backward (same weights, order shuffles, DropPath masks and upstream gradient) in that mode, against the
 oracle in its autocast mode (oracle/ptv3_ref.autocast: every value CUDA autocast holds in fp16 rounded to fp16;
 the reference's GradScaler loss scaling emulated):
-the refined residual's and the qkv gradients' distances to the fp32 / fp64 oracle are at most 1.5x the autocast
-oracle's own (the autocast oracle replays the amp run's head ReLU active sets) (and the residual measurably differs from the fp32 mode's, > 1e-5: the mode is on).
+the refined residual's distance to the fp32 oracle and the qkv gradients' distance to the fp32 oracle run on the amp
+run's head ReLU active sets are at most 1.5x the autocast oracle's own (the autocast oracle replays the same active
+sets, so neither side carries ReLU-flip error and the bar measures the fp16 rounding, ~1e-3); the residual
+measurably differs from the fp32 mode's (> 1e-5: the mode is on).
 """
 import pytest
 import torch
@@ -258,12 +260,23 @@ def test_config_c_amp_train_forward(hip_c, hip_amp, oracle32, oracle_amp):
     assert 1e-5 < e_hip <= 1.5 * e_orc
 
 
-def test_config_c_amp_qkv_grads(hip_c, hip_amp, oracle64, oracle_amp):
+@pytest.fixture(scope="module")
+def oracle32_amp_relu(hip_c, hip_amp):
+    """The fp32 oracle on the amp run's head ReLU active sets: the reference the amp-side qkv gradients are held to.
+    Against the fp64 oracle (the fp32 run's active sets) both amp sides carry the same ~1e-2 of ReLU flips, which
+    would hide ~1e-2 of extra amp-path error under a 1.5x bar; with the flips replayed on the reference side the
+    distance measured is the fp16 rounding itself (~1e-3)."""
+    return _oracle(hip_c, torch.float32, relu=hip_amp["relu"])[0]
+
+
+def test_config_c_amp_qkv_grads(hip_c, hip_amp, oracle_amp, oracle32_amp_relu):
     g16, _ = oracle_amp
     names = hip_c["names"]
     hip = torch.cat([hip_amp["grads"][k].double().reshape(-1) for k in names])
     r16 = torch.cat([g16[k].reshape(-1) for k in names])
-    r64 = torch.cat([oracle64[k].reshape(-1) for k in names])
-    e_hip, e_orc = rel_l2(hip, r64), rel_l2(r16, r64)
-    print(f"\n[config C amp] qkv grads to fp64: HIP amp {e_hip:.2e}, autocast oracle {e_orc:.2e}")
+    r32 = torch.cat([oracle32_amp_relu[k].double().reshape(-1) for k in names])
+    e_hip, e_orc = rel_l2(hip, r32), rel_l2(r16, r32)
+    print(f"\n[config C amp] qkv grads to the fp32 oracle on the amp ReLU sets: HIP amp {e_hip:.2e}, "
+          f"autocast oracle {e_orc:.2e}")
+    assert e_orc < 1e-2  # the reference carries no ReLU-flip error: the bar measures fp16 rounding
     assert e_hip <= 1.5 * e_orc

@@ -20,7 +20,7 @@ Checked:
   averaged bucket (rel <= 1e-6); against Adam on the fp64 oracle's gradient every updated weight agrees to
   1e-2 lr except where the fp64 gradient itself is within 1e-3 of its rms of zero (a first Adam step is
   lr * sign(g): an element whose gradient is rounding noise may take either sign), and such disagreements are
-  at most 2x (+100) as many as the fp32 oracle's own;
+  at most 1.01x (+1) as many as the fp32 oracle's own;
 * the next micro-step's train forward on the updated weights vs the oracle's on its own updated weights:
   refined residual rel L2 <= 1e-5.
 """
