@@ -295,6 +295,16 @@ int sfx_window_attention(int num_windows, int window, int heads, int head_dim, i
 int sfx_window_attention_varlen(int num_windows, int max_window, int heads, int head_dim, int channels,
                                 const float* qkv, const int* order, const int* win3, float scale, float* out,
                                 const unsigned long long* qkv_amax, unsigned qkv_tag, void* stream);
+/* (ABI v15) Fused attention + output projection + residual for the eval Block (calflops.py:51-69:
+ * x = shortcut + proj(attn(norm1 x))): x2[r] = x1[r] + bias + W . concat_h(softmax(q_h k_h^T scale) v_h)[r] over the
+ * non-flash windows of sfx_window_attention (same `win` table, order, scale), all heads of a window in one
+ * workgroup, the per-head outputs never leaving the chip.  fp16x2 terms only: qkv_amax (required) bounds |qkv|;
+ * w_split / w_inv = sfx_weight_split of the projection weight [C][C]; bias [C]; x1 [n][ldx1] and x2 [n][ldx2]
+ * distinct, 16-byte aligned rows.  (channels, head_dim) in {(64, 32), (96, 24), (128, 16), (256, 16)}. */
+int sfx_window_attention_proj(int num_windows, int window, int heads, int head_dim, int channels, const float* qkv,
+                              const int* order, const int* win, float scale, const unsigned long long* qkv_amax,
+                              unsigned qkv_tag, const float* w_split, const float* w_inv, const float* bias,
+                              const float* x1, long long ldx1, float* x2, long long ldx2, void* stream);
 
 /* Point.serialization: codes[R][n] = batch << 3*depth | enc_t(grid) for order types t0..t3 (0 z, 1 z-trans,
  * 2 hilbert, 3 hilbert-trans) and combined sort keys r << code_bits | code; finalize turns the argsort of

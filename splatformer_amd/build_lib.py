@@ -9,6 +9,7 @@ from __future__ import annotations
 import concurrent.futures as cf
 import glob
 import os
+import re
 import subprocess
 import sys
 
@@ -33,9 +34,24 @@ CFLAGS = [
 ]
 
 
-def _headers_mtime() -> float:
-    hs = glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(ROOT, "include", "*.h"))
-    return max((os.path.getmtime(h) for h in hs), default=0.0)
+_INC = re.compile(r'^\s*#\s*include\s*"([^"]+)"', re.M)
+
+
+def _deps_mtime(path: str, seen=None) -> float:
+    """Newest mtime of `path` and of the in-tree headers it includes (transitively): an object is rebuilt only when
+    one of ITS sources changed, not on every header edit (the gfx950 compile of the larger kernels takes minutes)."""
+    seen = set() if seen is None else seen
+    if path in seen or not os.path.exists(path):
+        return 0.0
+    seen.add(path)
+    t = os.path.getmtime(path)
+    for inc in _INC.findall(open(path, errors="ignore").read()):
+        for d in (os.path.dirname(path), CSRC, os.path.join(ROOT, "include")):
+            cand = os.path.join(d, inc)
+            if os.path.exists(cand):
+                t = max(t, _deps_mtime(cand, seen))
+                break
+    return t
 
 
 def _flags_stamp() -> float:
@@ -49,9 +65,9 @@ def _flags_stamp() -> float:
     return os.path.getmtime(stamp)
 
 
-def _compile(src: str, hdr_mtime: float) -> str:
+def _compile(src: str, flags_mtime: float) -> str:
     obj = os.path.join(BUILD, os.path.basename(src).replace(".hip", ".o"))
-    if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(src), hdr_mtime):
+    if os.path.exists(obj) and os.path.getmtime(obj) >= max(_deps_mtime(src), flags_mtime):
         return obj
     cmd = [HIPCC, *CFLAGS, "-c", src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
@@ -63,7 +79,7 @@ def _compile(src: str, hdr_mtime: float) -> str:
 def build(verbose: bool = False, jobs: int | None = None) -> str:
     os.makedirs(BUILD, exist_ok=True)
     srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
-    hm = max(_headers_mtime(), _flags_stamp())
+    hm = _flags_stamp()
     jobs = jobs or min(8, len(srcs))
     with cf.ThreadPoolExecutor(jobs) as ex:
         objs = list(ex.map(lambda s: _compile(s, hm), srcs))

@@ -173,6 +173,11 @@ class Block(nn.Module):
                                             qkv_amax=q_amax)
         else:
             K, win, nw = point_windows(point, self.attn.patch_size_max)
+            if ops.window_attention_proj_ok(C, self.attn.num_heads):
+                # attention + proj + residual in one launch: the attention output never reaches HBM (attn_proj.hip)
+                x2 = ops.window_attention_proj(qkv, point.order_phys[oi], win, nw, K, self.attn.num_heads, C,
+                                               self.attn.proj, x1, q_amax)
+                return self._mlp_tail(point, x2, out, rowexp=fused)
             a = ops.window_attention(qkv, point.order_phys[oi], win, nw, K, self.attn.num_heads, C, qkv_amax=q_amax)
         x2 = ops.linear(a, self.attn.proj.weight, self.attn.proj.bias, residual=x1)
         return self._mlp_tail(point, x2, out, rowexp=fused)

@@ -28,6 +28,7 @@ _lib.register("sfx_cpe_residual_ln", [I, I, P, P, P, P, P, P, F, P, P, P])
 _lib.register("sfx_cpe_residual_ln_pairs", [I, I, P, P, P, L, P, P, P, P, P, F, P, P, P])
 _lib.register("sfx_window_attention", [I, I, I, I, I, P, P, P, F, P, P, I, P])
 _lib.register("sfx_window_attention_varlen", [I, I, I, I, I, P, P, P, F, P, P, I, P])
+_lib.register("sfx_window_attention_proj", [I, I, I, I, I, P, P, P, F, P, I, P, P, P, P, L, P, L, P])
 _lib.register("sfx_serialize_keys", [I, P, P, I, I, I, I, I, I, I, P, P, P])
 _lib.register("sfx_serialize_finalize", [I, I, P, P, P, P])
 _lib.register("sfx_serialize_permute", [I, I, P, P, P, P, P, P, P, P, P, P, P])
@@ -526,6 +527,39 @@ def window_attention(qkv: Tensor, order: Tensor, win: Tensor, num_windows: int, 
         out = torch.empty(n, channels, device=qkv.device, dtype=torch.float32)
     call("sfx_window_attention", num_windows, K, heads, d, channels, ptr(qkv), ptr(order, torch.int32),
          ptr(win, torch.int32), float(d ** -0.5), ptr(out), *_slot_args(qkv_amax), stream())
+    return out
+
+
+# Fused attention + output projection + residual (csrc/attn_proj.hip, ABI v15) on the eval path for these
+# (channels, head_dim); SFX_ATTN_PROJ=0 restores the attention launch + projection GEMM
+ATTN_PROJ = os.environ.get("SFX_ATTN_PROJ", "1") != "0"
+_ATTN_PROJ_SHAPES = {(64, 32), (96, 24), (128, 16), (256, 16)}
+
+
+def window_attention_proj_ok(channels: int, heads: int) -> bool:
+    return ATTN_PROJ and get_precision() == "fp32" and (channels, channels // heads) in _ATTN_PROJ_SHAPES
+
+
+def window_attention_proj(qkv: Tensor, order: Tensor, win: Tensor, num_windows: int, K: int, heads: int,
+                          channels: int, proj: "torch.nn.Linear", x1: Tensor, qkv_amax: Tuple[int, int],
+                          out: Optional[Tensor] = None) -> Tensor:
+    """x1 + proj(window_attention(qkv)) in one launch (the per-head outputs stay on chip, csrc/attn_proj.hip):
+    SerializedAttention's attention + proj and the Block's residual add (calflops.py:51-69).  fp16x2 MFMA terms
+    (q / k / v / O scaled from the qkv amax slot, the projection weight from its cached pre-split)."""
+    n = qkv.shape[0]
+    d = channels // heads
+    if qkv.shape != (n, 3 * channels) or order.shape[0] != n or x1.shape != (n, channels):
+        raise ValueError(f"window_attention_proj: shapes qkv {tuple(qkv.shape)} order {tuple(order.shape)} "
+                         f"x1 {tuple(x1.shape)} for C={channels}")
+    wsp, winv = weight_split(proj.weight)
+    if wsp is None:
+        raise RuntimeError("window_attention_proj: the projection weight has no fp16x2 pre-split")
+    if out is None:
+        out = torch.empty(n, channels, device=qkv.device, dtype=torch.float32)
+    px, ldx = _rows(x1)
+    po, ldo = _rows(out)
+    call("sfx_window_attention_proj", num_windows, K, heads, d, channels, ptr(qkv), ptr(order, torch.int32),
+         ptr(win, torch.int32), float(d ** -0.5), *qkv_amax, wsp, winv, ptr(proj.bias), px, ldx, po, ldo, stream())
     return out
 
 

@@ -466,6 +466,46 @@ def test_window_attention_vs_reference_padding(device, n, heads, C, terms):
     assert rel_l2(out.cpu(), ref) < 2e-6
 
 
+@pytest.mark.parametrize("n,heads,C", [(1000, 2, 64), (777, 4, 96), (300, 8, 128), (3000, 16, 256), (100, 16, 256),
+                                       (129, 4, 96), (37_759, 16, 256), (100_000, 2, 64)])
+def test_window_attention_proj(device, n, heads, C):
+    """Fused attention + proj + residual (attn_proj.hip: x2 = x1 + proj(attn(qkv)), calflops.py:51-69) vs the fp64
+    reference of the Pointcept padding semantics (as test_window_attention_vs_reference_padding) followed by the
+    Linear and the residual add: ragged last windows, K = n < 128, a window of 129 points, the config-B stage
+    shapes; fp16x2 terms from an 8x loose qkv bound.  Also within fp32 rounding of the unfused HIP path."""
+    g = torch.Generator().manual_seed(n + C)
+    qkv = torch.randn(n, 3 * C, generator=g) * 0.5
+    x1 = torch.randn(n, C, generator=g)
+    lin = torch.nn.Linear(C, C)
+    with torch.no_grad():
+        lin.weight.copy_(torch.randn(C, C, generator=g) * C ** -0.5)
+        lin.bias.copy_(torch.randn(C, generator=g) * 0.1)
+    order = torch.randperm(n, generator=g)
+    inverse = torch.empty_like(order)
+    inverse[order] = torch.arange(n)
+    K = min(n, 128)
+    pad, unpad = ptv3_ref.get_padding_and_inverse(torch.tensor([n]), K)
+    q, k, v = qkv.double()[order[pad]].reshape(-1, K, 3, heads, C // heads).permute(2, 0, 3, 1, 4).unbind(0)
+    att = torch.softmax((q * (C // heads) ** -0.5) @ k.transpose(-2, -1), -1)
+    a = (att @ v).transpose(1, 2).reshape(-1, C)[unpad[inverse]]
+    ref = x1.double() + a @ lin.weight.double().T + lin.bias.double()
+    tab = ops.window_table([n], K)
+    win = torch.tensor(tab, dtype=torch.int32).to(device)
+    qd, od = qkv.to(device), order.int().to(device)
+    lin = lin.to(device)
+    slot = ops.new_amax(qd.device)
+    big = qd * 8
+    from splatformer_amd._lib import call, ptr, stream
+    call("sfx_amax_f32", n, 3 * C, ptr(big), 3 * C, slot[0], slot[1], stream())
+    x2 = ops.window_attention_proj(qd, od, win, len(tab), K, heads, C, lin, x1.to(device), slot)
+    e = rel_l2(x2.cpu().double() - x1.double(), ref - x1.double())
+    unf = ops.linear(ops.window_attention(qd, od, win, len(tab), K, heads, C, qkv_amax=slot), lin.weight, lin.bias,
+                     residual=x1.to(device))
+    e_unf = rel_l2(unf.cpu().double() - x1.double(), ref - x1.double())
+    print(f"\n[attn+proj n={n} C={C}] branch rel L2 vs fp64: fused {e:.2e}, unfused {e_unf:.2e}")
+    assert e < 2e-6 and e <= 2 * e_unf + 1e-7
+
+
 @pytest.mark.parametrize("n,heads,C", [(100_000, 2, 64), (90_434, 4, 96), (37_759, 16, 256), (14_764, 32, 512),
                                        (3000, 4, 96), (77, 2, 64)])
 def test_window_attention_seq_bitwise(device, n, heads, C, monkeypatch):
