@@ -44,30 +44,41 @@ __device__ __forceinline__ floatx16 mfma16(const f16x8& a, const f16x8& b, float
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
 }
 
+// LDS-DMA piece: 16 B per lane from its own global address to M0 + 16 lane (inline asm, as subm_fused.hip: the
+// builtin makes the compiler drain vmcnt whenever an address register is reused; here every wait is ours)
+__device__ __forceinline__ void dma16(const void* gsrc, unsigned lds_dst) {
+  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gsrc), "s"(lds_dst) : "memory", "m0");
+}
+__device__ __forceinline__ void wait_vm0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// Raw staging layout of a [rows][P] array of 16-byte pieces (a head's K or V slice: rows = keys, P = D / 4 float4;
+// the projection slice: rows = couts, P = D / 4 pre-split groups): piece (r, p) at slot (r >> 4) 16 P + 16 p + (r & 15).
+// One DMA instruction (64 consecutive slots) then reads 16 rows x P pieces -- P * 16-byte contiguous segments per
+// row -- and a fragment read (32 consecutive rows, one piece) touches consecutive 16-byte slots: conflict-free.
+template <int P>
+__device__ __forceinline__ int raw_slot(int r, int p) { return (r >> 4) * (16 * P) + 16 * p + (r & 15); }
+
 template <int D, int C, int NWV>
-__global__ void __launch_bounds__(NWV * 64, 8 / NWV)
+__global__ void __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
 attn_proj_kernel(const float* __restrict__ qkv, const int* __restrict__ order, const int* __restrict__ win, int Kwin,
                  float scale, const unsigned long long* __restrict__ qkv_amax, unsigned qkv_tag,
                  const uint4* __restrict__ wsp, const float* __restrict__ winv, const float* __restrict__ bias,
                  const float* __restrict__ x1, long long ldx1, float* __restrict__ x2, long long ldx2, int nwin) {
   constexpr int H = C / D;
-  constexpr int KD = D == 16 ? 16 : 32;  // K image / q fragment depth (S^T contraction, zero past D)
-  constexpr int NKS = KD / 16;
-  constexpr int QROW = KD == 16 ? 48 : 64;  // bytes per K term row
-  constexpr int VST = 136;                  // V^T row stride (16-bit elements)
-  constexpr int KB = 2 * KMAX * QROW;
+  constexpr int NKS = (D + 15) / 16;  // 16-deep k-steps over a head's dd (S^T contraction and projection)
+  constexpr int CH = D / 4;           // 16-byte pieces per head row slice (fp32 q / k / v, pre-split Wp groups)
+  constexpr int VST = 136;            // V^T row stride (16-bit elements)
   constexpr int VB = 2 * D * VST * 2;
-  constexpr int NKP = (D + 15) / 16;  // projection k-steps over the head's dd
-  constexpr int WROW = NKP * 32;      // Wp image bytes per cout row and term (NKP steps x 2 lane halves x 16 B)
-  constexpr int WB = 2 * C * WROW;
-  constexpr int NCB = C / 32;         // 32-cout accumulator blocks
+  constexpr int KRAW = KMAX * CH * 16, WRAW = C * CH * 16;
+  constexpr int RAW = 2 * KRAW + WRAW;  // one head's raw K, V and Wp slices
+  constexpr int NBUF = 2 * RAW + VB <= 79 * 1024 ? 2 : 1;  // (two workgroups per CU)
+  constexpr int NCB = C / 32;
   constexpr int NT = NWV * 64;
-  constexpr int QPW = NWV * 32;       // queries per workgroup
-  constexpr int QS = KMAX / QPW;      // workgroups per window
-  constexpr int CH = D / 4;           // float4 per head row slice
-  static_assert(C % 32 == 0 && C % D == 0, "shape");
+  constexpr int QPW = NWV * 32;
+  constexpr int QS = KMAX / QPW;
+  constexpr int KPIECES = KMAX * CH / 64, WPIECES = C * CH / 64;  // DMA instructions per slice
+  static_assert(C % 32 == 0 && C % D == 0 && (KMAX * CH) % 64 == 0 && (C * CH) % 64 == 0, "shape");
 
-  // operand scales: qkv (and O) by sq, probabilities by 2^14
   float sq = 1.f, iq = 1.f;
   {
     const float m = sfx::read_amax(qkv_amax, qkv_tag);
@@ -81,59 +92,103 @@ attn_proj_kernel(const float* __restrict__ qkv, const int* __restrict__ order, c
     iq = ldexpf(1.f, -e);
   }
 
-  __shared__ __attribute__((aligned(16))) char lds[KB + VB + WB];
+  __shared__ __attribute__((aligned(16))) char lds[NBUF * RAW + VB];
   __shared__ int rows[KMAX];
-  char* Ks = lds;
-  unsigned short* Vt = reinterpret_cast<unsigned short*>(lds + KB);
-  char* Ws = lds + KB + VB;
-  auto qk_off = [](int r, int c) -> int {
-    return KD == 16 ? r * 48 + c * 16 : r * 64 + (((c ^ (r >> 2)) & 3) << 4);
-  };
+  unsigned short* Vt = reinterpret_cast<unsigned short*>(lds + NBUF * RAW);
+  const unsigned lds_base = (unsigned)(uintptr_t)lds;
 
-  // XCD-aware numbering (as window_attn_split_kernel): the QS workgroups of a window run back to back on one XCD
   const int nb = (int)gridDim.x;
   const int L = (int)(blockIdx.x % 8) * (nb / 8) + (int)(blockIdx.x / 8);
   if (L >= nwin * QS) return;
   const int w = L / QS, qh = L - w * QS;
   const int key_start = win[2 * w], query_start = win[2 * w + 1];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, h = lane >> 5, l32 = lane & 31;
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // (scalar: the DMA destinations go to M0)
   const long long ld = 3ll * C;
 
+  // padding keys (Kwin < 128) read row 0's slices: finite values whose probability is exactly 0
   for (int r = tid; r < KMAX; r += NT) rows[r] = r < Kwin ? order[key_start + r] : -1;
-  if (D < KD)  // K columns D..KD-1: zero once, the per-head staging never writes them
-    for (int rr = tid; rr < 2 * KMAX; rr += NT) *reinterpret_cast<uint4*>(Ks + qk_off(rr, D / 8)) = make_uint4(0, 0, 0, 0);
   __syncthreads();
 
-  const int qi = QPW * qh + 32 * wid + l32;  // this lane's query (window position)
+  // ---- head hd's raw K / V / Wp slices -> raw buffer `buf` by LDS-DMA (no registers held) ----
+  auto issue = [&](int hd, int buf) {
+    const unsigned base = lds_base + (unsigned)(buf * RAW);
+#pragma unroll
+    for (int i = wid; i < 2 * KPIECES; i += NWV) {  // K then V: slot i * 64 + lane of the [128][CH] piece array
+      const int kv = i >= KPIECES, ii = kv ? i - KPIECES : i;
+      const int sl = ii * 64 + lane;
+      const int blk = sl / (16 * CH), rem = sl - blk * 16 * CH;
+      const int p = rem >> 4, r = blk * 16 + (rem & 15);
+      const int src = max(rows[r], 0);
+      dma16(qkv + (long long)src * ld + (kv ? 2 * C : C) + hd * D + 4 * p,
+            __builtin_amdgcn_readfirstlane(base + (unsigned)(kv * KRAW + ii * 1024)));
+    }
+#pragma unroll
+    for (int i = wid; i < WPIECES; i += NWV) {  // Wp_h: [C couts][CH groups] of the pre-split
+      const int sl = i * 64 + lane;
+      const int blk = sl / (16 * CH), rem = sl - blk * 16 * CH;
+      const int p = rem >> 4, n = blk * 16 + (rem & 15);
+      dma16(wsp + (long long)n * (C / 4) + hd * CH + p,
+            __builtin_amdgcn_readfirstlane(base + (unsigned)(2 * KRAW + i * 1024)));
+    }
+  };
+  // ---- this lane's query slice of head hd (B operand of S^T = K Q^T): dd = 16 ks + 8 h + j, zero past D ----
+  const int qi = QPW * qh + 32 * wid + l32;
   const int qrow = rows[qi];
+  const float qs = scale * 1.4426950408889634f;  // scale * log2(e): the exponentials are plain exp2
+  float4 qa[NKS], qb[NKS];
+  auto load_q = [&](int hd) {
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      const int d0 = 16 * ks + 8 * h;
+      qa[ks] = make_float4(0.f, 0.f, 0.f, 0.f);
+      qb[ks] = qa[ks];
+      if (qrow >= 0 && d0 < D) {
+        const float* qp = qkv + (long long)qrow * ld + hd * D + d0;
+        qa[ks] = *reinterpret_cast<const float4*>(qp);
+        if (d0 + 4 < D) qb[ks] = *reinterpret_cast<const float4*>(qp + 4);
+      }
+    }
+  };
+
   floatx16 y[NCB];
 #pragma unroll
   for (int b = 0; b < NCB; ++b)
 #pragma unroll
     for (int r = 0; r < 16; ++r) y[b][r] = 0.f;
 
+  issue(0, 0);
+  load_q(0);
+  wait_vm0();
+  __syncthreads();
+
 #pragma unroll 1
   for (int hd = 0; hd < H; ++hd) {
-    if (hd) __syncthreads();  // every wave is done reading the previous head's images
-    // ---- stage K_h [key][dd], V_h^T [dd][key] and Wp_h [cout][dd] (fp16x2 terms) ----
-    for (int e = tid; e < KMAX * CH; e += NT) {
-      const int row = e / CH, ch = e - row * CH;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      const int src = rows[row];
-      if (src >= 0) v = *reinterpret_cast<const float4*>(qkv + (long long)src * ld + C + hd * D + 4 * ch);
-      uint2 t[2];
-      sfx::split2h(v, sq, t);
-      const int o = qk_off(row, ch >> 1) + ((ch & 1) << 3);
-      *reinterpret_cast<uint2*>(Ks + o) = t[0];
-      *reinterpret_cast<uint2*>(Ks + KMAX * QROW + o) = t[1];
+    const int buf = NBUF == 2 ? (hd & 1) : 0;
+    const char* raw = lds + buf * RAW;
+    // q fragments of this head (loaded one head ahead)
+    f16x8 qf[NKS][2];
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      float4 a = qa[ks], b = qb[ks];
+      a.x *= qs; a.y *= qs; a.z *= qs; a.w *= qs;
+      b.x *= qs; b.y *= qs; b.z *= qs; b.w *= qs;
+      uint2 ta[2], tb[2];
+      sfx::split2h(a, sq, ta);  // (|q * qs| <= |q|: the qkv bound holds)
+      sfx::split2h(b, sq, tb);
+#pragma unroll
+      for (int q = 0; q < 2; ++q) qf[ks][q] = __builtin_bit_cast(f16x8, (uintx4){ta[q].x, ta[q].y, tb[q].x, tb[q].y});
     }
+    if (NBUF == 2 && hd + 1 < H) {  // the next head's slices fly while this one computes
+      issue(hd + 1, buf ^ 1);
+      load_q(hd + 1);
+    }
+    // V^T image of this head from the raw V slice (key pairs x float4: whole-dword transposed stores)
     for (int e = tid; e < (KMAX / 2) * CH; e += NT) {
       const int kp = e / CH, ch = e - kp * CH;
       const int row = 2 * kp;
-      const int s0 = rows[row], s1 = rows[row + 1];
-      float4 v0 = make_float4(0.f, 0.f, 0.f, 0.f), v1 = v0;
-      if (s0 >= 0) v0 = *reinterpret_cast<const float4*>(qkv + (long long)s0 * ld + 2 * C + hd * D + 4 * ch);
-      if (s1 >= 0) v1 = *reinterpret_cast<const float4*>(qkv + (long long)s1 * ld + 2 * C + hd * D + 4 * ch);
+      const float4 v0 = *reinterpret_cast<const float4*>(raw + KRAW + 16 * raw_slot<CH>(row, ch));
+      const float4 v1 = *reinterpret_cast<const float4*>(raw + KRAW + 16 * raw_slot<CH>(row + 1, ch));
       uint2 t0[2], t1[2];
       sfx::split2h(v0, sq, t0);
       sfx::split2h(v1, sq, t1);
@@ -148,138 +203,128 @@ attn_proj_kernel(const float* __restrict__ qkv, const int* __restrict__ order, c
         vt[3 * VST / 2] = (t0[q].y >> 16) | (t1[q].y & 0xffff0000u);
       }
     }
-    // Wp_h: chunk c = 2 s + half of cout row n holds the dd of k-step s, lane half `half` in the MFMA's permuted
-    // order: 4-element groups g0 = 4 s + half (dd 16 s + 4 half ..) and g1 = g0 + 2 (dd 16 s + 8 + 4 half ..); a group
-    // of the pre-split is 16 bytes (4 fp16 h terms, then 4 fp16 l terms); groups at dd >= D are zero
-    for (int e = tid; e < C * 2 * NKP; e += NT) {
-      const int n = e / (2 * NKP), c = e - n * (2 * NKP);
-      const int g0 = 4 * (c >> 1) + (c & 1), g1 = g0 + 2;
-      uint4 a = make_uint4(0, 0, 0, 0), b = a;
-      const uint4* wr = wsp + (long long)n * (C / 4) + hd * (D / 4);
-      if (4 * g0 < D) a = wr[g0];
-      if (4 * g1 < D) b = wr[g1];
-      *reinterpret_cast<uint4*>(Ws + n * WROW + c * 16) = make_uint4(a.x, a.y, b.x, b.y);
-      *reinterpret_cast<uint4*>(Ws + C * WROW + n * WROW + c * 16) = make_uint4(a.z, a.w, b.z, b.w);
-    }
-    // this lane's query slices (B operand of S^T = K Q^T): dd = 16 ks + 8 h + j, zero past D
-    f16x8 qf[NKS][2];
-#pragma unroll
-    for (int ks = 0; ks < NKS; ++ks) {
-      const int d0 = 16 * ks + 8 * h;
-      float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
-      if (qrow >= 0 && d0 < D) {
-        const float* qp = qkv + (long long)qrow * ld + hd * D + d0;
-        a = *reinterpret_cast<const float4*>(qp);
-        if (d0 + 4 < D) b = *reinterpret_cast<const float4*>(qp + 4);
-      }
-      const float qs = scale * 1.4426950408889634f;  // scale * log2(e): the exponentials are plain exp2
-      a.x *= qs; a.y *= qs; a.z *= qs; a.w *= qs;
-      b.x *= qs; b.y *= qs; b.z *= qs; b.w *= qs;
-      uint2 ta[2], tb[2];
-      sfx::split2h(a, sq, ta);
-      sfx::split2h(b, sq, tb);
-#pragma unroll
-      for (int q = 0; q < 2; ++q) qf[ks][q] = __builtin_bit_cast(f16x8, (uintx4){ta[q].x, ta[q].y, tb[q].x, tb[q].y});
-    }
-    __syncthreads();
+    __syncthreads();  // V^T written
 
-    // ---- S^T[key][query] (4 key blocks of 32), three term products each, smallest first ----
-    floatx16 s[4];
-#pragma unroll
-    for (int kb = 0; kb < 4; ++kb)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) s[kb][r] = 0.f;
-#pragma unroll
-    for (int ks = 0; ks < NKS; ++ks)
-#pragma unroll
-      for (int kb = 0; kb < 4; ++kb) {
-        const int o = qk_off(kb * 32 + l32, 2 * ks + h);
-        const f16x8 kh = __builtin_bit_cast(f16x8, *reinterpret_cast<const uint4*>(Ks + o));
-        const f16x8 kl = __builtin_bit_cast(f16x8, *reinterpret_cast<const uint4*>(Ks + KMAX * QROW + o));
-        s[kb] = mfma16(kl, qf[ks][0], s[kb]);
-        s[kb] = mfma16(kh, qf[ks][1], s[kb]);
-        s[kb] = mfma16(kh, qf[ks][0], s[kb]);
-      }
+    // ---- S^T[key][query] -> softmax -> O^T[dd][query] = V^T P^T, in NPASS passes over the 128 keys (online
+    // softmax across passes: C = 256's 128 projection accumulators leave room for 64 score registers, not 128) ----
+    constexpr int NPASS = NCB >= 8 ? 2 : 1, KBP = 4 / NPASS;
     const float iqq = iq * iq;
-#pragma unroll
-    for (int kb = 0; kb < 4; ++kb)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) s[kb][r] *= iqq;
-    if (Kwin < KMAX) {
-#pragma unroll
-      for (int kb = 0; kb < 4; ++kb)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int key = kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-          if (key >= Kwin) s[kb][r] = -INFINITY;
-        }
-    }
-    float mx = -INFINITY;
-#pragma unroll
-    for (int kb = 0; kb < 4; ++kb)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[kb][r]);
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    float sum = 0.f;
-#pragma unroll
-    for (int kb = 0; kb < 4; ++kb)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float ex = __builtin_amdgcn_exp2f(s[kb][r] - mx);
-        s[kb][r] = ex;
-        sum += ex;
-      }
-    sum += __shfl_xor(sum, 32, 64);
-    const float rinv = 1.f / sum;
-
-    // ---- O^T[dd][query] = V^T P^T (P^T from the softmax registers, scaled by 2^14) ----
+    float mx = -INFINITY, sum = 0.f;
     floatx16 o;
 #pragma unroll
     for (int r = 0; r < 16; ++r) o[r] = 0.f;
 #pragma unroll
-    for (int kb = 0; kb < 4; ++kb)
+    for (int ps = 0; ps < NPASS; ++ps) {
+      floatx16 s[KBP];
 #pragma unroll
-      for (int st = 0; st < 2; ++st) {
-        uint2 a[2], b[2];
-        sfx::split2h(make_float4(s[kb][8 * st + 0], s[kb][8 * st + 1], s[kb][8 * st + 2], s[kb][8 * st + 3]), 16384.f, a);
-        sfx::split2h(make_float4(s[kb][8 * st + 4], s[kb][8 * st + 5], s[kb][8 * st + 6], s[kb][8 * st + 7]), 16384.f, b);
-        const f16x8 ph = __builtin_bit_cast(f16x8, make_uint4(a[0].x, a[0].y, b[0].x, b[0].y));
-        const f16x8 pl = __builtin_bit_cast(f16x8, make_uint4(a[1].x, a[1].y, b[1].x, b[1].y));
-        uint4 vh = make_uint4(0, 0, 0, 0), vl = vh;  // dd = l32 >= D: zero rows of V^T
-        if (l32 < D) {
-          const int co = ((2 * (2 * kb + st) + h) ^ vt_swz(l32)) << 3;
-          vh = *reinterpret_cast<const uint4*>(Vt + l32 * VST + co);
-          vl = *reinterpret_cast<const uint4*>(Vt + (D + l32) * VST + co);
+      for (int j = 0; j < KBP; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s[j][r] = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks)
+#pragma unroll
+        for (int j = 0; j < KBP; ++j) {  // K fragments split from the raw slice as they are read
+          const int kb = ps * KBP + j, p0 = 4 * ks + 2 * h;
+          float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+          if (4 * p0 < D) {
+            a = *reinterpret_cast<const float4*>(raw + 16 * raw_slot<CH>(kb * 32 + l32, p0));
+            b = *reinterpret_cast<const float4*>(raw + 16 * raw_slot<CH>(kb * 32 + l32, p0 + 1));
+          }
+          uint2 ta[2], tb[2];
+          sfx::split2h(a, sq, ta);
+          sfx::split2h(b, sq, tb);
+          const f16x8 kh = __builtin_bit_cast(f16x8, (uintx4){ta[0].x, ta[0].y, tb[0].x, tb[0].y});
+          const f16x8 kl = __builtin_bit_cast(f16x8, (uintx4){ta[1].x, ta[1].y, tb[1].x, tb[1].y});
+          s[j] = mfma16(kl, qf[ks][0], s[j]);
+          s[j] = mfma16(kh, qf[ks][1], s[j]);
+          s[j] = mfma16(kh, qf[ks][0], s[j]);
         }
-        const f16x8 fvh = __builtin_bit_cast(f16x8, vh), fvl = __builtin_bit_cast(f16x8, vl);
-        o = mfma16(fvl, ph, o);
-        o = mfma16(fvh, pl, o);
-        o = mfma16(fvh, ph, o);
-      }
-
-    // ---- Y^T[cout][query] += Wp_h O_h^T: O^T (true values x sq) split into fp16 terms, registers 8s..8s+7 as the
-    // B fragment of k-step s (rows dd >= D are zero: V^T rows past D fed zeros) ----
-    const float osc = rinv * (1.f / 16384.f);  // o = 2^14 sq sum_k p v  ->  O sq
-    f16x8 oh[NKP], ol[NKP];
+      float pm = -INFINITY;
 #pragma unroll
-    for (int sp = 0; sp < NKP; ++sp) {
+      for (int j = 0; j < KBP; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          float v = s[j][r] * iqq;
+          const int key = (ps * KBP + j) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          if (Kwin < KMAX && key >= Kwin) v = -INFINITY;
+          s[j][r] = v;
+          pm = fmaxf(pm, v);
+        }
+      pm = fmaxf(pm, __shfl_xor(pm, 32, 64));
+      const float mn = fmaxf(mx, pm);  // finite: every window has >= 1 key in pass 0
+      if (ps > 0) {
+        const float al = __builtin_amdgcn_exp2f(mx - mn);
+        sum *= al;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[r] *= al;
+      }
+      mx = mn;
+      float ps_sum = 0.f;
+#pragma unroll
+      for (int j = 0; j < KBP; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float ex = __builtin_amdgcn_exp2f(s[j][r] - mx);
+          s[j][r] = ex;
+          ps_sum += ex;
+        }
+      sum += ps_sum + __shfl_xor(ps_sum, 32, 64);
+#pragma unroll
+      for (int j = 0; j < KBP; ++j)
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+          const int kb = ps * KBP + j;
+          uint2 a[2], b[2];
+          sfx::split2h(make_float4(s[j][8 * st + 0], s[j][8 * st + 1], s[j][8 * st + 2], s[j][8 * st + 3]), 16384.f, a);
+          sfx::split2h(make_float4(s[j][8 * st + 4], s[j][8 * st + 5], s[j][8 * st + 6], s[j][8 * st + 7]), 16384.f, b);
+          const f16x8 ph = __builtin_bit_cast(f16x8, make_uint4(a[0].x, a[0].y, b[0].x, b[0].y));
+          const f16x8 pl = __builtin_bit_cast(f16x8, make_uint4(a[1].x, a[1].y, b[1].x, b[1].y));
+          uint4 vh = make_uint4(0, 0, 0, 0), vl = vh;  // dd = l32 >= D: zero rows of V^T
+          if (l32 < D) {
+            const int co = ((2 * (2 * kb + st) + h) ^ vt_swz(l32)) << 3;
+            vh = *reinterpret_cast<const uint4*>(Vt + l32 * VST + co);
+            vl = *reinterpret_cast<const uint4*>(Vt + (D + l32) * VST + co);
+          }
+          const f16x8 fvh = __builtin_bit_cast(f16x8, vh), fvl = __builtin_bit_cast(f16x8, vl);
+          o = mfma16(fvl, ph, o);
+          o = mfma16(fvh, pl, o);
+          o = mfma16(fvh, ph, o);
+        }
+    }
+    const float rinv = 1.f / sum;
+
+    // ---- Y^T[cout][query] += Wp_h O_h^T: O^T (x sq) as fp16 terms from registers 8s..8s+7 (k-step s, permuted
+    // order dd = 16 s + 8 (j >> 2) + 4 h + (j & 3): groups 4 s + h and 4 s + 2 + h of the pre-split Wp rows) ----
+    const float osc = rinv * (1.f / 16384.f);  // o = 2^14 sq sum_k p v  ->  O sq
+#pragma unroll
+    for (int sp = 0; sp < NKS; ++sp) {
       uint2 a[2], b[2];
       sfx::split2h(make_float4(o[8 * sp + 0], o[8 * sp + 1], o[8 * sp + 2], o[8 * sp + 3]), osc, a);
       sfx::split2h(make_float4(o[8 * sp + 4], o[8 * sp + 5], o[8 * sp + 6], o[8 * sp + 7]), osc, b);
-      oh[sp] = __builtin_bit_cast(f16x8, make_uint4(a[0].x, a[0].y, b[0].x, b[0].y));
-      ol[sp] = __builtin_bit_cast(f16x8, make_uint4(a[1].x, a[1].y, b[1].x, b[1].y));
-    }
+      const f16x8 oh = __builtin_bit_cast(f16x8, make_uint4(a[0].x, a[0].y, b[0].x, b[0].y));
+      const f16x8 ol = __builtin_bit_cast(f16x8, make_uint4(a[1].x, a[1].y, b[1].x, b[1].y));
+      const int g0 = 4 * sp + h, g1 = g0 + 2;
 #pragma unroll
-    for (int cb = 0; cb < NCB; ++cb)
-#pragma unroll
-      for (int sp = 0; sp < NKP; ++sp) {
-        const int wo = (cb * 32 + l32) * WROW + (2 * sp + h) * 16;
-        const f16x8 wh = __builtin_bit_cast(f16x8, *reinterpret_cast<const uint4*>(Ws + wo));
-        const f16x8 wl = __builtin_bit_cast(f16x8, *reinterpret_cast<const uint4*>(Ws + C * WROW + wo));
-        y[cb] = mfma16(wl, oh[sp], y[cb]);
-        y[cb] = mfma16(wh, ol[sp], y[cb]);
-        y[cb] = mfma16(wh, oh[sp], y[cb]);
+      for (int cb = 0; cb < NCB; ++cb) {
+        uint4 wa = make_uint4(0, 0, 0, 0), wb = wa;
+        if (4 * g0 < D) wa = *reinterpret_cast<const uint4*>(raw + 2 * KRAW + 16 * raw_slot<CH>(cb * 32 + l32, g0));
+        if (4 * g1 < D) wb = *reinterpret_cast<const uint4*>(raw + 2 * KRAW + 16 * raw_slot<CH>(cb * 32 + l32, g1));
+        const f16x8 wh = __builtin_bit_cast(f16x8, make_uint4(wa.x, wa.y, wb.x, wb.y));
+        const f16x8 wl = __builtin_bit_cast(f16x8, make_uint4(wa.z, wa.w, wb.z, wb.w));
+        y[cb] = mfma16(wl, oh, y[cb]);
+        y[cb] = mfma16(wh, ol, y[cb]);
+        y[cb] = mfma16(wh, oh, y[cb]);
       }
+    }
+    if (hd + 1 < H) {
+      if (NBUF == 1) {  // single raw buffer: fetch the next head only after every wave is done with this one
+        __syncthreads();
+        issue(hd + 1, 0);
+        load_q(hd + 1);
+      }
+      wait_vm0();       // this thread's DMAs (and q loads) of the next head have landed
+      __syncthreads();  // ... and everyone's: the next head's raw slices are visible, this head's reads are done
+    }
   }
 
   // ---- epilogue: x2 = Y / (s_w sq) + b + x1, lane = query, 4 consecutive couts per register group ----
@@ -324,7 +369,8 @@ int proj_waves(int nwin, int C) {
   }
   if (force == 2 || force == 4) return force;
   (void)C;
-  return nwin < 512 ? 2 : 4;
+  (void)nwin;
+  return 4;  // (the raw double buffer is per workgroup: half-window workgroups would stage every slice twice)
 }
 
 }  // namespace

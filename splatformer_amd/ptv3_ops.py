@@ -530,14 +530,21 @@ def window_attention(qkv: Tensor, order: Tensor, win: Tensor, num_windows: int, 
     return out
 
 
-# Fused attention + output projection + residual (csrc/attn_proj.hip, ABI v15) on the eval path for these
-# (channels, head_dim); SFX_ATTN_PROJ=0 restores the attention launch + projection GEMM
-ATTN_PROJ = os.environ.get("SFX_ATTN_PROJ", "1") != "0"
+# Fused attention + output projection + residual (csrc/attn_proj.hip, ABI v15) on the eval path.  Default on the
+# (channels, head_dim) where it measured faster than the attention launch + projection GEMM (config B, round 6:
+# C = 64: 51 vs 58 us, C = 96: 79 vs 89 us per Block); at C = 128 / 256 one workgroup per window keeps too few
+# head gathers in flight (92 vs ~80 us, 145 vs ~99 us: DESIGN.md §14).  SFX_ATTN_PROJ=0: never; =all: every
+# supported shape.
+_ATTN_PROJ_MODE = os.environ.get("SFX_ATTN_PROJ", "1")
 _ATTN_PROJ_SHAPES = {(64, 32), (96, 24), (128, 16), (256, 16)}
+_ATTN_PROJ_DEFAULT = {(64, 32), (96, 24)}
 
 
 def window_attention_proj_ok(channels: int, heads: int) -> bool:
-    return ATTN_PROJ and get_precision() == "fp32" and (channels, channels // heads) in _ATTN_PROJ_SHAPES
+    if _ATTN_PROJ_MODE == "0":
+        return False
+    shapes = _ATTN_PROJ_SHAPES if _ATTN_PROJ_MODE == "all" else _ATTN_PROJ_DEFAULT
+    return (channels, channels // heads) in shapes and get_precision() == "fp32"
 
 
 def window_attention_proj(qkv: Tensor, order: Tensor, win: Tensor, num_windows: int, K: int, heads: int,
