@@ -331,6 +331,11 @@ int sfx_serialize_finalize(int n, int num_orders, const int* sorted_pos, int* or
  * Then segment max (+BN affine +GELU) of the projected features and the mean of the coords. */
 int sfx_pool_run_flags(int n, int num_orders, const int* order, const int64_t* codes, int shift, int* flags,
                        void* stream);
+/* (ABI v15) counts[k] (k < nshift <= 8; host array `shifts`) = the number of runs of codes[order[j]] >> shifts[k]
+ * along ONE serialized row (order, codes: row 0's [n]) = the sum of sfx_pool_run_flags' flags for that shift: every
+ * pooling's cluster count from the stage-0 codes in one launch (plus a 4-byte memset) */
+int sfx_pool_run_counts(int n, const int* order, const int64_t* codes, const int* shifts, int nshift, int* counts,
+                        void* stream);
 int sfx_pool_assign_runs(int n, int m, int row0, const int* order, const int* pos, const int* flags, int* cluster,
                          int* idx_ptr, int* head, int* sorted_idx, void* stream);
 int sfx_pool_reorder(int n, int m, int num_orders, const int* order, const int* pos, const int* flags,

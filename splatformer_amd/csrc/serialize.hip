@@ -109,6 +109,36 @@ __global__ void pool_run_flags_kernel(int n, int R, const int* __restrict__ orde
   flags[q] = (j == 0 || c != ((uint64_t)cr[order[q - 1]] >> shift)) ? 1 : 0;
 }
 
+// Run counts of code >> shift_k along one serialized row for up to 8 shifts at once (every pooling's cluster count
+// from the stage-0 codes, PointTransformerV3.forward): counts[k] += the flags of pool_run_flags_kernel, summed per
+// wave by ballot + popcount and per workgroup in LDS, one integer atomic per (workgroup, shift) -- one launch
+// instead of a flag pass + scan per pooling (the count is a sum, not a prefix).
+struct RunShifts {
+  int s[8];
+};
+__global__ void __launch_bounds__(256) pool_run_counts_kernel(int n, const int* __restrict__ order,
+                                                              const int64_t* __restrict__ codes, RunShifts sh,
+                                                              int nshift, int* __restrict__ counts) {
+  __shared__ int part[8];
+  if (threadIdx.x < 8) part[threadIdx.x] = 0;
+  __syncthreads();
+  const long long j = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  uint64_t c = 0, p = 0;
+  if (j < n) {
+    c = (uint64_t)codes[order[j]];
+    if (j > 0) p = (uint64_t)codes[order[j - 1]];
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    if (k >= nshift) break;
+    const bool f = j < n && (j == 0 || (c >> sh.s[k]) != (p >> sh.s[k]));
+    const int cnt = __popcll(__ballot(f));
+    if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(&part[k], cnt);
+  }
+  __syncthreads();
+  if (threadIdx.x < nshift && part[threadIdx.x]) atomicAdd(counts + threadIdx.x, part[threadIdx.x]);
+}
+
 // row0's runs -> cluster id of every point, CSR of the members (sidx / idx_ptr), one head per cluster
 __global__ void pool_assign_runs_kernel(int n, int m, int row0, const int* __restrict__ order,
                                         const int* __restrict__ pos, const int* __restrict__ flags,
@@ -266,6 +296,25 @@ int sfx_pool_run_flags(int n, int num_orders, const int* order, const int64_t* c
   pool_run_flags_kernel<<<sfx::ceil_div(tot, 256), 256, 0, sfx::as_stream(stream)>>>(n, num_orders, order, codes,
                                                                                      shift, flags);
   return sfx::check_launch("sfx_pool_run_flags");
+}
+
+// (ABI v15) counts[k] = number of runs of codes[order[j]] >> shifts[k] along one serialized row (k < nshift <= 8)
+int sfx_pool_run_counts(int n, const int* order, const int64_t* codes, const int* shifts, int nshift, int* counts,
+                        void* stream) {
+  SFX_REQUIRE(n >= 0 && nshift >= 1 && nshift <= 8, "sfx_pool_run_counts: bad args");
+  SFX_REQUIRE(shifts && counts, "sfx_pool_run_counts: null buffer");
+  RunShifts sh{};
+  for (int k = 0; k < nshift; ++k) {
+    SFX_REQUIRE(shifts[k] >= 0 && shifts[k] < 64, "sfx_pool_run_counts: shift out of range");
+    sh.s[k] = shifts[k];
+  }
+  hipStream_t st = sfx::as_stream(stream);
+  if (hipMemsetAsync(counts, 0, sizeof(int) * (size_t)nshift, st) != hipSuccess)
+    return sfx::check_launch("sfx_pool_run_counts (zero)");
+  if (n == 0) return SFX_OK;
+  SFX_REQUIRE(order && codes, "sfx_pool_run_counts: null buffer");
+  pool_run_counts_kernel<<<sfx::ceil_div(n, 256), 256, 0, st>>>(n, order, codes, sh, nshift, counts);
+  return sfx::check_launch("sfx_pool_run_counts");
 }
 
 int sfx_pool_assign_runs(int n, int m, int row0, const int* order, const int* pos, const int* flags, int* cluster,

@@ -35,6 +35,9 @@ ORDERS = ("z", "z-trans", "hilbert", "hilbert-trans")
 POOL_COUNTS_UPFRONT = os.environ.get("SFX_POOL_COUNTS_UPFRONT", "1") != "0"
 
 
+# the stage-0 SubM map is enqueued before the host waits for the grid depth (SFX_NBR_EARLY=0: after the serialization)
+NBR_EARLY = os.environ.get("SFX_NBR_EARLY", "1") != "0"
+
 class Point(dict):
     """addict-style dict (Pointcept `Point`) with attribute access."""
 
@@ -416,6 +419,9 @@ class PointTransformerV3(nn.Module):
             batch = torch.empty(n, device=dev, dtype=torch.int32)
             offs = torch.tensor(offset, dtype=torch.int64, device=dev)
             _lib.call("sfx_offsets_to_batch", n, B, offs.data_ptr(), batch.data_ptr(), _lib.stream())
+        # the stage-0 neighbour map needs no serialization: enqueued before the depth read, it keeps the GPU busy
+        # while the host enqueues the serialization (the read drains the queue up to the grid max's copy)
+        nbr = None if (reorder or not NBR_EARLY) else ops.subm_neighbors(grid, batch, with_pairs=pairs)
         d = data_dict.get("serialized_depth")
         if isinstance(d, _lib.HostRead):  # the grid max, read back while the embedding runs
             depth = int(d.get()[0]).bit_length()
@@ -438,7 +444,7 @@ class PointTransformerV3(nn.Module):
             point.perm = perm
         if batch is not None:
             point.batch = batch
-        point.nbr = ops.subm_neighbors(grid, batch, with_pairs=pairs)
+        point.nbr = nbr if nbr is not None else ops.subm_neighbors(grid, batch, with_pairs=pairs)
         return point
 
     @torch.no_grad()

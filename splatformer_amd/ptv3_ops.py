@@ -33,6 +33,7 @@ _lib.register("sfx_serialize_keys", [I, P, P, I, I, I, I, I, I, I, P, P, P])
 _lib.register("sfx_serialize_finalize", [I, I, P, P, P, P])
 _lib.register("sfx_serialize_permute", [I, I, P, P, P, P, P, P, P, P, P, P, P])
 _lib.register("sfx_pool_run_flags", [I, I, P, P, I, P, P])
+_lib.register("sfx_pool_run_counts", [I, P, P, P, I, P, P])
 _lib.register("sfx_pool_assign_runs", [I, I, I, P, P, P, P, P, P, P, P])
 _lib.register("sfx_pool_reorder", [I, I, I, P, P, P, P, P, P, P])
 _lib.register("sfx_pool_gather", [I, I, I, P, P, I, P, P, I, P, P, P, P, P])
@@ -640,12 +641,11 @@ def pool_counts_begin(codes: Tensor, order: Tensor, shifts: Sequence[int]) -> "_
     k is the number of runs of code0 >> k along serialized row 0 -- one flag pass + scan per pooling, read back in
     one asynchronous copy.  The forward then never waits for a pooled count (pool_geometry_end(m=...))."""
     n = codes.shape[1]
-    counts = torch.zeros(max(len(shifts), 1), device=codes.device, dtype=torch.int32)
-    flags = torch.empty(n, device=codes.device, dtype=torch.int32)
-    for i, sh in enumerate(shifts):
-        call("sfx_pool_run_flags", n, 1, ptr(order[0], torch.int32), ptr(codes[0], torch.int64), sh, ptr(flags),
-             stream())
-        scan_i32(flags, total=counts[i:i + 1])
+    counts = torch.empty(max(len(shifts), 1), device=codes.device, dtype=torch.int32)
+    for k in range(0, len(shifts), 8):  # one launch for up to 8 poolings (sfx_pool_run_counts)
+        sh = list(shifts[k:k + 8])
+        call("sfx_pool_run_counts", n, ptr(order[0], torch.int32), ptr(codes[0], torch.int64),
+             ctypes.cast((ctypes.c_int * len(sh))(*sh), ctypes.c_void_p), len(sh), counts[k:].data_ptr(), stream())
     return _lib.HostRead(counts)
 
 

@@ -435,6 +435,22 @@ def test_pooling_geometry_exact(device, stride, B, perm, res):
     assert torch.allclose(new.coord.cpu().double(), mean, rtol=1e-6, atol=1e-7)
 
 
+@pytest.mark.parametrize("n", [1, 1000, 100_003])
+def test_pool_run_counts(device, n):
+    """sfx_pool_run_counts (every pooling's cluster count in one launch) == the run counts of code >> shift along
+    the serialized row, for 1..9 shifts (9: two launches)."""
+    g = torch.Generator().manual_seed(n)
+    codes = torch.randint(0, 1 << 40, (1, n), generator=g, dtype=torch.int64) >> torch.randint(0, 30, (1, n),
+                                                                                              generator=g)
+    order = torch.randperm(n, generator=g).int()
+    shifts = [0, 3, 6, 9, 12, 21, 27, 33, 39]
+    c = codes[0][order.long()]
+    ref = [int(1 + ((c[1:] >> s) != (c[:-1] >> s)).sum()) if n else 0 for s in shifts]
+    for k in (1, 4, 9):
+        got = ops.pool_counts_begin(codes.to(device), order[None].to(device), shifts[:k]).get()
+        assert got == ref[:k]
+
+
 @pytest.mark.parametrize("terms", ["bf16x3", "fp16x2"])
 @pytest.mark.parametrize("n,heads,C", [(1000, 2, 64), (777, 4, 96), (300, 8, 128), (100, 2, 32)])
 def test_window_attention_vs_reference_padding(device, n, heads, C, terms):
