@@ -26,6 +26,21 @@ __device__ __forceinline__ unsigned slot_of(unsigned long long key, int log2cap)
   return (unsigned)((key * 0x9E3779B97F4A7C15ull) >> (64 - log2cap));
 }
 
+// one launch for the table / mask initialisation (was 2-4 fills): keys EMPTY, vals 0x7f7f7f7f (atomicMin start),
+// masks 0
+__global__ void subm_init_kernel(long long cap, int n, unsigned long long* __restrict__ keys, int* __restrict__ vals,
+                                 unsigned* __restrict__ mask, unsigned long long* __restrict__ mask_keys) {
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < cap) {
+    keys[t] = EMPTY;
+    vals[t] = 0x7f7f7f7f;
+  }
+  if (t < n) {
+    if (mask) mask[t] = 0u;
+    if (mask_keys) mask_keys[t] = 0ull;
+  }
+}
+
 __global__ void subm_insert_kernel(int n, const int* __restrict__ grid, const int* __restrict__ batch,
                                    unsigned long long* __restrict__ keys, int* __restrict__ vals, int log2cap) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -144,11 +159,9 @@ int sfx_subm_neighbors(int n, const int* grid_coord, const int* batch, int log2c
   SFX_REQUIRE(grid_coord && table_keys && table_vals && nbr, "sfx_subm_neighbors: null buffer");
   hipStream_t st = sfx::as_stream(stream);
   const size_t cap = (size_t)1 << log2cap;
-  hipMemsetAsync(table_keys, 0xff, cap * sizeof(unsigned long long), st);
-  hipMemsetAsync(table_vals, 0x7f, cap * sizeof(int), st);
+  subm_init_kernel<<<sfx::ceil_div((long long)cap, 256), 256, 0, st>>>((long long)cap, n, table_keys, table_vals, mask,
+                                                                       mask_keys);  // (cap >= 2n)
   subm_insert_kernel<<<sfx::ceil_div(n, 256), 256, 0, st>>>(n, grid_coord, batch, table_keys, table_vals, log2cap);
-  if (mask) hipMemsetAsync(mask, 0, (size_t)n * sizeof(unsigned), st);
-  if (mask_keys) hipMemsetAsync(mask_keys, 0, (size_t)n * sizeof(unsigned long long), st);
   subm_query_kernel<<<sfx::ceil_div(27ll * n, 256), 256, 0, st>>>(n, grid_coord, batch, table_keys, table_vals,
                                                                   log2cap, nbr, mask, mask_keys);
   return sfx::check_launch("sfx_subm_neighbors");
