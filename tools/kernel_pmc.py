@@ -35,6 +35,7 @@ FAMILIES = [  # (family, kernel-name regex) -- first match wins
     ("fused output heads", r"^heads_kernel"),
     ("point embedding", r"^point_embed"),
     ("attention", r"^window_attn"),
+    ("attention + proj (fused)", r"^attn_proj_kernel"),
     ("rasterizer", r"^rasterize_fwd"),
     ("render prep/project + records", r"^render_prep_project|^pack_raster_records|^isect_emit|^tile_bins"),
     ("radix sort + scans", r"^radix_|^scan_"),
