@@ -276,8 +276,10 @@ int sfx_cpe_residual_ln(int M, int C, const float* T, const float* X, const floa
                         const float* gamma1, const float* beta1, float eps, float* X_out, float* H, void* stream);
 /* (ABI v6) the same with T = the centre output of sfx_subm_conv_partials plus, per row, the SubM pair partials
  * partials[pair_pos[row][k]] summed in ascending offset order k (pair_pos: sfx_subm_pair_pos; -1 entries skipped):
- * the conv without float atomics, bitwise reproducible.  C in {64, 96, 128, 256, 512}, 16-byte aligned rows. */
-int sfx_cpe_residual_ln_pairs(int M, int C, const float* T, const float* partials, const int* pair_pos,
+ * the conv without float atomics, bitwise reproducible.  C in {64, 96, 128, 256, 512}, 16-byte aligned rows.
+ * (ABI v15) ldt = T's row stride: C, or 0 when T is the conv bias [C] alone and the pair lists carry the centre
+ * offset (sfx_subm_pairs with_centre = 1: the centre's products are partial rows too, added at k = 13). */
+int sfx_cpe_residual_ln_pairs(int M, int C, const float* T, long long ldt, const float* partials, const int* pair_pos,
                               long long num_pairs, const float* X, const float* gamma_cpe, const float* beta_cpe,
                               const float* gamma1, const float* beta1, float eps, float* X_out, float* H,
                               void* stream);
@@ -359,12 +361,16 @@ int sfx_subm_neighbors(int n, const int* grid_coord, const int* batch, int log2c
 int sfx_subm_permute(int n, const int* perm, const int* nbr, const unsigned* mask, int* nbr_sorted,
                      unsigned* mask_sorted, void* stream);
 /* Offset-major indice pairs (centre offset excluded, output rows ascending within an offset):
- * pair_in/pair_out [<= 26 n], pair_off[28] (device) = per-offset prefix of the pair counts. */
+ * pair_in/pair_out [<= 26 n], pair_off[28] (device) = per-offset prefix of the pair counts.
+ * (ABI v15) with_centre = 1: the centre offset k = 13 is listed too ([<= 27 n] entries) -- the eval conv then runs
+ * as ONE pair launch (sfx_subm_conv_partials_pairs) whose centre products are partial rows like the others
+ * (summed by sfx_cpe_residual_ln_pairs with ldt = 0); sfx_subm_conv / sfx_subm_conv_bwd_data take lists without it. */
 size_t sfx_subm_pairs_workspace_bytes(int n);
 int sfx_subm_pairs(int n, const int* nbr, void* ws, size_t ws_bytes, int* pair_in, int* pair_out, int* pair_off,
-                   void* stream);
+                   int with_centre, void* stream);
 /* (ABI v6) inverted pair index: pair_pos[i][k] = index of pair (k, out = i) in pair_in/pair_out, -1 if none
- * (always -1 for the centre k = 13); pair_off = the device pair_off of sfx_subm_pairs, num_pairs = pair_off[27]. */
+ * (always -1 for the centre k = 13 unless the lists carry it); pair_off = the device pair_off of sfx_subm_pairs,
+ * num_pairs = pair_off[27]. */
 int sfx_subm_pair_pos(int n, long long num_pairs, const int* pair_out, const int* pair_off, int* pair_pos,
                       void* stream);
 /* spconv SubMConv3d(Cin, Cout, 3, bias) forward on the pair lists: out = bias + x[nbr[:,13]] W_13^T (dense centre

@@ -155,8 +155,7 @@ __device__ __forceinline__ void add_pair_partials(float4 (&v)[NV], const float* 
 #pragma unroll
   for (int k = 0; k < 27; ++k) q[k] = pos[27ll * row + k];
 #pragma unroll
-  for (int k = 0; k < 27; ++k) {
-    if (k == 13) continue;
+  for (int k = 0; k < 27; ++k) {  // (k = 13: the centre's row when the pair lists carry it, else -1: adds 0)
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const unsigned off = q[k] >= 0 ? ((unsigned)q[k] * (unsigned)C + 4u * (unsigned)(sub + G * i)) * 4u : 0x7ffffff0u;
@@ -167,7 +166,7 @@ __device__ __forceinline__ void add_pair_partials(float4 (&v)[NV], const float* 
 }
 
 template <int G, int NV, bool PAIRS>
-__global__ void __launch_bounds__(256) cpe_residual_ln4_kernel(int M, const float* __restrict__ T,
+__global__ void __launch_bounds__(256) cpe_residual_ln4_kernel(int M, const float* __restrict__ T, long long ldt,
                                                                const float* __restrict__ X,
                                                                const float* __restrict__ g_cpe,
                                                                const float* __restrict__ b_cpe,
@@ -184,7 +183,7 @@ __global__ void __launch_bounds__(256) cpe_residual_ln4_kernel(int M, const floa
   float4 v[NV], o[NV], x[NV];
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
-    v[i] = *reinterpret_cast<const float4*>(T + base + 4 * (sub + G * i));
+    v[i] = *reinterpret_cast<const float4*>(T + (long long)row * ldt + 4 * (sub + G * i));
     x[i] = *reinterpret_cast<const float4*>(X + base + 4 * (sub + G * i));
   }
   if constexpr (PAIRS) add_pair_partials<G, NV>(v, P, pos, row, sub);
@@ -255,7 +254,7 @@ int sfx_cpe_residual_ln(int M, int C, const float* T, const float* X, const floa
   const bool v4 = al16(T) && al16(X) && al16(X_out) && al16(H) && al16(gamma_cpe) && al16(beta_cpe) && al16(gamma1) &&
                   al16(beta1);
 #define SFX_CPE4(G, NV)                                                                                         \
-  cpe_residual_ln4_kernel<G, NV, false><<<sfx::ceil_div(M, 256 / G), 256, 0, st>>>(M, T, X, gamma_cpe, beta_cpe,   \
+  cpe_residual_ln4_kernel<G, NV, false><<<sfx::ceil_div(M, 256 / G), 256, 0, st>>>(M, T, C, X, gamma_cpe, beta_cpe,\
                                                                                    gamma1, beta1, eps, X_out, H,   \
                                                                                    nullptr, nullptr)
   if (v4 && C == 64) SFX_CPE4(16, 1);
@@ -270,11 +269,14 @@ int sfx_cpe_residual_ln(int M, int C, const float* T, const float* X, const floa
 }
 
 // sfx_cpe_residual_ln with T = the centre output of sfx_subm_conv_partials and the pair partials summed per row
-// in ascending offset order (pair_pos: sfx_subm_pair_pos; partials: [num_pairs][C], contiguous).
-int sfx_cpe_residual_ln_pairs(int M, int C, const float* T, const float* partials, const int* pair_pos,
+// in ascending offset order (pair_pos: sfx_subm_pair_pos; partials: [num_pairs][C], contiguous).  (ABI v15) ldt: T's
+// row stride -- C for a per-row centre output, 0 for the conv bias alone when the pair lists carry the centre
+// offset (sfx_subm_pairs with_centre: its products are partial rows like every other offset's, summed at k = 13).
+int sfx_cpe_residual_ln_pairs(int M, int C, const float* T, long long ldt, const float* partials, const int* pair_pos,
                               long long num_pairs, const float* X, const float* gamma_cpe, const float* beta_cpe,
                               const float* gamma1, const float* beta1, float eps, float* X_out, float* H,
                               void* stream) {
+  SFX_REQUIRE(ldt == 0 || ldt == C, "sfx_cpe_residual_ln_pairs: ldt must be C or 0");
   SFX_REQUIRE(M >= 0 && num_pairs >= 0, "sfx_cpe_residual_ln_pairs: bad sizes");
   if (M == 0) return SFX_OK;
   SFX_REQUIRE(T && X && gamma_cpe && beta_cpe && gamma1 && beta1 && X_out && H && pair_pos &&
@@ -287,7 +289,7 @@ int sfx_cpe_residual_ln_pairs(int M, int C, const float* T, const float* partial
               "sfx_cpe_residual_ln_pairs: needs 16-byte aligned rows and C in {64, 96, 128, 256, 512}");
   hipStream_t st = sfx::as_stream(stream);
 #define SFX_CPE4P(G, NV)                                                                                        \
-  cpe_residual_ln4_kernel<G, NV, true><<<sfx::ceil_div(M, 256 / G), 256, 0, st>>>(M, T, X, gamma_cpe, beta_cpe,   \
+  cpe_residual_ln4_kernel<G, NV, true><<<sfx::ceil_div(M, 256 / G), 256, 0, st>>>(M, T, ldt, X, gamma_cpe, beta_cpe,\
                                                                                   gamma1, beta1, eps, X_out, H,   \
                                                                                   partials, pair_pos)
   if (C == 64) SFX_CPE4P(16, 1);

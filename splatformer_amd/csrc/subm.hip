@@ -103,11 +103,12 @@ __global__ void subm_permute_kernel(int n, const int* __restrict__ perm, const i
 }
 
 // offset-major pair lists (spconv indice pairs, centre offset excluded): flags over [27][n]
-__global__ void subm_pair_flags_kernel(int n, const int* __restrict__ nbr, int* __restrict__ flags) {
+// (with_centre: the centre offset k = 13 is listed too -- the eval conv's single pair launch)
+__global__ void subm_pair_flags_kernel(int n, const int* __restrict__ nbr, int* __restrict__ flags, int with_centre) {
   const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= 27ll * n) return;
   const int k = (int)(t / n), i = (int)(t - (long long)k * n);
-  flags[t] = (k != 13 && nbr[27ll * i + k] >= 0) ? 1 : 0;
+  flags[t] = ((k != 13 || with_centre) && nbr[27ll * i + k] >= 0) ? 1 : 0;
 }
 
 __global__ void subm_pair_fill_kernel(int n, const int* __restrict__ nbr, const int* __restrict__ flags,
@@ -167,15 +168,15 @@ int sfx_subm_neighbors(int n, const int* grid_coord, const int* batch, int log2c
   return sfx::check_launch("sfx_subm_neighbors");
 }
 
-// pair lists for sfx_subm_conv: pair_in/pair_out hold up to 26*n entries; pair_off[28] (device) receives the
-// per-offset prefix (centre slice empty).  ws: 2 * 27 * n int32 + sfx_scan_workspace_bytes(27 * n).
+// pair lists for sfx_subm_conv: pair_in/pair_out hold up to 26*n entries (27*n with_centre); pair_off[28] (device)
+// receives the per-offset prefix (centre slice empty unless with_centre).  ws: 2 * 27 * n int32 + sfx_scan_workspace_bytes(27 * n).
 size_t sfx_subm_pairs_workspace_bytes(int n) {
   const long long e = 27ll * (n > 0 ? n : 1);
   return (size_t)(2 * e * sizeof(int) + 256) + sfx_scan_workspace_bytes(e);
 }
 
 int sfx_subm_pairs(int n, const int* nbr, void* ws, size_t ws_bytes, int* pair_in, int* pair_out, int* pair_off,
-                   void* stream) {
+                   int with_centre, void* stream) {
   SFX_REQUIRE(n >= 0, "sfx_subm_pairs: n < 0");
   SFX_REQUIRE(ws_bytes >= sfx_subm_pairs_workspace_bytes(n), "sfx_subm_pairs: workspace too small");
   SFX_REQUIRE(pair_off, "sfx_subm_pairs: null pair_off");
@@ -190,7 +191,7 @@ int sfx_subm_pairs(int n, const int* nbr, void* ws, size_t ws_bytes, int* pair_i
   int* pos = flags + e;
   char* scan_ws = reinterpret_cast<char*>(pos + e);
   scan_ws += (256 - (reinterpret_cast<uintptr_t>(scan_ws) & 255)) & 255;
-  subm_pair_flags_kernel<<<sfx::ceil_div(e, 256), 256, 0, st>>>(n, nbr, flags);
+  subm_pair_flags_kernel<<<sfx::ceil_div(e, 256), 256, 0, st>>>(n, nbr, flags, with_centre);
   int rc = sfx_scan_i32(e, flags, pos, 0, scan_ws, sfx_scan_workspace_bytes(e), pair_off + 27, stream);
   if (rc) return rc;
   subm_pair_fill_kernel<<<sfx::ceil_div(e, 256), 256, 0, st>>>(n, nbr, flags, pos, pair_in, pair_out, pair_off);

@@ -239,7 +239,7 @@ class SerializedPooling(nn.Module):
         return ops.pool_geometry_begin(point.codes_phys, point.order_phys, self._pd(point))
 
     def geometry_end(self, point: Point, perm: Sequence[int], state, m: Optional[int] = None,
-                     deferred: Optional[list] = None, pairs: bool = True):
+                     deferred: Optional[list] = None, pairs: bool = True, centre: bool = False):
         """The integer half of SerializedPooling.forward: clusters (code >> 3*pd, unique), their members
         (sidx / idx_ptr CSR), the pooled coords, codes, orders and neighbour map.  -> (new Point, sidx, idx_ptr, m)
         m: the cluster count when already known (PointTransformerV3.forward's pool_counts_begin)."""
@@ -258,18 +258,18 @@ class SerializedPooling(nn.Module):
             new.offset = torch.cumsum(torch.bincount(batch.long().cpu(), minlength=len(point.offset)), 0).tolist()
         else:
             new.offset = [m]
-        new.nbr = ops.subm_neighbors(grid, new.get("batch"), with_pairs=pairs)
+        new.nbr = ops.subm_neighbors(grid, new.get("batch"), with_pairs=pairs, centre=centre)
         return new, sidx, idx_ptr, m
 
     def geometry(self, point: Point, perm: Sequence[int]):
         return self.geometry_end(point, perm, self.geometry_begin(point))
 
     def run(self, point: Point, perm: Sequence[int], m: Optional[int] = None, deferred: Optional[list] = None,
-            pairs: bool = True) -> Point:
+            pairs: bool = True, centre: bool = False) -> Point:
         st = self.geometry_begin(point)
         # the projection does not depend on the clusters: enqueued while the host waits for the pooled count
         pf = ops.linear(point.feat, self.proj.weight, self.proj.bias)
-        new, sidx, idx_ptr, m = self.geometry_end(point, perm, st, m, deferred, pairs=pairs)
+        new, sidx, idx_ptr, m = self.geometry_end(point, perm, st, m, deferred, pairs=pairs, centre=centre)
         sc, sh = bn_affine(self.norm[0])
         new.feat = ops.segment_max_affine_act(pf, idx_ptr, sidx, m, sc, sh, ops.ACT_GELU)
         return new
@@ -396,7 +396,7 @@ class PointTransformerV3(nn.Module):
         return not all(ops.subm_fused_ok(c, n) for c in chans)
 
     def prepare(self, data_dict, perms: Optional[List[Sequence[int]]] = None, pairs: bool = True,
-                reorder: bool = False) -> Point:
+                reorder: bool = False, centre_pairs: bool = False) -> Point:
         """Point + serialization (randperm draw 0) + stage-0 neighbour map; `feat` is not embedded yet.
 
         reorder: renumber the points by their first serialized order (sfx_serialize_permute; `point.perm[i]` is the
@@ -421,7 +421,8 @@ class PointTransformerV3(nn.Module):
             _lib.call("sfx_offsets_to_batch", n, B, offs.data_ptr(), batch.data_ptr(), _lib.stream())
         # the stage-0 neighbour map needs no serialization: enqueued before the depth read, it keeps the GPU busy
         # while the host enqueues the serialization (the read drains the queue up to the grid max's copy)
-        nbr = None if (reorder or not NBR_EARLY) else ops.subm_neighbors(grid, batch, with_pairs=pairs)
+        nbr = None if (reorder or not NBR_EARLY) else ops.subm_neighbors(grid, batch, with_pairs=pairs,
+                                                                          centre=centre_pairs)
         d = data_dict.get("serialized_depth")
         if isinstance(d, _lib.HostRead):  # the grid max, read back while the embedding runs
             depth = int(d.get()[0]).bit_length()
@@ -444,7 +445,7 @@ class PointTransformerV3(nn.Module):
             point.perm = perm
         if batch is not None:
             point.batch = batch
-        point.nbr = nbr if nbr is not None else ops.subm_neighbors(grid, batch, with_pairs=pairs)
+        point.nbr = nbr if nbr is not None else ops.subm_neighbors(grid, batch, with_pairs=pairs, centre=centre_pairs)
         return point
 
     @torch.no_grad()
@@ -461,7 +462,10 @@ class PointTransformerV3(nn.Module):
             emb_feat = ops.point_embed(feat, emb.weight, emb.bias, sc, sh)
         else:
             emb_feat = ops.linear(feat, emb.weight, emb.bias, scale=sc, shift=sh, act=ops.ACT_GELU)
-        point = self.prepare(data_dict, perms, pairs=self.stage_needs_pairs(0, feat.shape[0]), reorder=reorder)
+        # eval maps list the centre offset with the pairs: one pair launch per SubM conv (ops.SUBM_CENTRE_PAIRS)
+        cp = ops.SUBM_CENTRE_PAIRS
+        point = self.prepare(data_dict, perms, pairs=self.stage_needs_pairs(0, feat.shape[0]), reorder=reorder,
+                             centre_pairs=cp)
         perm = point.get("perm")
         point.feat = emb_feat if perm is None else ops.move_rows(emb_feat, perm)
         final_out = out
@@ -485,7 +489,7 @@ class PointTransformerV3(nn.Module):
                 if name == "down":
                     m = counts_rd.get()[k - 1] if counts_rd is not None else None
                     point = mod.run(point, self._draw_perm(perms, k), m=m, deferred=deferred,
-                                    pairs=self.stage_needs_pairs(s, m))
+                                    pairs=self.stage_needs_pairs(s, m), centre=cp)
                     k += 1
                 else:
                     point = mod.run(point)

@@ -25,7 +25,7 @@ _lib.register("sfx_amax_f32", [I, I, P, L, P, I, P])
 _lib.register("sfx_ln_amax_bound", [I, P, P, P, I, P])
 _lib.register("sfx_layernorm", [I, I, P, L, P, P, F, P, L, P])
 _lib.register("sfx_cpe_residual_ln", [I, I, P, P, P, P, P, P, F, P, P, P])
-_lib.register("sfx_cpe_residual_ln_pairs", [I, I, P, P, P, L, P, P, P, P, P, F, P, P, P])
+_lib.register("sfx_cpe_residual_ln_pairs", [I, I, P, L, P, P, L, P, P, P, P, P, F, P, P, P])
 _lib.register("sfx_window_attention", [I, I, I, I, I, P, P, P, F, P, P, I, P])
 _lib.register("sfx_window_attention_varlen", [I, I, I, I, I, P, P, P, F, P, P, I, P])
 _lib.register("sfx_window_attention_proj", [I, I, I, I, I, P, P, P, F, P, I, P, P, P, P, L, P, L, P])
@@ -43,7 +43,7 @@ _lib.register("sfx_subm_table_log2", [I])
 _lib.register("sfx_subm_neighbors", [I, P, P, I, P, P, P, P, P, P])
 _lib.register("sfx_subm_permute", [I, P, P, P, P, P, P])
 _lib.register("sfx_subm_pairs_workspace_bytes", [I], Z)
-_lib.register("sfx_subm_pairs", [I, P, P, Z, P, P, P, P])
+_lib.register("sfx_subm_pairs", [I, P, P, Z, P, P, P, I, P])
 _lib.register("sfx_subm_conv", [I, I, I, P, L, P, P, P, P, P, P, P, L, P, I, P, I, P, P, P])
 _lib.register("sfx_subm_conv_partials", [I, I, I, P, L, P, P, P, P, P, P, P, L, P, L, P, P, P])
 _lib.register("sfx_subm_conv_partials_pairs", [I, I, I, P, L, P, P, P, P, P, P, P, L, P, L, P, P, P])
@@ -442,7 +442,8 @@ def cpe_residual_ln(t, x: Tensor, g_cpe: Tensor, b_cpe: Tensor, g1: Tensor, b1: 
     x_out = torch.empty_like(x) if x_out is None else x_out
     h = torch.empty_like(x)
     if isinstance(t, SubmPartials):
-        call("sfx_cpe_residual_ln_pairs", M, C, ptr(t.centre), ptr(t.partials), ptr(t.pair_pos), t.num_pairs, ptr(x),
+        call("sfx_cpe_residual_ln_pairs", M, C, ptr(t.centre), t.ldt, ptr(t.partials), ptr(t.pair_pos), t.num_pairs,
+             ptr(x),
              ptr(g_cpe), ptr(b_cpe), ptr(g1), ptr(b1), float(eps), ptr(x_out), ptr(h), stream())
     else:
         call("sfx_cpe_residual_ln", M, C, ptr(t), ptr(x), ptr(g_cpe), ptr(b_cpe), ptr(g1), ptr(b1), float(eps),
@@ -714,51 +715,91 @@ def segment_mean(x: Tensor, idx_ptr: Tensor, sorted_idx: Tensor, m: int) -> Tens
     return out
 
 
-class SubmMap:
-    """Per-stage SubMConv3d indice map (indice_key=stage{s}): nbr [n,27] + offset-major pair lists.  The pair
-    lists are built on first use (ensure_pairs; subm_neighbors(with_pairs=True) builds them right away): the fused
-    conv (subm_cpe_ln) reads nbr only.  The 28 pair offsets reach the host asynchronously; the first conv that
-    needs them waits for that copy only."""
+class PairLists:
+    """Offset-major SubM pair lists of one map (sfx_subm_pairs): pair_in / pair_out, the 28 per-offset prefixes (read
+    back asynchronously; the first conv that needs them waits for that copy only) and the inverted index pair_pos.
+    centre=True also lists the centre offset k = 13 (the eval conv's single pair launch, ABI v15)."""
 
-    def __init__(self, nbr: Tensor, mask: Tensor):
-        self.nbr, self.mask = nbr, mask
-        self._pairs = None  # (pair_in, pair_out, offsets source: _lib.HostRead, device offsets)
+    def __init__(self, nbr: Tensor, centre: bool):
+        n = nbr.shape[0]
+        dev = nbr.device
+        cap = max(1, (27 if centre else 26) * n)
+        self.centre = centre
+        self.pair_in = torch.empty(cap, device=dev, dtype=torch.int32)
+        self.pair_out = torch.empty(cap, device=dev, dtype=torch.int32)
+        self.off_dev = torch.empty(28, device=dev, dtype=torch.int32)
+        ws = _lib.workspace(_lib.fn("sfx_subm_pairs_workspace_bytes")(n), dev)
+        call("sfx_subm_pairs", n, ptr(nbr), ptr(ws), ws.numel(), ptr(self.pair_in), ptr(self.pair_out),
+             ptr(self.off_dev), 1 if centre else 0, stream())
+        self._rd = _lib.HostRead(self.off_dev)
+        self._n = n
         self._off = None
         self._off_c = None
         self._pos = None
+
+    def off_ready(self) -> bool:
+        return self._off is not None
+
+    @property
+    def pair_off(self) -> List[int]:
+        if self._off is None:
+            self._off = self._rd.get()
+        return self._off
+
+    @property
+    def off_host(self):
+        if self._off_c is None:
+            self._off_c = (ctypes.c_int * 28)(*self.pair_off)
+        return self._off_c
+
+    @property
+    def num_pairs(self) -> int:
+        return self.pair_off[27]
+
+    @property
+    def pair_pos(self) -> Tensor:
+        """[n, 27] inverted pair index (sfx_subm_pair_pos), built once per list."""
+        if self._pos is None:
+            pos = torch.empty(self._n, 27, device=self.pair_in.device, dtype=torch.int32)
+            call("sfx_subm_pair_pos", self._n, self.num_pairs, ptr(self.pair_out), ptr(self.off_dev), ptr(pos),
+                 stream())
+            self._pos = pos
+        return self._pos
+
+
+class SubmMap:
+    """Per-stage SubMConv3d indice map (indice_key=stage{s}): nbr [n,27] + offset-major pair lists (PairLists), built
+    on first use (subm_neighbors(with_pairs=True) builds the preferred kind right away): the fused conv
+    (subm_cpe_ln) reads nbr only.  Two kinds of lists: without the centre offset (the atomic conv, the training
+    backward) and with it (centre_pref: the eval conv's single pair launch)."""
+
+    def __init__(self, nbr: Tensor, mask: Tensor, centre_pref: bool = False):
+        self.nbr, self.mask = nbr, mask
+        self.centre_pref = centre_pref
+        self._lists = {}
         self._order = None
 
+    def lists(self, centre: bool = False) -> PairLists:
+        pl = self._lists.get(centre)
+        if pl is None:
+            pl = self._lists[centre] = PairLists(self.nbr, centre)
+        return pl
+
     def ensure_pairs(self) -> "SubmMap":
-        if self._pairs is None:
-            n = self.nbr.shape[0]
-            dev = self.nbr.device
-            cap = max(1, 26 * n)
-            pin = torch.empty(cap, device=dev, dtype=torch.int32)
-            pout = torch.empty(cap, device=dev, dtype=torch.int32)
-            poff = torch.empty(28, device=dev, dtype=torch.int32)
-            ws = _lib.workspace(_lib.fn("sfx_subm_pairs_workspace_bytes")(n), dev)
-            call("sfx_subm_pairs", n, ptr(self.nbr), ptr(ws), ws.numel(), ptr(pin), ptr(pout), ptr(poff), stream())
-            self._pairs = (pin, pout, _lib.HostRead(poff), poff)
+        self.lists(False)
         return self
 
     @property
     def pair_in(self) -> Tensor:
-        return self.ensure_pairs()._pairs[0]
+        return self.lists(False).pair_in
 
     @property
     def pair_out(self) -> Tensor:
-        return self.ensure_pairs()._pairs[1]
+        return self.lists(False).pair_out
 
     @property
     def pair_pos(self) -> Tensor:
-        """[n, 27] inverted pair index (sfx_subm_pair_pos), built once per map."""
-        if self._pos is None:
-            n = self.nbr.shape[0]
-            off_dev = self.ensure_pairs()._pairs[3]
-            pos = torch.empty(n, 27, device=self.nbr.device, dtype=torch.int32)
-            call("sfx_subm_pair_pos", n, self.num_pairs, ptr(self.pair_out), ptr(off_dev), ptr(pos), stream())
-            self._pos = pos
-        return self._pos
+        return self.lists(False).pair_pos
 
     @property
     def order(self) -> Tensor:
@@ -772,21 +813,16 @@ class SubmMap:
         return self._order
 
     def pair_off_ready(self) -> bool:
-        """Whether the pair offsets are already on the host (reading them costs no wait)."""
-        return self._off is not None
+        """Whether the (centre-free) pair offsets are already on the host (reading them costs no wait)."""
+        return self.lists(False).off_ready()
 
     @property
     def pair_off(self) -> List[int]:
-        if self._off is None:
-            self._off = self.ensure_pairs()._pairs[2].get()
-        return self._off
+        return self.lists(False).pair_off
 
     @property
     def _off_host(self):
-        if self._off_c is None:
-            import ctypes
-            self._off_c = (ctypes.c_int * 28)(*self.pair_off)
-        return self._off_c
+        return self.lists(False).off_host
 
     @property
     def shape(self):
@@ -794,11 +830,12 @@ class SubmMap:
 
     @property
     def num_pairs(self) -> int:
-        return self.pair_off[27]
+        return self.lists(False).num_pairs
 
 
-def subm_neighbors(grid_coord: Tensor, batch: Optional[Tensor], with_pairs: bool = True):
-    """27-neighbour map; with_pairs also builds the offset-major pair lists (their offsets read back asynchronously)."""
+def subm_neighbors(grid_coord: Tensor, batch: Optional[Tensor], with_pairs: bool = True, centre: bool = False):
+    """27-neighbour map; with_pairs also builds the offset-major pair lists (their offsets read back asynchronously):
+    with the centre offset when `centre` (the eval forward's maps), else without."""
     n = grid_coord.shape[0]
     dev = grid_coord.device
     l2 = _lib.fn("sfx_subm_table_log2")(n)
@@ -808,12 +845,17 @@ def subm_neighbors(grid_coord: Tensor, batch: Optional[Tensor], with_pairs: bool
     mask = torch.empty(n, device=dev, dtype=torch.int32)
     call("sfx_subm_neighbors", n, ptr(grid_coord, torch.int32), ptr(batch), l2, ptr(tk), ptr(tv), ptr(nbr), ptr(mask),
          None, stream())
-    smap = SubmMap(nbr, mask)
-    return smap.ensure_pairs() if with_pairs else smap
+    smap = SubmMap(nbr, mask, centre_pref=centre)
+    if with_pairs:
+        smap.lists(centre)
+    return smap
 
 
 # eval-path SubM convs: store per-pair partials and sum them in the consumer (default), or add them atomically
 SUBM_PARTIALS = os.environ.get("SFX_SUBM_ATOMIC", "0") != "1"
+# the eval forward's maps list the centre offset with the pairs: each conv is ONE pair launch, the centre's products
+# being partial rows like the other offsets' (was a separate centre GEMM launch); SFX_SUBM_CENTRE_PAIRS=0 restores it
+SUBM_CENTRE_PAIRS = os.environ.get("SFX_SUBM_CENTRE_PAIRS", "1") != "0"
 # the first conv of a new SubM map enqueues its centre GEMM before waiting for the pair offsets
 SUBM_CENTRE_FIRST = os.environ.get("SFX_SUBM_CENTRE_FIRST", "1") != "0"
 PAIRS_LN_CHANNELS = (64, 96, 128, 256, 512)  # the channel counts sfx_cpe_residual_ln_pairs has kernels for
@@ -823,10 +865,10 @@ def subm_partials_ok(x: Tensor, smap: "SubmMap", cout: int) -> bool:
     """Whether the atomic-free SubM form can run for this launch: its consumer (sfx_cpe_residual_ln_pairs) needs
     C in PAIRS_LN_CHANNELS, 16-byte aligned contiguous rows and partials below the 2 GiB buffer range; other
     launches (e.g. enc_dim=32's C=32 stage 0, reference pointtransformer_v3.py:113) take the atomic form."""
-    # the 2 GiB partials bound from 26 n (no host wait for the pair count) unless that bound is too coarse
+    # the 2 GiB partials bound from 27 n (no host wait for the pair count) unless that bound is too coarse
     return (SUBM_PARTIALS and cout in PAIRS_LN_CHANNELS and x.shape[1] == cout and x.is_contiguous()
-            and x.data_ptr() % 16 == 0 and (26 * smap.nbr.shape[0] * cout * 4 + 64 < 0x7ffffff0
-                                            or smap.num_pairs * cout * 4 + 64 < 0x7ffffff0))
+            and x.data_ptr() % 16 == 0 and (27 * smap.nbr.shape[0] * cout * 4 + 64 < 0x7ffffff0
+                                            or smap.lists(smap.centre_pref).num_pairs * cout * 4 + 64 < 0x7ffffff0))
 
 
 # Block.cpe + shortcut + norm1 of the eval forward in one launch, the conv summed in MFMA registers over all 27
@@ -893,18 +935,21 @@ _ZERO_OFFS = (ctypes.c_int * 28)()  # pair offsets of a centre-only sfx_subm_con
 
 class SubmPartials:
     """Atomic-free SubM conv output: centre [n, Cout] (bias + centre offset) and partials [num_pairs, Cout] (one row
-    per (offset, output) pair), summed per output row by the consumer (cpe_residual_ln) or by `total()`."""
+    per (offset, output) pair), summed per output row by the consumer (cpe_residual_ln) or by `total()`.  ldt = 0:
+    `centre` is the bias [Cout] alone and the centre offset's products are partial rows (pair lists with the centre)."""
 
-    def __init__(self, centre: Tensor, partials: Tensor, pair_pos: Tensor, num_pairs: int):
+    def __init__(self, centre: Tensor, partials: Tensor, pair_pos: Tensor, num_pairs: int, ldt: Optional[int] = None):
         self.centre, self.partials, self.pair_pos, self.num_pairs = centre, partials, pair_pos, num_pairs
+        self.ldt = centre.shape[-1] if ldt is None else ldt
 
     def total(self) -> Tensor:
-        """The conv output, summed in the consumer's order (ascending offsets after the centre)."""
-        out = self.centre.clone()
+        """The conv output, summed in the consumer's order (ascending offsets after the centre / the bias)."""
+        n = self.pair_pos.shape[0]
+        out = self.centre.expand(n, -1).clone() if self.ldt == 0 else self.centre.clone()
         pos = self.pair_pos.long()
         for k in range(27):
             sel = pos[:, k] >= 0
-            if k != 13 and bool(sel.any()):
+            if bool(sel.any()):
                 out[sel] += self.partials[pos[sel, k]]
         return out
 
@@ -923,6 +968,14 @@ def subm_conv(x: Tensor, smap: "SubmMap", weight: Tensor, bias: Optional[Tensor]
     po, ldo = _rows(out)
     if partials:
         wsp = weight_split(weight)
+        if smap.centre_pref and SUBM_CENTRE_PAIRS:  # one pair launch over all 27 offsets (the lists carry the centre)
+            pl = smap.lists(True)
+            npairs = pl.num_pairs
+            part = torch.empty(max(1, npairs), cout, device=x.device, dtype=torch.float32)
+            call("sfx_subm_conv_partials_pairs", n, cin, cout, px, ldx, ptr(smap.nbr), ptr(weight), ptr(bias),
+                 ptr(pl.pair_in), ptr(pl.pair_out), pl.off_host, po, ldo, ptr(part), cout, *wsp, stream())
+            b = bias if bias is not None else torch.zeros(cout, device=x.device, dtype=torch.float32)
+            return SubmPartials(b.contiguous(), part, pl.pair_pos, npairs, ldt=0)
         if SUBM_CENTRE_FIRST and not smap.pair_off_ready():  # centre GEMM first, then wait for the pair offsets
             call("sfx_subm_conv_partials", n, cin, cout, px, ldx, ptr(smap.nbr), ptr(weight), ptr(bias), None, None,
                  _ZERO_OFFS, po, ldo, None, cout, *wsp, stream())

@@ -199,21 +199,25 @@ def test_linear_gather_is_subm_conv(device):
         assert rel_l2(y2.cpu(), ref2) < 2e-6
 
 
-def test_subm_conv_partials_atomic_free(device):
+@pytest.mark.parametrize("centre,unique", [(False, True), (True, True), (True, False)])
+def test_subm_conv_partials_atomic_free(device, centre, unique):
     """Atomic-free SubM conv (sfx_subm_conv_partials + sfx_subm_pair_pos + sfx_cpe_residual_ln_pairs): the inverted
     pair index names every pair, the per-row sum in ascending offset order equals the oracle conv, the fused
-    cpe/residual/LN tail equals the unfused one on that sum bit for bit, and two runs agree bit for bit."""
+    cpe/residual/LN tail equals the unfused one on that sum bit for bit, and two runs agree bit for bit.
+    centre=True: the eval forward's lists with the centre offset (one pair launch, bias-only T; ABI v15), incl.
+    duplicate voxels (the centre pair's input is the voxel's lowest-index point)."""
     n = 6000
-    s = make_scene(n, 1, seed=5, unique_voxels=True)
+    s = make_scene(n, 1, seed=5, unique_voxels=unique)
     grid = torch.floor(s["means"] * 320).int()
     nbr_ref = ptv3_ref.subm_neighbors(grid, torch.zeros(grid.shape[0], dtype=torch.int64))
-    smap = ops.subm_neighbors(grid.to(device), None)
-    off = smap.pair_off
-    pos = smap.pair_pos.cpu().long()
-    pout = smap.pair_out.cpu().long()
-    assert int((pos >= 0).sum()) == off[27] and bool((pos[:, 13] < 0).all())
+    smap = ops.subm_neighbors(grid.to(device), None, centre=centre)
+    pl = smap.lists(centre)
+    off = pl.pair_off
+    pos = pl.pair_pos.cpu().long()
+    pout = pl.pair_out.cpu().long()
+    assert int((pos >= 0).sum()) == off[27] and bool((pos[:, 13] >= 0).all() if centre else (pos[:, 13] < 0).all())
     for k in range(27):
-        if k == 13:
+        if k == 13 and not centre:
             continue
         p = torch.arange(off[k], off[k + 1])
         assert torch.equal(pos[pout[p], k], p)
