@@ -58,7 +58,8 @@ HBM_PEAK_GBS = 8000.0
 # kernel-name prefixes of the dominant family: the GEMMs, the fused Block MLP, the fused SubM conv + CPE
 # LayerNorm (subm_fused.hip), the fused output heads (heads.hip) and, since round 6, the fused attention + output
 # projection (attn_proj.hip: it absorbed the projection GEMMs)
-GEMM_FAMILY = ("gemm_kernel", "wgrad_kernel", "mlp_kernel", "subm_cpe_ln_kernel", "heads_kernel", "attn_proj_kernel")
+GEMM_FAMILY = ("gemm_kernel", "wgrad_kernel", "mlp_kernel", "subm_cpe_ln_kernel", "heads_kernel", "attn_proj_kernel",
+               "cpe_ln_qkv_kernel")
 
 
 def in_family(kernel_name: str) -> bool:
@@ -193,6 +194,10 @@ def _gemm_cost(kind, args, kw, res):
         fl = 2.0 * M * (ng * (kin * 128 + 2 * 128 * 128) + 128 * out_dim)
         return fl, (M * x.shape[1] + M * out_dim + ng * (kin * 128 + 2 * 128 * 128) + out_dim * 128) * f4, \
             (M, ng * 128, kin)
+    if kind == "cpe_ln_qkv":  # pair-sum LayerNorms + the qkv projection (its GEMM FLOPs), one launch
+        x = args[1]
+        M, C = x.shape
+        return 6.0 * M * C * C, (3 * M * C + 3 * M * C + 3 * C * C) * f4, (M, 3 * C, C)
     if kind == "window_attention_proj":  # fused attention (QK^T + PV over K-key windows) + projection + residual
         qkv, K, C = args[0], args[4], args[6]
         n = qkv.shape[0]
@@ -218,7 +223,7 @@ class GemmTimer:
                           (train_ops, "linear_bwd_data"), (train_ops, "linear_wgrad"),
                           (train_ops, "subm_conv_bwd_data"), (ptv3_ops, "cpe_residual_ln"),
                           (ptv3_ops, "block_mlp"), (ptv3_ops, "subm_cpe_ln"), (ptv3_ops, "heads"),
-                          (ptv3_ops, "window_attention_proj")]:
+                          (ptv3_ops, "window_attention_proj"), (ptv3_ops, "cpe_ln_qkv")]:
             fn = getattr(mod, name)
             self._saved.append((mod, name, fn))
             setattr(mod, name, self._wrap(name, fn))
@@ -276,7 +281,7 @@ def roofline_probe(unit_fn, passes=3, dump=None):
     # the family grew (round 3: + the fused MLP and the pair-sum LayerNorm); the pure-GEMM subset
     # (gemm_kernel / wgrad_kernel launches only) is the figure comparable with rounds 1-2
     pure = [p for p in per if p[1] not in ("block_mlp", "cpe_residual_ln", "subm_cpe_ln", "heads",
-                                           "window_attention_proj")]
+                                           "window_attention_proj", "cpe_ln_qkv")]
     pms, pfl = sum(p[0] for p in pure), sum(p[3] for p in pure)
     pure_tf = pfl / (pms * 1e-3) / 1e12 if pms > 0 else 0.0
     return {
@@ -292,7 +297,9 @@ def roofline_probe(unit_fn, passes=3, dump=None):
                    "subm_cpe_ln_kernel, the SubM conv with its pair products summed on chip + the CPE LayerNorm "
                    "tail (C <= 128); heads_kernel, the six output MLPs; attn_proj_kernel, the window attention "
                    "fused with the output projection + residual (counted with its attention FLOP, 4 K C per point, "
-                   "and its projection FLOP, 2 C^2 per point); and cpe_residual_ln4_kernel<.., true>, the "
+                   "and its projection FLOP, 2 C^2 per point); cpe_ln_qkv_kernel, the SubM conv's pair sums + the CPE "
+                   "and norm1 LayerNorms + the qkv projection (its 6 C^2 FLOP per point) at C <= 128; and "
+                   "cpe_residual_ln4_kernel<.., true>, the "
                    "C >= 256 SubM conv's per-row sum of its stored pair products), "
                    "every launch of one unit of work incl. operand-maxima passes"),
         "timing": "HIP events around each launch on its stream, in the real launch sequence; median of "

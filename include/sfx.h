@@ -283,6 +283,15 @@ int sfx_cpe_residual_ln_pairs(int M, int C, const float* T, long long ldt, const
                               long long num_pairs, const float* X, const float* gamma_cpe, const float* beta_cpe,
                               const float* gamma1, const float* beta1, float eps, float* X_out, float* H,
                               void* stream);
+/* (ABI v15) sfx_cpe_residual_ln_pairs followed by the Block's qkv projection in one launch (eval, C in {64, 96, 128};
+ * calflops.py:45-55): X_out = X + LN_cpe(T + pair partials); qkv [M][3C] = LN1(X_out) W^T + bias with
+ * W = sfx_weight_split of the qkv weight [3C][C] (w_split, w_inv) -- the norm1 output never leaves the chip.
+ * max |qkv| is published into amax_slot (tag; may be NULL) for sfx_window_attention's fp16x2 scale.  X_out != X. */
+int sfx_cpe_ln_qkv_pairs(int M, int C, const float* T, long long ldt, const float* partials, const int* pair_pos,
+                         long long num_pairs, const float* X, const float* gamma_cpe, const float* beta_cpe,
+                         const float* gamma1, const float* beta1, float eps, float* X_out, const float* w_split,
+                         const float* w_inv, const float* bias, float* qkv, unsigned long long* amax_slot,
+                         unsigned tag, void* stream);
 
 /* SerializedAttention (non-flash): windows win[w] = (key_start, query_start) over serialized positions,
  * qkv [N,3C] in point order, order [N] serialized->point; out[order[p]] for every query position p. */

@@ -198,6 +198,146 @@ __global__ void __launch_bounds__(256) cpe_residual_ln4_kernel(int M, const floa
   for (int i = 0; i < NV; ++i) *reinterpret_cast<float4*>(H + base + 4 * (sub + G * i)) = o[i];
 }
 
+// ---- pair-sum CPE LayerNorm + shortcut + norm1 + the qkv projection in one launch (eval Block, C <= 128) --------
+// The Block's front half after its SubM conv (calflops.py:45-53 cpe tail, shortcut, norm1; :55 attn.qkv): per row
+// t = T + sum_k partials (ascending k), x1 = X + LN_cpe(t) (written: the attention's residual), h = LN1(x1) -- kept
+// on chip -- and qkv = h W^T + b (written, with max |qkv| published for the attention's fp16x2 scale).  h never
+// reaches HBM and the qkv GEMM launch is gone.
+// Mapping: wave w owns 32 consecutive rows.  Phase A (the LayerNorms, G lanes per row as cpe_residual_ln4_kernel,
+// identical arithmetic) splits each h row into fp16x2 terms at the row's own power-of-two scale (max in
+// [2^14, 2^15)) and stores them in the wave's LDS image [2 terms][32 rows][C fp16] (16-byte chunk c of row r at
+// c ^ (r & 7): conflict-free fragment reads).  Phase B: qkv^T[32 features][32 points] per chunk of 32 features on
+// v_mfma_f32_32x32x16_f16 (h*h + h*l + l*h, fp32 accumulation): A = the pre-split W rows (sfx_weight_split, read
+// from L2), B = the wave's h image (all k-steps held in registers across the 3C / 32 chunks); the epilogue unscales
+// by the feature's and the point's scale, adds the bias and stores 16-byte row pieces.
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+template <int G>
+__device__ __forceinline__ float group_max(float v) {
+#pragma unroll
+  for (int o = G / 2; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+template <int G, int NV>
+__global__ void __launch_bounds__(256) cpe_ln_qkv_kernel(int M, const float* __restrict__ T, long long ldt,
+                                                         const float* __restrict__ P, const int* __restrict__ pos,
+                                                         const float* __restrict__ X, const float* __restrict__ g_cpe,
+                                                         const float* __restrict__ b_cpe,
+                                                         const float* __restrict__ g1, const float* __restrict__ b1,
+                                                         float eps, float* __restrict__ X1,
+                                                         const uint4* __restrict__ wsp, const float* __restrict__ winv,
+                                                         const float* __restrict__ bq, float* __restrict__ QKV,
+                                                         unsigned long long* __restrict__ amax, unsigned tag) {
+  constexpr int C = 4 * G * NV, N = 3 * C, NCHK = N / 32, KS = C / 16, RPP = 64 / G;
+  constexpr int ROWB = 2 * C;  // bytes per image row and term
+  static_assert(C % 64 == 0 || C == 96, "C");
+  __shared__ __attribute__((aligned(16))) char himg[4][2][32 * ROWB];
+  __shared__ float rsc[4][32];
+  __shared__ float red[4];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, sub = lane % G, grp = lane / G;
+  const int r0 = blockIdx.x * 128 + 32 * wid;
+  char* H0 = himg[wid][0];
+  char* H1 = himg[wid][1];
+  auto hoff = [](int r, int c) -> int { return r * ROWB + ((c ^ (r & 7)) << 4); };
+
+  // ---- phase A: LayerNorms (cpe_residual_ln4_kernel's arithmetic), h -> the wave's fp16x2 image ----
+#pragma unroll 1
+  for (int p = 0; p < 32 / RPP; ++p) {
+    const int lr = p * RPP + grp;
+    const int row = r0 + lr;
+    float4 o[NV];
+    if (row < M) {
+      float4 v[NV], x[NV];
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        v[i] = *reinterpret_cast<const float4*>(T + (long long)row * ldt + 4 * (sub + G * i));
+        x[i] = *reinterpret_cast<const float4*>(X + (long long)row * C + 4 * (sub + G * i));
+      }
+      add_pair_partials<G, NV>(v, P, pos, row, sub);
+      ln_row4<G, NV>(v, g_cpe, b_cpe, eps, sub, o);
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        v[i] = make_float4(x[i].x + o[i].x, x[i].y + o[i].y, x[i].z + o[i].z, x[i].w + o[i].w);
+        *reinterpret_cast<float4*>(X1 + (long long)row * C + 4 * (sub + G * i)) = v[i];
+      }
+      ln_row4<G, NV>(v, g1, b1, eps, sub, o);
+    } else {
+#pragma unroll
+      for (int i = 0; i < NV; ++i) o[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    float m = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) m = fmaxf(m, fmaxf(fmaxf(fabsf(o[i].x), fabsf(o[i].y)), fmaxf(fabsf(o[i].z), fabsf(o[i].w))));
+    m = group_max<G>(m);
+    int e = 0;
+    if (m > 0.f && m <= 3.4028235e38f) {
+      (void)frexpf(m, &e);
+      e = 15 - e;
+      e = e > 126 ? 126 : (e < -126 ? -126 : e);
+    }
+    const float sc = ldexpf(1.f, e);
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c0 = 4 * (sub + G * i);  // channels c0 .. c0 + 3: half (c0 & 4) of 16-byte chunk c0 / 8
+      uint2 t[2];
+      sfx::split2h(o[i], sc, t);
+      const int off = hoff(lr, c0 >> 3) + ((c0 & 4) << 1);
+      *reinterpret_cast<uint2*>(H0 + off) = t[0];
+      *reinterpret_cast<uint2*>(H1 + off) = t[1];
+    }
+    if (sub == 0) rsc[wid][lr] = ldexpf(1.f, -e);
+  }
+  __syncthreads();
+
+  // ---- phase B: qkv^T chunks of 32 features for the wave's 32 points (lane = point) ----
+  const int l32 = lane & 31, h = lane >> 5;
+  const float ri = rsc[wid][l32];
+  const int prow = r0 + l32;
+  f16x8 bh[KS], bl[KS];
+#pragma unroll
+  for (int t = 0; t < KS; ++t) {
+    const int off = hoff(l32, 2 * t + h);
+    bh[t] = __builtin_bit_cast(f16x8, *reinterpret_cast<const uint4*>(H0 + off));
+    bl[t] = __builtin_bit_cast(f16x8, *reinterpret_cast<const uint4*>(H1 + off));
+  }
+  float mx = 0.f;
+#pragma unroll 1
+  for (int ck = 0; ck < NCHK; ++ck) {
+    floatx16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    const uint4* wr = wsp + (long long)(ck * 32 + l32) * (C / 4);
+#pragma unroll
+    for (int t = 0; t < KS; ++t) {
+      const uint4 a = wr[4 * t + 2 * h], b = wr[4 * t + 2 * h + 1];  // k = 16 t + 8 h .. + 7 of feature row n
+      const f16x8 wh = __builtin_bit_cast(f16x8, make_uint4(a.x, a.y, b.x, b.y));
+      const f16x8 wl = __builtin_bit_cast(f16x8, make_uint4(a.z, a.w, b.z, b.w));
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wl, bh[t], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, bl[t], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, bh[t], acc, 0, 0, 0);
+    }
+    if (prow < M) {
+      float* dst = QKV + (long long)prow * N + ck * 32;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int n0 = ck * 32 + 8 * g + 4 * h;
+        const float4 wi = *reinterpret_cast<const float4*>(winv + n0);
+        const float4 bb = *reinterpret_cast<const float4*>(bq + n0);
+        float4 y;
+        y.x = acc[4 * g + 0] * (wi.x * ri) + bb.x;
+        y.y = acc[4 * g + 1] * (wi.y * ri) + bb.y;
+        y.z = acc[4 * g + 2] * (wi.z * ri) + bb.z;
+        y.w = acc[4 * g + 3] * (wi.w * ri) + bb.w;
+        mx = fmaxf(mx, fmaxf(fmaxf(fabsf(y.x), fabsf(y.y)), fmaxf(fabsf(y.z), fabsf(y.w))));
+        *reinterpret_cast<float4*>(dst + 8 * g + 4 * h) = y;
+      }
+    }
+  }
+  if (amax) sfx::publish_amax(mx, amax, tag, red);
+}
+
 inline bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 // |LN(x)_c| = |z_c gamma_c + beta_c| with |z_c| <= sqrt(C - 1) (biased variance, eps only shrinks z)
@@ -299,6 +439,38 @@ int sfx_cpe_residual_ln_pairs(int M, int C, const float* T, long long ldt, const
   else SFX_CPE4P(64, 2);
 #undef SFX_CPE4P
   return sfx::check_launch("sfx_cpe_residual_ln_pairs");
+}
+
+// (ABI v15) sfx_cpe_residual_ln_pairs + the qkv projection in one launch (eval, C in {64, 96, 128}): X_out = X +
+// LN_cpe(T + pair partials), h = LN1(X_out) kept on chip, qkv [M][3C] = h W^T + b with W = sfx_weight_split of the
+// qkv weight [3C][C] (w_split, w_inv); max |qkv| published into amax_slot (tag) for sfx_window_attention.
+int sfx_cpe_ln_qkv_pairs(int M, int C, const float* T, long long ldt, const float* partials, const int* pair_pos,
+                         long long num_pairs, const float* X, const float* gamma_cpe, const float* beta_cpe,
+                         const float* gamma1, const float* beta1, float eps, float* X_out, const float* w_split,
+                         const float* w_inv, const float* bias, float* qkv, unsigned long long* amax_slot,
+                         unsigned tag, void* stream) {
+  SFX_REQUIRE(M >= 0 && num_pairs >= 0 && (ldt == 0 || ldt == C), "sfx_cpe_ln_qkv_pairs: bad sizes");
+  SFX_REQUIRE(C == 64 || C == 96 || C == 128, "sfx_cpe_ln_qkv_pairs: C must be 64, 96 or 128 (got %d)", C);
+  if (M == 0) return SFX_OK;
+  SFX_REQUIRE(T && X && gamma_cpe && beta_cpe && gamma1 && beta1 && X_out && pair_pos && w_split && w_inv && bias &&
+                  qkv && (num_pairs == 0 || partials) && (!amax_slot || tag != 0),
+              "sfx_cpe_ln_qkv_pairs: null buffer");
+  SFX_REQUIRE(num_pairs * C * 4 + 64 < 0x7ffffff0ll, "sfx_cpe_ln_qkv_pairs: partials exceed 2 GiB");
+  SFX_REQUIRE(al16(T) && al16(X) && al16(X_out) && al16(gamma_cpe) && al16(beta_cpe) && al16(gamma1) &&
+                  al16(beta1) && al16(w_split) && al16(w_inv) && al16(bias) && al16(qkv) && (!partials || al16(partials)),
+              "sfx_cpe_ln_qkv_pairs: buffers must be 16-byte aligned");
+  SFX_REQUIRE(X_out != X, "sfx_cpe_ln_qkv_pairs: in-place output is not supported");
+  hipStream_t st = sfx::as_stream(stream);
+  const unsigned grid = (unsigned)((M + 127) / 128);
+  const uint4* w = reinterpret_cast<const uint4*>(w_split);
+#define SFX_LNQKV(G, NV)                                                                                            \
+  cpe_ln_qkv_kernel<G, NV><<<grid, 256, 0, st>>>(M, T, ldt, partials, pair_pos, X, gamma_cpe, beta_cpe, gamma1, beta1, \
+                                                 eps, X_out, w, w_inv, bias, qkv, amax_slot, tag)
+  if (C == 64) SFX_LNQKV(16, 1);
+  else if (C == 96) SFX_LNQKV(8, 3);
+  else SFX_LNQKV(32, 1);
+#undef SFX_LNQKV
+  return sfx::check_launch("sfx_cpe_ln_qkv_pairs");
 }
 
 }  // extern "C"

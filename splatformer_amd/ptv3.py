@@ -165,11 +165,18 @@ class Block(nn.Module):
             # the conv's pair products go to per-pair rows that the LN kernel sums in a fixed order (no float
             # atomics, reproducible); SFX_SUBM_ATOMIC=1 restores the atomic accumulation
             t = ops.subm_conv(xc, point.nbr, wf, bf, partials=ops.subm_partials_ok(xc, point.nbr, C))
-            x1, h = ops.cpe_residual_ln(t, x, ln_c.weight, ln_c.bias, ln1.weight, ln1.bias, ln1.eps)
+            if ops.cpe_ln_qkv_ok(t, C, self.attn.qkv.weight):
+                # pair sums + LN_cpe + shortcut + norm1 + qkv in one launch: norm1's output never reaches HBM
+                x1, qkv, q_amax = ops.cpe_ln_qkv(t, x, ln_c.weight, ln_c.bias, ln1.weight, ln1.bias, ln1.eps,
+                                                 self.attn.qkv)
+                h = None
+            else:
+                x1, h = ops.cpe_residual_ln(t, x, ln_c.weight, ln_c.bias, ln1.weight, ln1.bias, ln1.eps)
         # The GEMMs scale their fp16x2 operands per row themselves (no operand bounds needed); the qkv GEMM
         # publishes max |qkv| for the attention's fp16x2 q / k / v terms (ptv3_ops.new_amax)
         oi = point.order_type[self.attn.order_index]
-        qkv, q_amax = ops.linear(h, self.attn.qkv.weight, self.attn.qkv.bias, y_amax=True)
+        if h is not None:
+            qkv, q_amax = ops.linear(h, self.attn.qkv.weight, self.attn.qkv.bias, y_amax=True)
         if self.attn.enable_flash:
             K, win3, nw = point_windows_flash(point, self.attn.patch_size_max)
             a = ops.window_attention_varlen(qkv, point.order_phys[oi], win3, nw, K, self.attn.num_heads, C,

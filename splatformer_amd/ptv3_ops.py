@@ -26,6 +26,7 @@ _lib.register("sfx_ln_amax_bound", [I, P, P, P, I, P])
 _lib.register("sfx_layernorm", [I, I, P, L, P, P, F, P, L, P])
 _lib.register("sfx_cpe_residual_ln", [I, I, P, P, P, P, P, P, F, P, P, P])
 _lib.register("sfx_cpe_residual_ln_pairs", [I, I, P, L, P, P, L, P, P, P, P, P, F, P, P, P])
+_lib.register("sfx_cpe_ln_qkv_pairs", [I, I, P, L, P, P, L, P, P, P, P, P, F, P, P, P, P, P, P, I, P])
 _lib.register("sfx_window_attention", [I, I, I, I, I, P, P, P, F, P, P, I, P])
 _lib.register("sfx_window_attention_varlen", [I, I, I, I, I, P, P, P, F, P, P, I, P])
 _lib.register("sfx_window_attention_proj", [I, I, I, I, I, P, P, P, F, P, I, P, P, P, P, L, P, L, P])
@@ -449,6 +450,32 @@ def cpe_residual_ln(t, x: Tensor, g_cpe: Tensor, b_cpe: Tensor, g1: Tensor, b1: 
         call("sfx_cpe_residual_ln", M, C, ptr(t), ptr(x), ptr(g_cpe), ptr(b_cpe), ptr(g1), ptr(b1), float(eps),
              ptr(x_out), ptr(h), stream())
     return x_out, h
+
+
+# the pair-sum CPE LayerNorm + norm1 + qkv projection as one launch on the eval Block (csrc/norm.hip
+# cpe_ln_qkv_kernel, ABI v15) for these channel counts; SFX_LN_QKV=0 restores LayerNorm launch + qkv GEMM
+LN_QKV = os.environ.get("SFX_LN_QKV", "1") != "0"
+LN_QKV_CHANNELS = (64, 96, 128)
+
+
+def cpe_ln_qkv_ok(t, C: int, qkv_weight: Tensor) -> bool:
+    return (LN_QKV and isinstance(t, SubmPartials) and C in LN_QKV_CHANNELS and get_precision() == "fp32"
+            and weight_split(qkv_weight)[0] is not None)
+
+
+def cpe_ln_qkv(t: "SubmPartials", x: Tensor, g_cpe: Tensor, b_cpe: Tensor, g1: Tensor, b1: Tensor, eps: float,
+               qkv: "torch.nn.Linear") -> Tuple[Tensor, Tensor, Tuple[int, int]]:
+    """(x', qkv, qkv amax slot): x' = x + LN_cpe(t), qkv = LN_norm1(x') W^T + b in one launch -- the Block front half
+    after the SubM conv (calflops.py:45-55); norm1's output stays on chip (sfx_cpe_ln_qkv_pairs)."""
+    M, C = x.shape
+    x_out = torch.empty_like(x)
+    out = torch.empty(M, 3 * C, device=x.device, dtype=torch.float32)
+    wsp, winv = weight_split(qkv.weight)
+    ys = new_amax(x.device)
+    call("sfx_cpe_ln_qkv_pairs", M, C, ptr(t.centre), t.ldt, ptr(t.partials), ptr(t.pair_pos), t.num_pairs, ptr(x),
+         ptr(g_cpe), ptr(b_cpe), ptr(g1), ptr(b1), float(eps), ptr(x_out), wsp, winv, ptr(qkv.bias), ptr(out),
+         ys[0], ys[1], stream())
+    return x_out, out, ys
 
 
 def window_table(offsets: Sequence[int], K: int) -> List[Tuple[int, int]]:

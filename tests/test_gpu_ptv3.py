@@ -242,6 +242,37 @@ def test_subm_conv_partials_atomic_free(device, centre, unique):
         assert torch.equal(xo, xo2) and torch.equal(h, h2)
 
 
+@pytest.mark.parametrize("C", [64, 96, 128])
+@pytest.mark.parametrize("n,centre", [(6000, True), (4133, False), (1, True), (129, True)])
+def test_cpe_ln_qkv_fused(device, C, n, centre):
+    """sfx_cpe_ln_qkv_pairs (pair sums + LN_cpe + shortcut + norm1 + qkv in one launch, norm1's output on chip) vs
+    the unfused HIP path (sfx_cpe_residual_ln_pairs + the qkv GEMM): x1 bit for bit (same LayerNorm arithmetic), qkv
+    against the fp64 product of the unfused path's h (fp16x2 terms: fp32-level error), the published amax bounding
+    |qkv|; ragged tile (n % 128 != 0), a single point, both pair-list kinds."""
+    s = make_scene(n, 1, seed=9, unique_voxels=False)
+    grid = torch.floor(s["means"] * 320).int()
+    smap = ops.subm_neighbors(grid.to(device), None, centre=centre)
+    g = torch.Generator().manual_seed(C + n)
+    x = torch.randn(n, C, generator=g).to(device)
+    w = (torch.randn(C, 3, 3, 3, C, generator=g) * 0.05).to(device)
+    b = torch.randn(C, generator=g).to(device)
+    ln = [torch.randn(C, generator=g).to(device) for _ in range(4)]
+    lin = torch.nn.Linear(C, 3 * C).to(device)
+    with torch.no_grad():
+        lin.weight.copy_(torch.randn(3 * C, C, generator=g) * C ** -0.5)
+        lin.bias.copy_(torch.randn(3 * C, generator=g) * 0.1)
+    sp = ops.subm_conv(x, smap, w, b, partials=True)
+    x1_u, h_u = ops.cpe_residual_ln(sp, x, *ln, 1e-5)
+    x1, qkv, slot = ops.cpe_ln_qkv(sp, x, *ln, 1e-5, lin)
+    assert torch.equal(x1, x1_u)
+    ref = h_u.double() @ lin.weight.double().T + lin.bias.double()
+    e = rel_l2(qkv.double(), ref)
+    e_gemm = rel_l2(ops.linear(h_u, lin.weight, lin.bias).double(), ref)
+    print(f"\n[cpe_ln_qkv C={C} n={n}] qkv rel L2 vs fp64: fused {e:.2e}, qkv GEMM {e_gemm:.2e}")
+    assert e < 2e-6
+    assert _slot_value(device, slot) >= float(qkv.abs().max())
+
+
 @pytest.mark.parametrize("C", [64, 96, 128, 256])
 @pytest.mark.parametrize("n,unique,sep", [(6000, True, False), (4133, False, True), (1, True, False),
                                           (20011, False, False)])

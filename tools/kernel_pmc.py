@@ -33,6 +33,7 @@ FAMILIES = [  # (family, kernel-name regex) -- first match wins
     ("subm pair-sum LayerNorm", r"^cpe_residual_ln4_kernel<\d+, \d+, true>"),
     ("fused subm conv + CPE LN", r"^subm_cpe_ln_kernel"),
     ("fused output heads", r"^heads_kernel"),
+    ("pair-sum LN + qkv (fused)", r"^cpe_ln_qkv_kernel"),
     ("point embedding", r"^point_embed"),
     ("attention", r"^window_attn"),
     ("attention + proj (fused)", r"^attn_proj_kernel"),
