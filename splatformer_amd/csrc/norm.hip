@@ -205,8 +205,8 @@ __global__ void __launch_bounds__(256) cpe_residual_ln4_kernel(int M, const floa
 // reaches HBM and the qkv GEMM launch is gone.
 // Mapping: wave w owns 32 consecutive rows.  Phase A (the LayerNorms, G lanes per row as cpe_residual_ln4_kernel,
 // identical arithmetic) splits each h row into fp16x2 terms at the row's own power-of-two scale (max in
-// [2^14, 2^15)) and stores them in the wave's LDS image [2 terms][32 rows][C fp16] (16-byte chunk c of row r at
-// c ^ (r & 7): conflict-free fragment reads).  Phase B: qkv^T[32 features][32 points] per chunk of 32 features on
+// [2^14, 2^15)) and stores them in the wave's LDS image [2 terms][32 rows][C fp16] (16-byte chunks XOR-swizzled by
+// row: spread fragment reads).  Phase B: qkv^T[32 features][32 points] per chunk of 32 features on
 // v_mfma_f32_32x32x16_f16 (h*h + h*l + l*h, fp32 accumulation): A = the pre-split W rows (sfx_weight_split, read
 // from L2), B = the wave's h image (all k-steps held in registers across the 3C / 32 chunks); the epilogue unscales
 // by the feature's and the point's scale, adds the bias and stores 16-byte row pieces.
@@ -240,7 +240,10 @@ __global__ void __launch_bounds__(256) cpe_ln_qkv_kernel(int M, const float* __r
   const int r0 = blockIdx.x * 128 + 32 * wid;
   char* H0 = himg[wid][0];
   char* H1 = himg[wid][1];
-  auto hoff = [](int r, int c) -> int { return r * ROWB + ((c ^ (r & 7)) << 4); };
+  // 16-byte chunk c of row r at c ^ (r & SW): SW = 7 when a row holds a multiple of 8 chunks (C = 64, 128), 3 for
+  // C = 96's 12 chunks (the XOR must stay inside the row)
+  constexpr int SW = (C / 8) % 8 == 0 ? 7 : 3;
+  auto hoff = [](int r, int c) -> int { return r * ROWB + ((c ^ (r & SW)) << 4); };
 
   // ---- phase A: LayerNorms (cpe_residual_ln4_kernel's arithmetic), h -> the wave's fp16x2 image ----
 #pragma unroll 1
