@@ -453,8 +453,11 @@ def cpe_residual_ln(t, x: Tensor, g_cpe: Tensor, b_cpe: Tensor, g1: Tensor, b1: 
 
 
 # the pair-sum CPE LayerNorm + norm1 + qkv projection as one launch on the eval Block (csrc/norm.hip
-# cpe_ln_qkv_kernel, ABI v15) for these channel counts; SFX_LN_QKV=0 restores LayerNorm launch + qkv GEMM
-LN_QKV = os.environ.get("SFX_LN_QKV", "1") != "0"
+# cpe_ln_qkv_kernel, ABI v15).  Opt-in (SFX_LN_QKV=1): measured slower on config B (C = 128: 222 us vs 78 + 68 us for
+# the LayerNorm launch + qkv GEMM; C = 96: 133 vs 58 + 54; C = 64: 77 vs 42 + 38; 602 vs 621 renders/s,
+# profiles/r06_ab_ln_qkv.txt): 128-row workgroups at two per CU keep far fewer pair-partial gathers in flight than
+# the LayerNorm kernel's 8-row workgroups, and the LayerNorm phase is the latency-bound part
+LN_QKV = os.environ.get("SFX_LN_QKV", "0") == "1"
 LN_QKV_CHANNELS = (64, 96, 128)
 
 
