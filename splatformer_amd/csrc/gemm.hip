@@ -1091,10 +1091,13 @@ constexpr TunedLaunch kTuned[] = {
 
 // The same for the SubM conv launches of config B's stages (sfx_subm_conv: n, Cout, Cin -> the tile shape /
 // Stream-K of its centre and pair launches; re-swept for the per-pair-store form,
-// profiles/r02_gemm_tune_conv_partials.jsonl -- Stream-K only applies to the atomic form)
+// profiles/r02_gemm_tune_conv_partials.jsonl -- Stream-K only applies to the atomic form; round 6 re-sweep with the
+// centre offset in the eval pair lists, profiles/r06_gemm_tune.jsonl: stage 2 -> 128x128 tiles (86 vs 103 us),
+// stage 0 -> 128x96 (37 vs 43 us))
 constexpr TunedLaunch kTunedConv[] = {
     {90434, 96, 96, 1, 1},
-    {70349, 128, 128, 3, 1},
+    {70349, 128, 128, 0, 0},
+    {100000, 64, 64, 1, 0},
     {37759, 256, 256, 6, 1},
     {14764, 512, 512, 6, 0},
     {100000, 96, 96, 1, 0},

@@ -39,8 +39,9 @@ class GemmRecorder:
             o = rec._conv(x, smap, weight, bias, out=out, **kw)
             n, cin = x.shape
             cout = weight.shape[0]
-            scratch = torch.empty_like(o.centre if isinstance(o, ops.SubmPartials) else o)
-            rec.calls.append(("subm_conv", 2.0 * (n + smap.num_pairs) * cin * cout,
+            scratch = torch.empty(n, cout, device=x.device, dtype=torch.float32)
+            npairs = smap.lists(True).num_pairs if smap.centre_pref else n + smap.num_pairs
+            rec.calls.append(("subm_conv", 2.0 * npairs * cin * cout,
                               lambda: rec._conv(x, smap, weight, bias, out=scratch, **kw), (n, cout, cin)))
             return o
 
