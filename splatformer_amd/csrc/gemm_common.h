@@ -181,4 +181,37 @@ using sfx::split2h;  // fp32 -> two fp16 terms of the scaled value (common.h)
 
 enum Mode { MODE_DENSE = 0, MODE_GATHER1 = 1, MODE_GATHERS = 2, MODE_PAIR = 3 };
 
+// CUs of the current device (cached per process)
+inline int num_cus() {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+  }
+  return cus;
+}
+
+// M-tiles of a launch: plain ceil(M / BM), or per-slice rounding in pair mode (fills slice_tile_off)
+inline int tiles_m_of(GemmArgs& a, int BM) {
+  if (!a.pair_mode) return (int)sfx::ceil_div(a.M, BM);
+  int t = 0;
+  for (int k = 0; k < a.num_slices; ++k) {
+    a.slice_tile_off[k] = t;
+    t += (a.slice_pair_off[k + 1] - a.slice_pair_off[k] + BM - 1) / BM;
+  }
+  a.slice_tile_off[a.num_slices] = t;
+  return t;
+}
+
+// Launchers of gemm_kernel (gemm_kernel.h), one translation unit per operand mode and wave count
+// (gemm_k<mode><4|8>.hip, compiled in parallel): cfg indexes gemm.hip's kCfgs (0-4 four-wave, 5-6 eight-wave).
+void launch_m0_w4(int cfg, const GemmArgs& a, int groups, bool vec, hipStream_t st);
+void launch_m0_w8(int cfg, const GemmArgs& a, int groups, bool vec, hipStream_t st);
+void launch_m1_w4(int cfg, const GemmArgs& a, int groups, bool vec, hipStream_t st);
+void launch_m1_w8(int cfg, const GemmArgs& a, int groups, bool vec, hipStream_t st);
+void launch_m2_w4(int cfg, const GemmArgs& a, int groups, bool vec, hipStream_t st);
+void launch_m3_w4(int cfg, const GemmArgs& a, int groups, bool vec, hipStream_t st);
+void launch_m3_w8(int cfg, const GemmArgs& a, int groups, bool vec, hipStream_t st);
+
 }  // namespace sfxg
