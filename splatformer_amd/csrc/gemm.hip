@@ -322,6 +322,8 @@ void dispatch_mode(GemmArgs a, int groups, bool vec, hipStream_t st) {
 
 void dispatch(const GemmArgs& a0, int groups, bool vec, hipStream_t st) {
   GemmArgs a = a0;
+  static const int dbg = getenv("SFX_GEMM_DEBUG") ? atoi(getenv("SFX_GEMM_DEBUG")) : 0;  // timing ablations
+  a.dbg = dbg;
   a.split = vec ? split_mode(a.K) : 0;
   // fp16x2 needs the pre-split W (per-row scales of A' are chosen in the kernel); without one the launch runs the
   // range-safe bf16x3 form.

@@ -97,6 +97,9 @@ struct GemmArgs {
   long long slice_winv_stride;  // pair mode: winv offset per slice (row-sliced weights, e.g. the conv backward)
   int tuned, tuned_sk;  // measured tile configuration + 1 (0: cost model / table) and its Stream-K flag
   int pair_store;  // pair mode: store each pair's row at row `pair index` of Y instead of adding into pair_out
+  // timing ablations only (SFX_GEMM_DEBUG, results wrong): bit 0 no MFMAs, 1 no operand loads (out-of-range
+  // offsets), 2 no epilogue, 3 no LDS staging (split + writes)
+  int dbg;
 };
 
 // fp16x2 row exponent: a row with maximum m is scaled by 2^e so that m * 2^e lies in [2^12, 2^13)

@@ -184,7 +184,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs
   auto load_tiles = [&](const Tile& ti, int kt, bool first) {
     const __amdgpu_buffer_rsrc_t rW = rsrc(ti.W);
     const int k = kt * BK + lcol;
-    const bool kin = k < K;
+    const bool kin = k < K && !(p.dbg & 2);
     int seg = 0, kk = k;
     if constexpr (MODE == MODE_GATHERS) {
       seg = k / p.Kseg;
@@ -238,6 +238,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs
   int sp = 0;  // segment parity (the s_inv copy of the current segment)
   // par: parity of the segment whose rows are staged (selects its s_inv copy)
   auto store_tiles = [&](int buf, bool first, int par) {
+    if (p.dbg & 8) return;
     if constexpr (SPLIT) {
       const int b = NBUF == 2 ? buf : 0;
       if constexpr (F16) {
@@ -494,6 +495,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs
   };
 
   auto epilogue = [&](const Tile& ti, bool partial, bool owner0) {
+    if (p.dbg & 4) return;
     if constexpr (F16) {  // undo the row scales of A' and W (powers of two: exact)
 #pragma unroll
       for (int a = 0; a < MB; ++a)
@@ -696,6 +698,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(GemmArgs
     }
   };
   auto compute = [&](int buf) {
+    if (p.dbg & 1) return;
     if constexpr (F16) {  // a later slab lowered some rows' scales: rescale their accumulators first
       ++cq;
       const int b = NBUF == 2 ? buf : 0;

@@ -151,6 +151,25 @@ __device__ __forceinline__ void add_pair_partials(float4 (&v)[NV], const float* 
   constexpr int C = 4 * G * NV;
   const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(P), (short)0, 0x7ffffff0,
                                                                       0x00020000);
+  if constexpr (G == 64 && NV == 1) {
+    // one row per wave: the row's 27 pair positions are wave-uniform -- scalar loads (all first, so they batch),
+    // then the 27 row loads back to back (absent offsets through an out-of-range offset: no branch, whose join
+    // would make hipcc wait for every load before it)
+    const int rowu = __builtin_amdgcn_readfirstlane(row);
+    const int* pr = pos + 27ll * rowu;
+    int q[27];
+#pragma unroll
+    for (int k = 0; k < 27; ++k) q[k] = __builtin_amdgcn_readfirstlane(pr[k]);
+    float4 a[27];
+#pragma unroll
+    for (int k = 0; k < 27; ++k) {
+      const unsigned off = q[k] >= 0 ? ((unsigned)q[k] * (unsigned)C + 4u * (unsigned)sub) * 4u : 0x7ffffff0u;
+      a[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rp, off, 0, 0));
+    }
+#pragma unroll
+    for (int k = 0; k < 27; ++k) v[0] = make_float4(v[0].x + a[k].x, v[0].y + a[k].y, v[0].z + a[k].z, v[0].w + a[k].w);
+    return;
+  }
   int q[27];
 #pragma unroll
   for (int k = 0; k < 27; ++k) q[k] = pos[27ll * row + k];
