@@ -382,6 +382,14 @@ int sfx_subm_pairs(int n, const int* nbr, void* ws, size_t ws_bytes, int* pair_i
  * num_pairs = pair_off[27]. */
 int sfx_subm_pair_pos(int n, long long num_pairs, const int* pair_out, const int* pair_off, int* pair_pos,
                       void* stream);
+/* (ABI v16) sfx_subm_pairs' lists -- the same pair_in / pair_out / pair_off, bit for bit -- and, when pair_pos is not
+ * null, sfx_subm_pair_pos's inverted index, in two passes over nbr: per-workgroup (256 points) pair counts of every
+ * offset, one scan of those 27 * ceil(n / 256) counts, then each workgroup writes its pairs (wave ballots keep the
+ * output rows ascending within an offset) and its rows of pair_pos.  No host value is needed (sfx_subm_pair_pos needs
+ * num_pairs). */
+size_t sfx_subm_pair_lists_workspace_bytes(int n);
+int sfx_subm_pair_lists(int n, const int* nbr, void* ws, size_t ws_bytes, int* pair_in, int* pair_out, int* pair_off,
+                        int* pair_pos, int with_centre, void* stream);
 /* spconv SubMConv3d(Cin, Cout, 3, bias) forward on the pair lists: out = bias + x[nbr[:,13]] W_13^T (dense centre
  * GEMM, plain stores), then one fp32 MFMA launch over the 26 other offsets' gathered rows whose partial products
  * are atomically added into out (float atomics: summation order across offsets is not fixed).

@@ -309,7 +309,7 @@ extern "C" {
 
 const char* sfx_last_error(void) { return sfx::g_err; }
 
-int sfx_abi_version(void) { return 15; }
+int sfx_abi_version(void) { return 16; }
 
 long long sfx_lookback_timeouts(void* stream) { return sfx::lookback_timeouts(sfx::as_stream(stream)); }
 

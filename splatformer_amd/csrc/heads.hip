@@ -18,6 +18,9 @@
 // registers: the input row's fragments (kept for all heads) for the first layer, the previous layer's accumulator
 // registers for the others (a 32x32 accumulator's registers 8s..8s+7 are the k-step-s B fragment with the k order
 // permuted, cdna_hip_programming.md §3 -- sfx_heads_pack lays the weights out in that order).
+#include <cstdlib>
+#include <cstring>
+
 #include "gemm_common.h"
 
 namespace {
@@ -63,10 +66,12 @@ __host__ __device__ constexpr int b4_off(int out_dim) { return W4_OFF + out_dim 
 template <int KP>
 __global__ void __launch_bounds__(WAVES * 64, 1)
 heads_kernel(int M, const float* __restrict__ X, long long ldx, const float* __restrict__ stream,
-             const float* __restrict__ par, int npar, HeadsArgs a, float* __restrict__ Y) {
+             const float* __restrict__ par, int npar, HeadsArgs a, float* __restrict__ Y, int gper) {
   constexpr int NT = KP / 16;       // 16-deep k-steps of the input
   constexpr int KC0 = KP / 32;      // first-layer k-chunks (phases)
   constexpr int PPH = KC0 + 8;      // phases per head
+  // heads [g0, g1) of this workgroup's points (blockIdx.y: head group; disjoint output columns, no combine)
+  const int g0 = (int)blockIdx.y * gper, g1 = min(a.ng, g0 + gper);
   __shared__ __attribute__((aligned(16))) char lds[RING * PHASE];
   extern __shared__ float s_par[];  // npar floats (dynamic LDS)
 
@@ -74,7 +79,7 @@ heads_kernel(int M, const float* __restrict__ X, long long ldx, const float* __r
   const int h = lane >> 5, r32 = lane & 31;
   const int prow = (int)blockIdx.x * (WAVES * 32) + wid * 32 + r32;
   const bool pok = prow < M;
-  const int NP = a.ng * PPH;
+  const int P0 = g0 * PPH, NP = g1 * PPH;  // this workgroup's phases of the weight stream
 
   const char* gstream = reinterpret_cast<const char*>(stream);
   auto issue = [&](int q) {
@@ -87,7 +92,7 @@ heads_kernel(int M, const float* __restrict__ X, long long ldx, const float* __r
   };
 #pragma unroll
   for (int q = 0; q < RING - 1; ++q)
-    if (q < NP) issue(q);
+    if (P0 + q < NP) issue(P0 + q);
 
   for (int i = tid; i < npar; i += WAVES * 64) s_par[i] = par[i];
 
@@ -140,8 +145,8 @@ heads_kernel(int M, const float* __restrict__ X, long long ldx, const float* __r
     return __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, c, 0, 0, 0);
   };
 
-  int p = 0;
-  for (int g = 0; g < a.ng; ++g) {
+  int p = P0;
+  for (int g = g0; g < g1; ++g) {
 #pragma unroll
     for (int L = 0; L < 3; ++L) {  // (unrolled: the fragment arrays are indexed by compile-time k-chunks)
 #pragma unroll
@@ -363,12 +368,30 @@ int sfx_heads(int M, int ng, int kin, int out_dim, const float* x, long long ldx
   SFX_REQUIRE(a.ocol[0] == 0 && a.ocol[ng] == out_dim, "sfx_heads: column table");
   const int npar = (int)sfx_heads_params_floats(out_dim);
   hipStream_t st = sfx::as_stream(stream_);
-  const unsigned grid = sfx::ceil_div(M, WAVES * 32);
+  const unsigned blocks = sfx::ceil_div(M, WAVES * 32);
+  // one workgroup per CU: a launch of B point blocks takes ceil(B / CUs) rounds; splitting every block's heads into S
+  // groups (grid.y) makes the rounds S times shorter, so the last, partly empty round costs 1/S of one (config B:
+  // 391 blocks = 1.53 rounds -> 2 at S = 1, 5 / 3 at S = 3).  Each group re-reads and re-splits its input rows and
+  // stages the parameters again: S is the smallest that reaches the best rounds x (1 / S) + 2 % per extra group.
+  const int cus = num_cus();
+  static const bool split_on = !(getenv("SFX_HEADS_SPLIT") && !strcmp(getenv("SFX_HEADS_SPLIT"), "0"));
+  int S = 1;
+  double best = 1e30;
+  for (int s = 1; s <= (split_on ? ng : 1); ++s) {
+    if (ng % s) continue;
+    const double cost = (double)sfx::ceil_div((long long)blocks * s, cus) / s * (1.0 + 0.02 * (s - 1));
+    if (cost < best - 1e-9) {
+      best = cost;
+      S = s;
+    }
+  }
+  const int gper = ng / S;
+  const dim3 grid(blocks, (unsigned)S);
   const size_t dyn = (size_t)npar * 4;
   if (kin <= 128)
-    heads_kernel<128><<<grid, WAVES * 64, dyn, st>>>(M, x, ldx, stream, params, npar, a, y);
+    heads_kernel<128><<<grid, WAVES * 64, dyn, st>>>(M, x, ldx, stream, params, npar, a, y, gper);
   else
-    heads_kernel<160><<<grid, WAVES * 64, dyn, st>>>(M, x, ldx, stream, params, npar, a, y);
+    heads_kernel<160><<<grid, WAVES * 64, dyn, st>>>(M, x, ldx, stream, params, npar, a, y, gper);
   return sfx::check_launch("sfx_heads");
 }
 

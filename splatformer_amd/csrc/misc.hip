@@ -12,7 +12,7 @@ namespace {
 // Packed elements (row i, column c of the 14 + rest_dim wide record) in a grid-stride loop, columns fastest: the
 // record rows are written as contiguous runs and each source attribute is read in row order (one thread per Gaussian
 // wrote 59 strided floats per lane at config E: 0.33 ms for 0.24 GB).  A bounded grid keeps the grid-max atomics to
-// one per wave (one per element-wave would serialise 460k atomics on one word).
+// one per workgroup (one per element-wave would serialise 460k atomics on one word).
 __global__ void __launch_bounds__(256) gs_pack_kernel(int n, const float* __restrict__ means, long long ld_m,
                                                       const float* __restrict__ scales, long long ld_s,
                                                       const float* __restrict__ opac, long long ld_o,
@@ -41,9 +41,15 @@ __global__ void __launch_bounds__(256) gs_pack_kernel(int n, const float* __rest
       mx = max(mx, g);
     }
   }
-  if (grid_coord && grid_max) {  // all lanes reach this: wave-reduce, one atomic per wave
+  if (grid_coord && grid_max) {  // all lanes reach this: wave-reduce, then one atomic per workgroup
+    __shared__ int wmx[4];
     mx = sfx::wave_max_i(mx);
-    if ((threadIdx.x & 63) == 0 && mx > 0) atomicMax(grid_max, mx);
+    if ((threadIdx.x & 63) == 0) wmx[threadIdx.x >> 6] = mx;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      mx = max(max(wmx[0], wmx[1]), max(wmx[2], wmx[3]));
+      if (mx > 0) atomicMax(grid_max, mx);
+    }
   }
 }
 
@@ -141,7 +147,9 @@ int sfx_gs_pack(int n, const float* means, long long ld_means, const float* scal
   SFX_REQUIRE(ld_feat >= 14 + rest_dim, "sfx_gs_pack: ld_feat too small");
   SFX_REQUIRE((long long)n * (14 + rest_dim) < (1ll << 31), "sfx_gs_pack: n * record width must fit int32");
   const unsigned blocks = sfx::ceil_div((long long)n * (14 + rest_dim), 256);
-  gs_pack_kernel<<<blocks < 2048u ? blocks : 2048u, 256, 0, sfx::as_stream(stream)>>>(
+  // two workgroups per CU: same-address atomics serialise at L2, so the grid-max costs one per workgroup (2048
+  // workgroups x 4 waves took ~0.1 ms at config B for ~10 us of copying)
+  gs_pack_kernel<<<blocks < 512u ? blocks : 512u, 256, 0, sfx::as_stream(stream)>>>(
       n, means, ld_means, scales, ld_scales, opacities, ld_opacities, quats, ld_quats, features_dc, ld_dc,
       features_rest, ld_rest, rest_dim, grid_resolution, feat, ld_feat, grid_coord, grid_max);
   return sfx::check_launch("sfx_gs_pack");

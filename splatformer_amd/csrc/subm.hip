@@ -137,6 +137,63 @@ __global__ void subm_pair_pos_kernel(long long num_pairs, const int* __restrict_
   pair_pos[27ll * pair_out[p] + k] = (int)p;
 }
 
+// ---- pair lists by block counts (sfx_subm_pair_lists) ----------------------------------------------------------
+// Workgroup b owns points [256 b, 256 b + 256) and reads each point's 27 neighbours once (row-major, the layout nbr is
+// written in).  Pass 1 counts the pairs of every (offset k, workgroup b); one scan over those 27 x nb counts gives
+// each (k, b) its first slot; pass 2 writes the pairs at that slot + the wave's offset + the lane's rank (ballot +
+// mbcnt), so within an offset the pairs stay in ascending output order, and writes the inverted index pair_pos
+// [n][27] on the way.  (The flag / scan / fill form scanned 27 n flags and read nbr transposed.)
+__device__ __forceinline__ bool pair_flag(const int* row, int k, bool in, int with_centre) {
+  return in && (k != 13 || with_centre) && row[k] >= 0;
+}
+__global__ void __launch_bounds__(256) subm_pair_count_kernel(int n, const int* __restrict__ nbr,
+                                                              int* __restrict__ counts, int nb, int with_centre) {
+  __shared__ int wc[27][4];
+  const int i = blockIdx.x * 256 + threadIdx.x, lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const bool in = i < n;
+  const int* row = nbr + 27ll * (in ? i : 0);
+#pragma unroll
+  for (int k = 0; k < 27; ++k) {
+    const unsigned long long bal = __ballot(pair_flag(row, k, in, with_centre));
+    if (lane == 0) wc[k][wid] = __popcll(bal);
+  }
+  __syncthreads();
+  if (threadIdx.x < 27) {
+    const int k = threadIdx.x;
+    counts[(long long)k * nb + blockIdx.x] = wc[k][0] + wc[k][1] + wc[k][2] + wc[k][3];
+  }
+}
+__global__ void __launch_bounds__(256) subm_pair_write_kernel(int n, const int* __restrict__ nbr,
+                                                              const int* __restrict__ first, int nb, int with_centre,
+                                                              int* __restrict__ pair_in, int* __restrict__ pair_out,
+                                                              int* __restrict__ pair_off, int* __restrict__ pair_pos) {
+  __shared__ int wc[27][4];
+  const int i = blockIdx.x * 256 + threadIdx.x, lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const bool in = i < n;
+  const int* row = nbr + 27ll * (in ? i : 0);
+  unsigned long long bal[27];
+#pragma unroll
+  for (int k = 0; k < 27; ++k) {
+    bal[k] = __ballot(pair_flag(row, k, in, with_centre));
+    if (lane == 0) wc[k][wid] = __popcll(bal[k]);
+  }
+  __syncthreads();
+  if (blockIdx.x == 0 && threadIdx.x < 27) pair_off[threadIdx.x] = first[(long long)threadIdx.x * nb];
+#pragma unroll
+  for (int k = 0; k < 27; ++k) {
+    int base = first[(long long)k * nb + blockIdx.x];
+    for (int w = 0; w < wid; ++w) base += wc[k][w];
+    const unsigned rank = __builtin_amdgcn_mbcnt_hi((unsigned)(bal[k] >> 32),
+                                                    __builtin_amdgcn_mbcnt_lo((unsigned)bal[k], 0u));
+    const bool fl = (bal[k] >> lane) & 1ull;
+    const int p = base + (int)rank;
+    if (fl) {
+      pair_out[p] = i;
+      pair_in[p] = row[k];
+    }
+    if (pair_pos && in) pair_pos[27ll * i + k] = fl ? p : -1;
+  }
+}
 }  // namespace
 
 extern "C" int sfx_scan_i32(long long n, const int32_t* in, int32_t* out, int inclusive, void* ws, size_t ws_bytes,
@@ -198,6 +255,35 @@ int sfx_subm_pairs(int n, const int* nbr, void* ws, size_t ws_bytes, int* pair_i
   return sfx::check_launch("sfx_subm_pairs");
 }
 
+// sfx_subm_pairs' lists (same order, same pair_off) plus, when pair_pos is not null, the inverted index pair_pos [n][27]
+// of sfx_subm_pair_pos -- by per-workgroup counts (two passes over nbr, a scan of 27 * ceil(n / 256) counts)
+size_t sfx_subm_pair_lists_workspace_bytes(int n) {
+  const long long e = 27ll * sfx::ceil_div(n > 0 ? n : 1, 256);
+  return (size_t)(2 * e * sizeof(int) + 256) + sfx_scan_workspace_bytes(e);
+}
+int sfx_subm_pair_lists(int n, const int* nbr, void* ws, size_t ws_bytes, int* pair_in, int* pair_out, int* pair_off,
+                        int* pair_pos, int with_centre, void* stream) {
+  SFX_REQUIRE(n >= 0, "sfx_subm_pair_lists: n < 0");
+  SFX_REQUIRE(ws_bytes >= sfx_subm_pair_lists_workspace_bytes(n), "sfx_subm_pair_lists: workspace too small");
+  SFX_REQUIRE(pair_off, "sfx_subm_pair_lists: null pair_off");
+  hipStream_t st = sfx::as_stream(stream);
+  if (n == 0) {
+    hipMemsetAsync(pair_off, 0, 28 * sizeof(int), st);
+    return sfx::check_launch("sfx_subm_pair_lists");
+  }
+  SFX_REQUIRE(nbr && ws && pair_in && pair_out, "sfx_subm_pair_lists: null buffer");
+  const int nb = (int)sfx::ceil_div(n, 256);
+  const long long e = 27ll * nb;
+  int* counts = reinterpret_cast<int*>(ws);
+  int* first = counts + e;
+  char* scan_ws = reinterpret_cast<char*>(first + e);
+  scan_ws += (256 - (reinterpret_cast<uintptr_t>(scan_ws) & 255)) & 255;
+  subm_pair_count_kernel<<<nb, 256, 0, st>>>(n, nbr, counts, nb, with_centre);
+  const int rc = sfx_scan_i32(e, counts, first, 0, scan_ws, sfx_scan_workspace_bytes(e), pair_off + 27, stream);
+  if (rc) return rc;
+  subm_pair_write_kernel<<<nb, 256, 0, st>>>(n, nbr, first, nb, with_centre, pair_in, pair_out, pair_off, pair_pos);
+  return sfx::check_launch("sfx_subm_pair_lists");
+}
 // pair_pos [n][27]: for output row i and offset k, the index of pair (k, i) in pair_in/pair_out (-1: no pair);
 // pair_off (device, 28 ints) as written by sfx_subm_pairs, num_pairs = pair_off[27]
 int sfx_subm_pair_pos(int n, long long num_pairs, const int* pair_out, const int* pair_off, int* pair_pos,

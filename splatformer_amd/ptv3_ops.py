@@ -49,6 +49,8 @@ _lib.register("sfx_subm_conv", [I, I, I, P, L, P, P, P, P, P, P, P, L, P, I, P, 
 _lib.register("sfx_subm_conv_partials", [I, I, I, P, L, P, P, P, P, P, P, P, L, P, L, P, P, P])
 _lib.register("sfx_subm_conv_partials_pairs", [I, I, I, P, L, P, P, P, P, P, P, P, L, P, L, P, P, P])
 _lib.register("sfx_subm_pair_pos", [I, L, P, P, P, P])
+_lib.register("sfx_subm_pair_lists_workspace_bytes", [I], Z)
+_lib.register("sfx_subm_pair_lists", [I, P, P, Z, P, P, P, P, I, P])
 _lib.register("sfx_subm_cpe_pack_bytes", [I], Z)
 _lib.register("sfx_subm_cpe_pack", [I, P, P, P, P, P])
 _lib.register("sfx_subm_cpe_ln", [I, I, P, P, P, P, P, P, P, P, P, P, P, P, F, P, P, P])
@@ -745,6 +747,9 @@ def segment_mean(x: Tensor, idx_ptr: Tensor, sorted_idx: Tensor, m: int) -> Tens
     return out
 
 
+PAIR_LISTS = os.environ.get("SFX_PAIR_LISTS", "1") != "0"  # 0: the older flag / scan / fill pair builder
+
+
 class PairLists:
     """Offset-major SubM pair lists of one map (sfx_subm_pairs): pair_in / pair_out, the 28 per-offset prefixes (read
     back asynchronously; the first conv that needs them waits for that copy only) and the inverted index pair_pos.
@@ -758,14 +763,21 @@ class PairLists:
         self.pair_in = torch.empty(cap, device=dev, dtype=torch.int32)
         self.pair_out = torch.empty(cap, device=dev, dtype=torch.int32)
         self.off_dev = torch.empty(28, device=dev, dtype=torch.int32)
-        ws = _lib.workspace(_lib.fn("sfx_subm_pairs_workspace_bytes")(n), dev)
-        call("sfx_subm_pairs", n, ptr(nbr), ptr(ws), ws.numel(), ptr(self.pair_in), ptr(self.pair_out),
-             ptr(self.off_dev), 1 if centre else 0, stream())
+        if PAIR_LISTS:
+            # lists and the inverted index pair_pos in one call (ABI v16: per-workgroup counts, no host value needed)
+            self._pos = torch.empty(max(1, n), 27, device=dev, dtype=torch.int32)
+            ws = _lib.workspace(_lib.fn("sfx_subm_pair_lists_workspace_bytes")(n), dev)
+            call("sfx_subm_pair_lists", n, ptr(nbr), ptr(ws), ws.numel(), ptr(self.pair_in), ptr(self.pair_out),
+                 ptr(self.off_dev), ptr(self._pos), 1 if centre else 0, stream())
+        else:  # the v6 / v15 pair (flags over [27][n] + scan + fill; pair_pos on first use, after the offsets read)
+            self._pos = None
+            ws = _lib.workspace(_lib.fn("sfx_subm_pairs_workspace_bytes")(n), dev)
+            call("sfx_subm_pairs", n, ptr(nbr), ptr(ws), ws.numel(), ptr(self.pair_in), ptr(self.pair_out),
+                 ptr(self.off_dev), 1 if centre else 0, stream())
         self._rd = _lib.HostRead(self.off_dev)
         self._n = n
         self._off = None
         self._off_c = None
-        self._pos = None
 
     def off_ready(self) -> bool:
         return self._off is not None
@@ -788,7 +800,8 @@ class PairLists:
 
     @property
     def pair_pos(self) -> Tensor:
-        """[n, 27] inverted pair index (sfx_subm_pair_pos), built once per list."""
+        """[n, 27] inverted pair index (written with the lists by sfx_subm_pair_lists; SFX_PAIR_LISTS=0: built on
+        first use by sfx_subm_pair_pos)."""
         if self._pos is None:
             pos = torch.empty(self._n, 27, device=self.pair_in.device, dtype=torch.int32)
             call("sfx_subm_pair_pos", self._n, self.num_pairs, ptr(self.pair_out), ptr(self.off_dev), ptr(pos),

@@ -25,7 +25,7 @@ def test_library_exports_all_declared_symbols():
     lib = _lib.load()
     missing = [s for s in declared_symbols() if not hasattr(lib, s)]
     assert not missing, f"libsfx.so lacks: {missing}"
-    assert lib.sfx_abi_version() == 15
+    assert lib.sfx_abi_version() == 16
 
 
 def test_python_signatures_cover_header():

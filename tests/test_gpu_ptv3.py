@@ -199,6 +199,41 @@ def test_linear_gather_is_subm_conv(device):
         assert rel_l2(y2.cpu(), ref2) < 2e-6
 
 
+@pytest.mark.parametrize("n", [1, 255, 256, 257, 6000, 70000])
+@pytest.mark.parametrize("centre", [False, True])
+def test_subm_pair_lists_match_flag_scan(device, n, centre):
+    """sfx_subm_pair_lists (ABI v16: per-workgroup counts + one scan of 27 ceil(n/256) counts, pair_pos written with
+    the lists) equals sfx_subm_pairs + sfx_subm_pair_pos (flags over [27][n], one scan, fill) bit for bit -- lists,
+    per-offset prefixes and the inverted index -- on ragged n (one point, workgroup edges) with duplicate voxels."""
+    from splatformer_amd import _lib
+    from splatformer_amd.ptv3_ops import call, ptr, stream
+    s = make_scene(n, 1, seed=7, unique_voxels=False)
+    grid = torch.floor(s["means"] * 256).int().to(device)
+    nbr = ops.subm_neighbors(grid, None, with_pairs=False).nbr
+    cap = max(1, 27 * n)
+    res = []
+    for new in (False, True):
+        pin = torch.full((cap,), -7, device=device, dtype=torch.int32)
+        pout = torch.full((cap,), -7, device=device, dtype=torch.int32)
+        off = torch.empty(28, device=device, dtype=torch.int32)
+        pos = torch.empty(n, 27, device=device, dtype=torch.int32)
+        if new:
+            ws = _lib.workspace(_lib.fn("sfx_subm_pair_lists_workspace_bytes")(n), device)
+            call("sfx_subm_pair_lists", n, ptr(nbr), ptr(ws), ws.numel(), ptr(pin), ptr(pout), ptr(off), ptr(pos),
+                 1 if centre else 0, stream())
+        else:
+            ws = _lib.workspace(_lib.fn("sfx_subm_pairs_workspace_bytes")(n), device)
+            call("sfx_subm_pairs", n, ptr(nbr), ptr(ws), ws.numel(), ptr(pin), ptr(pout), ptr(off),
+                 1 if centre else 0, stream())
+            call("sfx_subm_pair_pos", n, int(off[27].item()), ptr(pout), ptr(off), ptr(pos), stream())
+        torch.cuda.synchronize()
+        res.append((pin.cpu(), pout.cpu(), off.cpu(), pos.cpu()))
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
+    off = res[1][2]
+    assert int(off[27]) == int(((nbr >= 0).sum() - (0 if centre else (nbr[:, 13] >= 0).sum())).item())
+
+
 @pytest.mark.parametrize("centre,unique", [(False, True), (True, True), (True, False)])
 def test_subm_conv_partials_atomic_free(device, centre, unique):
     """Atomic-free SubM conv (sfx_subm_conv_partials + sfx_subm_pair_pos + sfx_cpe_residual_ln_pairs): the inverted
