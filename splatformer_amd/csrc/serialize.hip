@@ -9,6 +9,9 @@
 // and a finalize pass writes order/inverse.  Pooling sorts code[0] by its
 // bits above 3*pooling_depth (== torch.unique + sort(cluster)), marks run
 // heads, scans them into cluster ids and reduces features per run.
+#include <cstdlib>
+#include <cstring>
+
 #include "common.h"
 
 namespace {
@@ -193,6 +196,34 @@ __global__ void pool_gather_kernel(int m, int n, int R, const int* __restrict__ 
 }
 
 // max over each run of X rows (X = proj(feat), [n, C]) -> BN affine -> act   (segment_csr 'max' + norm + act)
+// One wave per cluster, four clusters per workgroup, lanes over 4-column groups (C % 4 == 0, 16-byte rows): the
+// one-workgroup-per-cluster form launched 15k-90k workgroups of 64-256 threads for runs of 1-8 rows.
+__global__ void __launch_bounds__(256) segment_max_affine_act4_kernel(int m, int C, const int* __restrict__ idx_ptr,
+                                                                      const int* __restrict__ sorted_idx,
+                                                                      const float* __restrict__ X,
+                                                                      const float* __restrict__ scale,
+                                                                      const float* __restrict__ shift, int act,
+                                                                      float* __restrict__ Y) {
+  const int c = (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (c >= m) return;
+  const int beg = __builtin_amdgcn_readfirstlane(idx_ptr[c]), end = __builtin_amdgcn_readfirstlane(idx_ptr[c + 1]);
+  for (int g = lane; 4 * g < C; g += 64) {
+    float4 v = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+    for (int p = beg; p < end; ++p) {
+      const int row = __builtin_amdgcn_readfirstlane(sorted_idx[p]);
+      const float4 x = *reinterpret_cast<const float4*>(X + (long long)row * C + 4 * g);
+      v = make_float4(fmaxf(v.x, x.x), fmaxf(v.y, x.y), fmaxf(v.z, x.z), fmaxf(v.w, x.w));
+    }
+    float o[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (scale) o[j] = o[j] * scale[4 * g + j] + shift[4 * g + j];
+      if (act == 1) o[j] = 0.5f * o[j] * (1.f + erff(o[j] * 0.70710678118654752f));
+    }
+    *reinterpret_cast<float4*>(Y + (long long)c * C + 4 * g) = make_float4(o[0], o[1], o[2], o[3]);
+  }
+}
+
 __global__ void segment_max_affine_act_kernel(int m, int C, const int* __restrict__ idx_ptr,
                                               const int* __restrict__ sorted_idx, const float* __restrict__ X,
                                               const float* __restrict__ scale, const float* __restrict__ shift,
@@ -357,6 +388,12 @@ int sfx_segment_max_affine_act(int m, int C, const int* idx_ptr, const int* sort
   SFX_REQUIRE(m >= 0 && C > 0 && (act == 0 || act == 1), "sfx_segment_max_affine_act: bad args");
   if (m == 0) return SFX_OK;
   SFX_REQUIRE(idx_ptr && sorted_idx && X && Y, "sfx_segment_max_affine_act: null buffer");
+  static const bool v4 = !(getenv("SFX_SEGMAX4") && !strcmp(getenv("SFX_SEGMAX4"), "0"));
+  if (v4 && C % 4 == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0 && (reinterpret_cast<uintptr_t>(Y) & 15) == 0) {
+    segment_max_affine_act4_kernel<<<sfx::ceil_div(m, 4), 256, 0, sfx::as_stream(stream)>>>(
+        m, C, idx_ptr, sorted_idx, X, scale, shift, act, Y);
+    return sfx::check_launch("sfx_segment_max_affine_act");
+  }
   const int threads = C >= 256 ? 256 : (C >= 128 ? 128 : 64);
   segment_max_affine_act_kernel<<<m, threads, 0, sfx::as_stream(stream)>>>(m, C, idx_ptr, sorted_idx, X, scale,
                                                                           shift, act, Y);

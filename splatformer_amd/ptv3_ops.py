@@ -816,7 +816,7 @@ class SubmMap:
     (subm_cpe_ln) reads nbr only.  Two kinds of lists: without the centre offset (the atomic conv, the training
     backward) and with it (centre_pref: the eval conv's single pair launch)."""
 
-    def __init__(self, nbr: Tensor, mask: Tensor, centre_pref: bool = False):
+    def __init__(self, nbr: Tensor, mask: Optional[Tensor], centre_pref: bool = False):
         self.nbr, self.mask = nbr, mask
         self.centre_pref = centre_pref
         self._lists = {}
@@ -876,6 +876,9 @@ class SubmMap:
         return self.lists(False).num_pairs
 
 
+SUBM_MASK = os.environ.get("SFX_SUBM_MASK", "0") == "1"
+
+
 def subm_neighbors(grid_coord: Tensor, batch: Optional[Tensor], with_pairs: bool = True, centre: bool = False):
     """27-neighbour map; with_pairs also builds the offset-major pair lists (their offsets read back asynchronously):
     with the centre offset when `centre` (the eval forward's maps), else without."""
@@ -885,7 +888,9 @@ def subm_neighbors(grid_coord: Tensor, batch: Optional[Tensor], with_pairs: bool
     tk = torch.empty(1 << l2, device=dev, dtype=torch.int64)
     tv = torch.empty(1 << l2, device=dev, dtype=torch.int32)
     nbr = torch.empty(n, 27, device=dev, dtype=torch.int32)
-    mask = torch.empty(n, device=dev, dtype=torch.int32)
+    # no neighbour bitmask by default: nothing reads it (the fused conv's row order comes from nbr,
+    # sfx_subm_order_keys), and the query would pay one atomicOr per present neighbour for it (SFX_SUBM_MASK=1: built)
+    mask = torch.empty(n, device=dev, dtype=torch.int32) if SUBM_MASK else None
     call("sfx_subm_neighbors", n, ptr(grid_coord, torch.int32), ptr(batch), l2, ptr(tk), ptr(tv), ptr(nbr), ptr(mask),
          None, stream())
     smap = SubmMap(nbr, mask, centre_pref=centre)

@@ -199,6 +199,27 @@ def test_linear_gather_is_subm_conv(device):
         assert rel_l2(y2.cpu(), ref2) < 2e-6
 
 
+@pytest.mark.parametrize("C", [64, 96, 128, 256, 512, 30])
+def test_segment_max_affine_act(device, C):
+    """Pooling's segment max -> BN affine -> GELU (sfx_segment_max_affine_act; one wave per cluster for C % 4 == 0,
+    the per-cluster workgroup form for C = 30) against torch: runs of 1-8 rows in a permuted order, ragged m."""
+    g = torch.Generator().manual_seed(C)
+    m = 5003
+    lens = torch.randint(1, 9, (m,), generator=g)
+    idx_ptr = torch.zeros(m + 1, dtype=torch.int64)
+    idx_ptr[1:] = torch.cumsum(lens, 0)
+    n = int(idx_ptr[-1])
+    sidx = torch.randperm(n, generator=g)
+    x = torch.randn(n, C, generator=g)
+    sc, sh = torch.rand(C, generator=g) + 0.5, torch.randn(C, generator=g)
+    y = ops.segment_max_affine_act(x.to(device), idx_ptr.int().to(device), sidx.int().to(device), m, sc.to(device),
+                                   sh.to(device), ops.ACT_GELU)
+    seg = torch.repeat_interleave(torch.arange(m), lens)
+    mx = torch.full((m, C), -float("inf")).scatter_reduce(0, seg[:, None].expand(n, C), x[sidx], "amax")
+    ref = torch.nn.functional.gelu(mx * sc + sh)
+    assert rel_l2(y.cpu(), ref) < 1e-6
+
+
 @pytest.mark.parametrize("n", [1, 255, 256, 257, 6000, 70000])
 @pytest.mark.parametrize("centre", [False, True])
 def test_subm_pair_lists_match_flag_scan(device, n, centre):
