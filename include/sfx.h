@@ -283,6 +283,13 @@ int sfx_cpe_residual_ln_pairs(int M, int C, const float* T, long long ldt, const
                               long long num_pairs, const float* X, const float* gamma_cpe, const float* beta_cpe,
                               const float* gamma1, const float* beta1, float eps, float* X_out, float* H,
                               void* stream);
+/* (ABI v16) sfx_cpe_residual_ln_pairs reading the compacted positions pair_cpos [M][32] of sfx_subm_pair_lists:
+ * the same sums in the same order (absent offsets add +0 in both), ceil(max count / 8) groups of 8 row loads per wave
+ * instead of 27 position and 27 row loads per row. */
+int sfx_cpe_residual_ln_cpairs(int M, int C, const float* T, long long ldt, const float* partials,
+                               const int* pair_cpos, long long num_pairs, const float* X, const float* gamma_cpe,
+                               const float* beta_cpe, const float* gamma1, const float* beta1, float eps, float* X_out,
+                               float* H, void* stream);
 /* (ABI v15) sfx_cpe_residual_ln_pairs followed by the Block's qkv projection in one launch (eval, C in {64, 96, 128};
  * calflops.py:45-55): X_out = X + LN_cpe(T + pair partials); qkv [M][3C] = LN1(X_out) W^T + bias with
  * W = sfx_weight_split of the qkv weight [3C][C] (w_split, w_inv) -- the norm1 output never leaves the chip.
@@ -389,7 +396,9 @@ int sfx_subm_pair_pos(int n, long long num_pairs, const int* pair_out, const int
  * num_pairs). */
 size_t sfx_subm_pair_lists_workspace_bytes(int n);
 int sfx_subm_pair_lists(int n, const int* nbr, void* ws, size_t ws_bytes, int* pair_in, int* pair_out, int* pair_off,
-                        int* pair_pos, int with_centre, void* stream);
+                        int* pair_pos, int* pair_cpos, int with_centre, void* stream);
+/* pair_cpos (nullable, [n][32], 16-byte aligned): row i's present pair indices in ascending offset order, -1 after
+ * them, their count in element 31 -- the compacted form sfx_cpe_residual_ln_cpairs reads. */
 /* spconv SubMConv3d(Cin, Cout, 3, bias) forward on the pair lists: out = bias + x[nbr[:,13]] W_13^T (dense centre
  * GEMM, plain stores), then one fp32 MFMA launch over the 26 other offsets' gathered rows whose partial products
  * are atomically added into out (float atomics: summation order across offsets is not fixed).

@@ -184,7 +184,62 @@ __device__ __forceinline__ void add_pair_partials(float4 (&v)[NV], const float* 
   }
 }
 
-template <int G, int NV, bool PAIRS>
+// The same sum from the compacted positions (sfx_subm_pair_lists pair_cpos [n][32]: the row's present pairs in
+// ascending offset order, -1 after them, the count in element 31): the wave loops over ceil(max count / 8) groups of 8
+// positions (two 16-byte index loads, 8 NV row loads, out-of-range past the row's count) instead of 27 position
+// loads and 27 NV row loads of which ~90 % are out of range at 100k points; same order of additions.
+template <int G, int NV>
+__device__ __forceinline__ void add_pair_partials_c(float4 (&v)[NV], const float* __restrict__ P,
+                                                    const int* __restrict__ cpos, int row, int sub) {
+  constexpr int C = 4 * G * NV;
+  const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(P), (short)0, 0x7ffffff0,
+                                                                      0x00020000);
+  if constexpr (G == 64 && NV == 1) {  // one row per wave: scalar count and positions, loads for present pairs only
+    const int* cu = cpos + 32ll * __builtin_amdgcn_readfirstlane(row);
+    const int n = __builtin_amdgcn_readfirstlane(cu[31]);
+    for (int j0 = 0; j0 < n; j0 += 8) {
+      int q[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) q[u] = __builtin_amdgcn_readfirstlane(cu[j0 + u]);
+      float4 a[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const unsigned off = j0 + u < n ? ((unsigned)q[u] * (unsigned)C + 4u * (unsigned)sub) * 4u : 0x7ffffff0u;
+        a[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rp, off, 0, 0));
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[0] = make_float4(v[0].x + a[u].x, v[0].y + a[u].y, v[0].z + a[u].z, v[0].w + a[u].w);
+    }
+    return;
+  }
+  const int* cr = cpos + 32ll * row;
+  const int cnt = cr[31];
+  int jmax = cnt;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) jmax = max(jmax, __shfl_xor(jmax, o, 64));
+  jmax = __builtin_amdgcn_readfirstlane(jmax);
+  for (int j0 = 0; j0 < jmax; j0 += 8) {
+    const int4 qa = *reinterpret_cast<const int4*>(cr + j0), qb = *reinterpret_cast<const int4*>(cr + j0 + 4);
+    const int q[8] = {qa.x, qa.y, qa.z, qa.w, qb.x, qb.y, qb.z, qb.w};
+    float4 a[8][NV];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        const unsigned off =
+            j0 + u < cnt ? ((unsigned)q[u] * (unsigned)C + 4u * (unsigned)(sub + G * i)) * 4u : 0x7ffffff0u;
+        a[u][i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rp, off, 0, 0));
+      }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)  // (past the count: + 0, as the [n][27] form adds for absent offsets)
+#pragma unroll
+      for (int i = 0; i < NV; ++i)
+        v[i] = make_float4(v[i].x + a[u][i].x, v[i].y + a[u][i].y, v[i].z + a[u][i].z, v[i].w + a[u][i].w);
+  }
+}
+
+// PAIRS: 0 T is the conv output, 1 add the pair partials named by pair_pos [n][27], 2 by pair_cpos [n][32]
+template <int G, int NV, int PAIRS>
 __global__ void __launch_bounds__(256) cpe_residual_ln4_kernel(int M, const float* __restrict__ T, long long ldt,
                                                                const float* __restrict__ X,
                                                                const float* __restrict__ g_cpe,
@@ -205,7 +260,8 @@ __global__ void __launch_bounds__(256) cpe_residual_ln4_kernel(int M, const floa
     v[i] = *reinterpret_cast<const float4*>(T + (long long)row * ldt + 4 * (sub + G * i));
     x[i] = *reinterpret_cast<const float4*>(X + base + 4 * (sub + G * i));
   }
-  if constexpr (PAIRS) add_pair_partials<G, NV>(v, P, pos, row, sub);
+  if constexpr (PAIRS == 1) add_pair_partials<G, NV>(v, P, pos, row, sub);
+  if constexpr (PAIRS == 2) add_pair_partials_c<G, NV>(v, P, pos, row, sub);
   ln_row4<G, NV>(v, g_cpe, b_cpe, eps, sub, o);
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
@@ -416,7 +472,7 @@ int sfx_cpe_residual_ln(int M, int C, const float* T, const float* X, const floa
   const bool v4 = al16(T) && al16(X) && al16(X_out) && al16(H) && al16(gamma_cpe) && al16(beta_cpe) && al16(gamma1) &&
                   al16(beta1);
 #define SFX_CPE4(G, NV)                                                                                         \
-  cpe_residual_ln4_kernel<G, NV, false><<<sfx::ceil_div(M, 256 / G), 256, 0, st>>>(M, T, C, X, gamma_cpe, beta_cpe,\
+  cpe_residual_ln4_kernel<G, NV, 0><<<sfx::ceil_div(M, 256 / G), 256, 0, st>>>(M, T, C, X, gamma_cpe, beta_cpe,\
                                                                                    gamma1, beta1, eps, X_out, H,   \
                                                                                    nullptr, nullptr)
   if (v4 && C == 64) SFX_CPE4(16, 1);
@@ -451,7 +507,7 @@ int sfx_cpe_residual_ln_pairs(int M, int C, const float* T, long long ldt, const
               "sfx_cpe_residual_ln_pairs: needs 16-byte aligned rows and C in {64, 96, 128, 256, 512}");
   hipStream_t st = sfx::as_stream(stream);
 #define SFX_CPE4P(G, NV)                                                                                        \
-  cpe_residual_ln4_kernel<G, NV, true><<<sfx::ceil_div(M, 256 / G), 256, 0, st>>>(M, T, ldt, X, gamma_cpe, beta_cpe,\
+  cpe_residual_ln4_kernel<G, NV, 1><<<sfx::ceil_div(M, 256 / G), 256, 0, st>>>(M, T, ldt, X, gamma_cpe, beta_cpe,\
                                                                                   gamma1, beta1, eps, X_out, H,   \
                                                                                   partials, pair_pos)
   if (C == 64) SFX_CPE4P(16, 1);
@@ -461,6 +517,37 @@ int sfx_cpe_residual_ln_pairs(int M, int C, const float* T, long long ldt, const
   else SFX_CPE4P(64, 2);
 #undef SFX_CPE4P
   return sfx::check_launch("sfx_cpe_residual_ln_pairs");
+}
+
+// (ABI v16) sfx_cpe_residual_ln_pairs with the compacted positions of sfx_subm_pair_lists (pair_cpos [M][32]):
+// bit-identical results, fewer position and row loads
+int sfx_cpe_residual_ln_cpairs(int M, int C, const float* T, long long ldt, const float* partials,
+                               const int* pair_cpos, long long num_pairs, const float* X, const float* gamma_cpe,
+                               const float* beta_cpe, const float* gamma1, const float* beta1, float eps, float* X_out,
+                               float* H, void* stream) {
+  SFX_REQUIRE(ldt == 0 || ldt == C, "sfx_cpe_residual_ln_cpairs: ldt must be C or 0");
+  SFX_REQUIRE(M >= 0 && num_pairs >= 0, "sfx_cpe_residual_ln_cpairs: bad sizes");
+  if (M == 0) return SFX_OK;
+  SFX_REQUIRE(T && X && gamma_cpe && beta_cpe && gamma1 && beta1 && X_out && H && pair_cpos &&
+                  (num_pairs == 0 || partials),
+              "sfx_cpe_residual_ln_cpairs: null buffer");
+  SFX_REQUIRE(num_pairs * C * 4 + 64 < 0x7ffffff0ll, "sfx_cpe_residual_ln_cpairs: partials exceed 2 GiB");
+  const bool v4 = al16(T) && al16(X) && al16(X_out) && al16(H) && al16(gamma_cpe) && al16(beta_cpe) && al16(gamma1) &&
+                  al16(beta1) && (!partials || al16(partials)) && al16(pair_cpos);
+  SFX_REQUIRE(v4 && (C == 64 || C == 96 || C == 128 || C == 256 || C == 512),
+              "sfx_cpe_residual_ln_cpairs: needs 16-byte aligned rows and C in {64, 96, 128, 256, 512}");
+  hipStream_t st = sfx::as_stream(stream);
+#define SFX_CPE4C(G, NV)                                                                                        \
+  cpe_residual_ln4_kernel<G, NV, 2><<<sfx::ceil_div(M, 256 / G), 256, 0, st>>>(M, T, ldt, X, gamma_cpe, beta_cpe,   \
+                                                                               gamma1, beta1, eps, X_out, H,      \
+                                                                               partials, pair_cpos)
+  if (C == 64) SFX_CPE4C(16, 1);
+  else if (C == 96) SFX_CPE4C(8, 3);
+  else if (C == 128) SFX_CPE4C(32, 1);
+  else if (C == 256) SFX_CPE4C(64, 1);
+  else SFX_CPE4C(64, 2);
+#undef SFX_CPE4C
+  return sfx::check_launch("sfx_cpe_residual_ln_cpairs");
 }
 
 // (ABI v15) sfx_cpe_residual_ln_pairs + the qkv projection in one launch (eval, C in {64, 96, 128}): X_out = X +

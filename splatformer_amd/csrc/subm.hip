@@ -166,7 +166,8 @@ __global__ void __launch_bounds__(256) subm_pair_count_kernel(int n, const int* 
 __global__ void __launch_bounds__(256) subm_pair_write_kernel(int n, const int* __restrict__ nbr,
                                                               const int* __restrict__ first, int nb, int with_centre,
                                                               int* __restrict__ pair_in, int* __restrict__ pair_out,
-                                                              int* __restrict__ pair_off, int* __restrict__ pair_pos) {
+                                                              int* __restrict__ pair_off, int* __restrict__ pair_pos,
+                                                              int* __restrict__ pair_cpos) {
   __shared__ int wc[27][4];
   const int i = blockIdx.x * 256 + threadIdx.x, lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const bool in = i < n;
@@ -179,6 +180,7 @@ __global__ void __launch_bounds__(256) subm_pair_write_kernel(int n, const int* 
   }
   __syncthreads();
   if (blockIdx.x == 0 && threadIdx.x < 27) pair_off[threadIdx.x] = first[(long long)threadIdx.x * nb];
+  int pk[27], rank[27], cnt = 0;
 #pragma unroll
   for (int k = 0; k < 27; ++k) {
     int base = first[(long long)k * nb + blockIdx.x];
@@ -192,6 +194,22 @@ __global__ void __launch_bounds__(256) subm_pair_write_kernel(int n, const int* 
       pair_in[p] = row[k];
     }
     if (pair_pos && in) pair_pos[27ll * i + k] = fl ? p : -1;
+    pk[k] = fl ? p : -1;
+    rank[k] = cnt;
+    cnt += fl ? 1 : 0;
+  }
+  if (pair_cpos && in) {  // compacted: the present pairs in ascending offset order (selects, no register indexing)
+    int c[32];
+#pragma unroll
+    for (int q = 0; q < 31; ++q) c[q] = -1;
+#pragma unroll
+    for (int k = 0; k < 27; ++k)
+#pragma unroll
+      for (int q = 0; q <= k; ++q) c[q] = (pk[k] >= 0 && rank[k] == q) ? pk[k] : c[q];
+    c[31] = cnt;
+    int4* dst = reinterpret_cast<int4*>(pair_cpos + 32ll * i);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) dst[q] = make_int4(c[4 * q], c[4 * q + 1], c[4 * q + 2], c[4 * q + 3]);
   }
 }
 }  // namespace
@@ -262,7 +280,7 @@ size_t sfx_subm_pair_lists_workspace_bytes(int n) {
   return (size_t)(2 * e * sizeof(int) + 256) + sfx_scan_workspace_bytes(e);
 }
 int sfx_subm_pair_lists(int n, const int* nbr, void* ws, size_t ws_bytes, int* pair_in, int* pair_out, int* pair_off,
-                        int* pair_pos, int with_centre, void* stream) {
+                        int* pair_pos, int* pair_cpos, int with_centre, void* stream) {
   SFX_REQUIRE(n >= 0, "sfx_subm_pair_lists: n < 0");
   SFX_REQUIRE(ws_bytes >= sfx_subm_pair_lists_workspace_bytes(n), "sfx_subm_pair_lists: workspace too small");
   SFX_REQUIRE(pair_off, "sfx_subm_pair_lists: null pair_off");
@@ -281,7 +299,8 @@ int sfx_subm_pair_lists(int n, const int* nbr, void* ws, size_t ws_bytes, int* p
   subm_pair_count_kernel<<<nb, 256, 0, st>>>(n, nbr, counts, nb, with_centre);
   const int rc = sfx_scan_i32(e, counts, first, 0, scan_ws, sfx_scan_workspace_bytes(e), pair_off + 27, stream);
   if (rc) return rc;
-  subm_pair_write_kernel<<<nb, 256, 0, st>>>(n, nbr, first, nb, with_centre, pair_in, pair_out, pair_off, pair_pos);
+  subm_pair_write_kernel<<<nb, 256, 0, st>>>(n, nbr, first, nb, with_centre, pair_in, pair_out, pair_off, pair_pos,
+                                             pair_cpos);
   return sfx::check_launch("sfx_subm_pair_lists");
 }
 // pair_pos [n][27]: for output row i and offset k, the index of pair (k, i) in pair_in/pair_out (-1: no pair);

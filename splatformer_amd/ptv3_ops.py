@@ -50,7 +50,8 @@ _lib.register("sfx_subm_conv_partials", [I, I, I, P, L, P, P, P, P, P, P, P, L, 
 _lib.register("sfx_subm_conv_partials_pairs", [I, I, I, P, L, P, P, P, P, P, P, P, L, P, L, P, P, P])
 _lib.register("sfx_subm_pair_pos", [I, L, P, P, P, P])
 _lib.register("sfx_subm_pair_lists_workspace_bytes", [I], Z)
-_lib.register("sfx_subm_pair_lists", [I, P, P, Z, P, P, P, P, I, P])
+_lib.register("sfx_subm_pair_lists", [I, P, P, Z, P, P, P, P, P, I, P])
+_lib.register("sfx_cpe_residual_ln_cpairs", [I, I, P, L, P, P, L, P, P, P, P, P, F, P, P, P])
 _lib.register("sfx_subm_cpe_pack_bytes", [I], Z)
 _lib.register("sfx_subm_cpe_pack", [I, P, P, P, P, P])
 _lib.register("sfx_subm_cpe_ln", [I, I, P, P, P, P, P, P, P, P, P, P, P, P, F, P, P, P])
@@ -445,9 +446,14 @@ def cpe_residual_ln(t, x: Tensor, g_cpe: Tensor, b_cpe: Tensor, g1: Tensor, b1: 
     x_out = torch.empty_like(x) if x_out is None else x_out
     h = torch.empty_like(x)
     if isinstance(t, SubmPartials):
-        call("sfx_cpe_residual_ln_pairs", M, C, ptr(t.centre), t.ldt, ptr(t.partials), ptr(t.pair_pos), t.num_pairs,
-             ptr(x),
-             ptr(g_cpe), ptr(b_cpe), ptr(g1), ptr(b1), float(eps), ptr(x_out), ptr(h), stream())
+        # compacted positions (fewer position / row loads) except at C = 256, whose one-row-per-wave [n][27] kernel reads
+        # the positions with scalar loads and is HBM-bound either way (100.6 vs 102.2 us, profiles/r06_ab_ln_compact.txt)
+        if t.cpos is not None and C != 256:
+            call("sfx_cpe_residual_ln_cpairs", M, C, ptr(t.centre), t.ldt, ptr(t.partials), ptr(t.cpos), t.num_pairs,
+                 ptr(x), ptr(g_cpe), ptr(b_cpe), ptr(g1), ptr(b1), float(eps), ptr(x_out), ptr(h), stream())
+        else:
+            call("sfx_cpe_residual_ln_pairs", M, C, ptr(t.centre), t.ldt, ptr(t.partials), ptr(t.pair_pos),
+                 t.num_pairs, ptr(x), ptr(g_cpe), ptr(b_cpe), ptr(g1), ptr(b1), float(eps), ptr(x_out), ptr(h), stream())
     else:
         call("sfx_cpe_residual_ln", M, C, ptr(t), ptr(x), ptr(g_cpe), ptr(b_cpe), ptr(g1), ptr(b1), float(eps),
              ptr(x_out), ptr(h), stream())
@@ -748,6 +754,7 @@ def segment_mean(x: Tensor, idx_ptr: Tensor, sorted_idx: Tensor, m: int) -> Tens
 
 
 PAIR_LISTS = os.environ.get("SFX_PAIR_LISTS", "1") != "0"  # 0: the older flag / scan / fill pair builder
+LN_COMPACT = os.environ.get("SFX_LN_COMPACT", "1") != "0"  # 0: the pair-sum LayerNorm reads pair_pos [n][27]
 
 
 class PairLists:
@@ -766,11 +773,14 @@ class PairLists:
         if PAIR_LISTS:
             # lists and the inverted index pair_pos in one call (ABI v16: per-workgroup counts, no host value needed)
             self._pos = torch.empty(max(1, n), 27, device=dev, dtype=torch.int32)
+            # and the compacted positions the pair-sum LayerNorm reads (present pairs first, count in column 31)
+            self.cpos = torch.empty(max(1, n), 32, device=dev, dtype=torch.int32) if LN_COMPACT else None
             ws = _lib.workspace(_lib.fn("sfx_subm_pair_lists_workspace_bytes")(n), dev)
             call("sfx_subm_pair_lists", n, ptr(nbr), ptr(ws), ws.numel(), ptr(self.pair_in), ptr(self.pair_out),
-                 ptr(self.off_dev), ptr(self._pos), 1 if centre else 0, stream())
+                 ptr(self.off_dev), ptr(self._pos), ptr(self.cpos), 1 if centre else 0, stream())
         else:  # the v6 / v15 pair (flags over [27][n] + scan + fill; pair_pos on first use, after the offsets read)
             self._pos = None
+            self.cpos = None
             ws = _lib.workspace(_lib.fn("sfx_subm_pairs_workspace_bytes")(n), dev)
             call("sfx_subm_pairs", n, ptr(nbr), ptr(ws), ws.numel(), ptr(self.pair_in), ptr(self.pair_out),
                  ptr(self.off_dev), 1 if centre else 0, stream())
@@ -986,9 +996,11 @@ class SubmPartials:
     per (offset, output) pair), summed per output row by the consumer (cpe_residual_ln) or by `total()`.  ldt = 0:
     `centre` is the bias [Cout] alone and the centre offset's products are partial rows (pair lists with the centre)."""
 
-    def __init__(self, centre: Tensor, partials: Tensor, pair_pos: Tensor, num_pairs: int, ldt: Optional[int] = None):
+    def __init__(self, centre: Tensor, partials: Tensor, pair_pos: Tensor, num_pairs: int, ldt: Optional[int] = None,
+                 cpos: Optional[Tensor] = None):
         self.centre, self.partials, self.pair_pos, self.num_pairs = centre, partials, pair_pos, num_pairs
         self.ldt = centre.shape[-1] if ldt is None else ldt
+        self.cpos = cpos  # compacted positions (PairLists.cpos) or None
 
     def total(self) -> Tensor:
         """The conv output, summed in the consumer's order (ascending offsets after the centre / the bias)."""
@@ -1023,7 +1035,7 @@ def subm_conv(x: Tensor, smap: "SubmMap", weight: Tensor, bias: Optional[Tensor]
             call("sfx_subm_conv_partials_pairs", n, cin, cout, px, ldx, ptr(smap.nbr), ptr(weight), ptr(bias),
                  ptr(pl.pair_in), ptr(pl.pair_out), pl.off_host, po, ldo, ptr(part), cout, *wsp, stream())
             b = bias if bias is not None else torch.zeros(cout, device=x.device, dtype=torch.float32)
-            return SubmPartials(b.contiguous(), part, pl.pair_pos, npairs, ldt=0)
+            return SubmPartials(b.contiguous(), part, pl.pair_pos, npairs, ldt=0, cpos=pl.cpos)
         if SUBM_CENTRE_FIRST and not smap.pair_off_ready():  # centre GEMM first, then wait for the pair offsets
             call("sfx_subm_conv_partials", n, cin, cout, px, ldx, ptr(smap.nbr), ptr(weight), ptr(bias), None, None,
                  _ZERO_OFFS, po, ldo, None, cout, *wsp, stream())
@@ -1031,12 +1043,12 @@ def subm_conv(x: Tensor, smap: "SubmMap", weight: Tensor, bias: Optional[Tensor]
             part = torch.empty(max(1, npairs), cout, device=x.device, dtype=torch.float32)
             call("sfx_subm_conv_partials_pairs", n, cin, cout, px, ldx, ptr(smap.nbr), ptr(weight), ptr(bias),
                  ptr(smap.pair_in), ptr(smap.pair_out), smap._off_host, po, ldo, ptr(part), cout, *wsp, stream())
-            return SubmPartials(out, part, smap.pair_pos, npairs)
+            return SubmPartials(out, part, smap.pair_pos, npairs, cpos=smap.lists(False).cpos)
         npairs = smap.num_pairs
         part = torch.empty(max(1, npairs), cout, device=x.device, dtype=torch.float32)
         call("sfx_subm_conv_partials", n, cin, cout, px, ldx, ptr(smap.nbr), ptr(weight), ptr(bias),
              ptr(smap.pair_in), ptr(smap.pair_out), smap._off_host, po, ldo, ptr(part), cout, *wsp, stream())
-        return SubmPartials(out, part, smap.pair_pos, npairs)
+        return SubmPartials(out, part, smap.pair_pos, npairs, cpos=smap.lists(False).cpos)
     call("sfx_subm_conv", n, cin, cout, px, ldx, ptr(smap.nbr), ptr(weight), ptr(bias), ptr(smap.pair_in),
          ptr(smap.pair_out), smap._off_host, po, ldo, *_slot_args(x_amax), *_slot_args(w_amax),
          *weight_split(weight), stream())

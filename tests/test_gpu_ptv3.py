@@ -240,8 +240,9 @@ def test_subm_pair_lists_match_flag_scan(device, n, centre):
         pos = torch.empty(n, 27, device=device, dtype=torch.int32)
         if new:
             ws = _lib.workspace(_lib.fn("sfx_subm_pair_lists_workspace_bytes")(n), device)
+            cpos = torch.empty(n, 32, device=device, dtype=torch.int32)
             call("sfx_subm_pair_lists", n, ptr(nbr), ptr(ws), ws.numel(), ptr(pin), ptr(pout), ptr(off), ptr(pos),
-                 1 if centre else 0, stream())
+                 ptr(cpos), 1 if centre else 0, stream())
         else:
             ws = _lib.workspace(_lib.fn("sfx_subm_pairs_workspace_bytes")(n), device)
             call("sfx_subm_pairs", n, ptr(nbr), ptr(ws), ws.numel(), ptr(pin), ptr(pout), ptr(off),
@@ -251,6 +252,14 @@ def test_subm_pair_lists_match_flag_scan(device, n, centre):
         res.append((pin.cpu(), pout.cpu(), off.cpu(), pos.cpu()))
     for a, b in zip(*res):
         assert torch.equal(a, b)
+    # the compacted positions: each row's present pair indices in ascending offset order, -1 after, count in column 31
+    cp, pos = cpos.cpu(), res[1][3]
+    cnt = (pos >= 0).sum(1)
+    assert torch.equal(cp[:, 31], cnt.int())
+    for i in range(0, n, max(1, n // 97)):
+        want = pos[i][pos[i] >= 0]
+        c = int(cnt[i])
+        assert torch.equal(cp[i, :c], want) and bool((cp[i, c:31] == -1).all())
     off = res[1][2]
     assert int(off[27]) == int(((nbr >= 0).sum() - (0 if centre else (nbr[:, 13] >= 0).sum())).item())
 
@@ -293,6 +302,10 @@ def test_subm_conv_partials_atomic_free(device, centre, unique):
         xo, h = ops.cpe_residual_ln(sp, xd, *args)
         xo_u, h_u = ops.cpe_residual_ln(t, xd, *args)
         assert torch.equal(xo, xo_u) and torch.equal(h, h_u)
+        if sp.cpos is not None:  # the compacted-position LayerNorm equals the [n][27] one bit for bit
+            sp_k = ops.SubmPartials(sp.centre, sp.partials, sp.pair_pos, sp.num_pairs, ldt=sp.ldt)
+            xo_k, h_k = ops.cpe_residual_ln(sp_k, xd, *args)
+            assert torch.equal(xo, xo_k) and torch.equal(h, h_k)
         sp2 = ops.subm_conv(xd, smap, wd, bd, partials=True)
         xo2, h2 = ops.cpe_residual_ln(sp2, xd, *args)
         assert torch.equal(xo, xo2) and torch.equal(h, h2)
