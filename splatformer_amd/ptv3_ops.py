@@ -446,9 +446,9 @@ def cpe_residual_ln(t, x: Tensor, g_cpe: Tensor, b_cpe: Tensor, g1: Tensor, b1: 
     x_out = torch.empty_like(x) if x_out is None else x_out
     h = torch.empty_like(x)
     if isinstance(t, SubmPartials):
-        # compacted positions (fewer position / row loads) except at C = 256, whose one-row-per-wave [n][27] kernel reads
-        # the positions with scalar loads and is HBM-bound either way (100.6 vs 102.2 us, profiles/r06_ab_ln_compact.txt)
-        if t.cpos is not None and C != 256:
+        # compacted positions (fewer position / row loads; at C = 256 HBM-bound either way, 102.2 vs 100.6 us for the
+        # [n][27] kernel, whose index the lists then need not write: profiles/r06_ab_ln_compact.txt)
+        if t.cpos is not None:
             call("sfx_cpe_residual_ln_cpairs", M, C, ptr(t.centre), t.ldt, ptr(t.partials), ptr(t.cpos), t.num_pairs,
                  ptr(x), ptr(g_cpe), ptr(b_cpe), ptr(g1), ptr(b1), float(eps), ptr(x_out), ptr(h), stream())
         else:
@@ -772,9 +772,10 @@ class PairLists:
         self.off_dev = torch.empty(28, device=dev, dtype=torch.int32)
         if PAIR_LISTS:
             # lists and the inverted index pair_pos in one call (ABI v16: per-workgroup counts, no host value needed)
-            self._pos = torch.empty(max(1, n), 27, device=dev, dtype=torch.int32)
-            # and the compacted positions the pair-sum LayerNorm reads (present pairs first, count in column 31)
+            # with the compacted positions the pair-sum LayerNorm reads (present pairs first, count in column 31);
+            # then the [n][27] index is only built if asked for (pair_pos, e.g. SubmPartials.total())
             self.cpos = torch.empty(max(1, n), 32, device=dev, dtype=torch.int32) if LN_COMPACT else None
+            self._pos = None if LN_COMPACT else torch.empty(max(1, n), 27, device=dev, dtype=torch.int32)
             ws = _lib.workspace(_lib.fn("sfx_subm_pair_lists_workspace_bytes")(n), dev)
             call("sfx_subm_pair_lists", n, ptr(nbr), ptr(ws), ws.numel(), ptr(self.pair_in), ptr(self.pair_out),
                  ptr(self.off_dev), ptr(self._pos), ptr(self.cpos), 1 if centre else 0, stream())
@@ -996,11 +997,16 @@ class SubmPartials:
     per (offset, output) pair), summed per output row by the consumer (cpe_residual_ln) or by `total()`.  ldt = 0:
     `centre` is the bias [Cout] alone and the centre offset's products are partial rows (pair lists with the centre)."""
 
-    def __init__(self, centre: Tensor, partials: Tensor, pair_pos: Tensor, num_pairs: int, ldt: Optional[int] = None,
+    def __init__(self, centre: Tensor, partials: Tensor, pair_pos, num_pairs: int, ldt: Optional[int] = None,
                  cpos: Optional[Tensor] = None):
-        self.centre, self.partials, self.pair_pos, self.num_pairs = centre, partials, pair_pos, num_pairs
+        """pair_pos: the [n][27] index, or the PairLists that builds it on first use."""
+        self.centre, self.partials, self._pair_pos, self.num_pairs = centre, partials, pair_pos, num_pairs
         self.ldt = centre.shape[-1] if ldt is None else ldt
         self.cpos = cpos  # compacted positions (PairLists.cpos) or None
+
+    @property
+    def pair_pos(self) -> Tensor:
+        return self._pair_pos.pair_pos if isinstance(self._pair_pos, PairLists) else self._pair_pos
 
     def total(self) -> Tensor:
         """The conv output, summed in the consumer's order (ascending offsets after the centre / the bias)."""
@@ -1035,7 +1041,7 @@ def subm_conv(x: Tensor, smap: "SubmMap", weight: Tensor, bias: Optional[Tensor]
             call("sfx_subm_conv_partials_pairs", n, cin, cout, px, ldx, ptr(smap.nbr), ptr(weight), ptr(bias),
                  ptr(pl.pair_in), ptr(pl.pair_out), pl.off_host, po, ldo, ptr(part), cout, *wsp, stream())
             b = bias if bias is not None else torch.zeros(cout, device=x.device, dtype=torch.float32)
-            return SubmPartials(b.contiguous(), part, pl.pair_pos, npairs, ldt=0, cpos=pl.cpos)
+            return SubmPartials(b.contiguous(), part, pl, npairs, ldt=0, cpos=pl.cpos)
         if SUBM_CENTRE_FIRST and not smap.pair_off_ready():  # centre GEMM first, then wait for the pair offsets
             call("sfx_subm_conv_partials", n, cin, cout, px, ldx, ptr(smap.nbr), ptr(weight), ptr(bias), None, None,
                  _ZERO_OFFS, po, ldo, None, cout, *wsp, stream())
@@ -1043,12 +1049,12 @@ def subm_conv(x: Tensor, smap: "SubmMap", weight: Tensor, bias: Optional[Tensor]
             part = torch.empty(max(1, npairs), cout, device=x.device, dtype=torch.float32)
             call("sfx_subm_conv_partials_pairs", n, cin, cout, px, ldx, ptr(smap.nbr), ptr(weight), ptr(bias),
                  ptr(smap.pair_in), ptr(smap.pair_out), smap._off_host, po, ldo, ptr(part), cout, *wsp, stream())
-            return SubmPartials(out, part, smap.pair_pos, npairs, cpos=smap.lists(False).cpos)
+            return SubmPartials(out, part, smap.lists(False), npairs, cpos=smap.lists(False).cpos)
         npairs = smap.num_pairs
         part = torch.empty(max(1, npairs), cout, device=x.device, dtype=torch.float32)
         call("sfx_subm_conv_partials", n, cin, cout, px, ldx, ptr(smap.nbr), ptr(weight), ptr(bias),
              ptr(smap.pair_in), ptr(smap.pair_out), smap._off_host, po, ldo, ptr(part), cout, *wsp, stream())
-        return SubmPartials(out, part, smap.pair_pos, npairs, cpos=smap.lists(False).cpos)
+        return SubmPartials(out, part, smap.lists(False), npairs, cpos=smap.lists(False).cpos)
     call("sfx_subm_conv", n, cin, cout, px, ldx, ptr(smap.nbr), ptr(weight), ptr(bias), ptr(smap.pair_in),
          ptr(smap.pair_out), smap._off_host, po, ldo, *_slot_args(x_amax), *_slot_args(w_amax),
          *weight_split(weight), stream())
