@@ -18,7 +18,7 @@ pytestmark = pytest.mark.gpu
 
 
 def rel_l2(a, b):
-    a, b = a.double(), b.double()
+    a, b = a.detach().double(), b.detach().double()
     return float((a - b).norm() / b.norm().clamp_min(1e-30))
 
 
