@@ -372,14 +372,16 @@ int sfx_heads(int M, int ng, int kin, int out_dim, const float* x, long long ldx
   // one workgroup per CU: a launch of B point blocks takes ceil(B / CUs) rounds; splitting every block's heads into S
   // groups (grid.y) makes the rounds S times shorter, so the last, partly empty round costs 1/S of one (config B:
   // 391 blocks = 1.53 rounds -> 2 at S = 1, 5 / 3 at S = 3).  Each group re-reads and re-splits its input rows and
-  // stages the parameters again: S is the smallest that reaches the best rounds x (1 / S) + 2 % per extra group.
+  // stages the parameters again: S is the smallest that reaches the best rounds x (1 / S) + 7 % per extra group (the
+  // measured overhead: B 235 -> 223 us at S = 3; config E's 7.63 rounds ran 0.3 % faster per step unsplit than at S = 3,
+  // profiles/r06_ab_heads_split_E.txt).
   const int cus = num_cus();
   static const bool split_on = !(getenv("SFX_HEADS_SPLIT") && !strcmp(getenv("SFX_HEADS_SPLIT"), "0"));
   int S = 1;
   double best = 1e30;
   for (int s = 1; s <= (split_on ? ng : 1); ++s) {
     if (ng % s) continue;
-    const double cost = (double)sfx::ceil_div((long long)blocks * s, cus) / s * (1.0 + 0.02 * (s - 1));
+    const double cost = (double)sfx::ceil_div((long long)blocks * s, cus) / s * (1.0 + 0.07 * (s - 1));
     if (cost < best - 1e-9) {
       best = cost;
       S = s;
